@@ -1,0 +1,264 @@
+"""Python mirror of the reference crate's public interface for the hot path.
+
+Names follow the Rust crate (src/lib.rs:1-6):
+
+=========================================  ==========================================
+reference (file:line)                      here
+=========================================  ==========================================
+``sketch_sequence`` (sketch.rs:29)         :meth:`Device.sketch_sequences`
+``Index::{load_from_mmi,save_to_mmi}``     :meth:`Index.load_from_mmi`, :meth:`Index.save_to_mmi`
+``build_index_from_fasta`` (index.rs:427)  :meth:`Index.build_index_from_fasta`
+``Index::get`` (index.rs:143)              :meth:`Index.get`
+``Index::calc_mid_occ`` (index.rs:124)     :meth:`Index.calc_mid_occ`
+``Index::stats`` (index.rs:111)            :meth:`Index.stats`
+``build_anchors_filtered`` (seeds.rs:42)   :meth:`Device.map` + :meth:`Device.debug_anchors`
+``chain_dp_all`` (lchain.rs:59)            :meth:`Device.map` + :meth:`Device.debug_dp`
+``write_paf`` (paf.rs:224)                 :meth:`Device.paf`
+Align flow (main.rs:189-230)               :func:`align`
+=========================================  ==========================================
+
+All compute runs on the MI355X through libmm2g.so; errors are raised, never
+papered over with a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import MapOpts, ReadResult, check, load
+
+
+@dataclass
+class Minimizer:
+    key_span: int           # hash << 8 | span
+    rid_pos_strand: int     # rid << 32 | pos << 1 | strand
+
+
+def map_opts(**kw) -> MapOpts:
+    """``mm2rs align`` defaults (main.rs:105-123) with keyword overrides."""
+    o = MapOpts()
+    load().mm2g_map_opts_default(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+class Index:
+    """Host index (``Index``, src/index.rs:33-42)."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+
+    @classmethod
+    def build_index_from_fasta(cls, path: str, w: int = 10, k: int = 15, b: int = 14, flag: int = 0, threads: int = 8) -> "Index":
+        h = C.c_void_p()
+        check(load().mm2g_index_build_fasta(path.encode(), w, k, b, flag, threads, C.byref(h)), "build_index_from_fasta")
+        return cls(h.value)
+
+    @classmethod
+    def build_from_seqs(cls, names: Optional[Sequence[str]], seqs: Sequence[bytes], w: int = 10, k: int = 15, b: int = 14,
+                        flag: int = 0, threads: int = 8) -> "Index":
+        n = len(seqs)
+        bufs = [C.create_string_buffer(bytes(s), len(s)) for s in seqs]
+        ptrs = (C.c_void_p * max(n, 1))(*[C.cast(x, C.c_void_p).value for x in bufs])
+        lens = (C.c_uint64 * max(n, 1))(*[len(s) for s in seqs])
+        nm = None
+        if names is not None:
+            nm = (C.c_char_p * max(n, 1))(*[x.encode() for x in names])
+        h = C.c_void_p()
+        check(load().mm2g_index_build_seqs(n, nm, ptrs, lens, w, k, b, flag, threads, C.byref(h)), "build_from_seqs")
+        return cls(h.value)
+
+    @classmethod
+    def load_from_mmi(cls, path: str) -> "Index":
+        h = C.c_void_p()
+        check(load().mm2g_index_load_mmi(path.encode(), C.byref(h)), "load_from_mmi")
+        return cls(h.value)
+
+    def save_to_mmi(self, path: str) -> None:
+        check(load().mm2g_index_save_mmi(self._h, path.encode()), "save_to_mmi")
+
+    def close(self) -> None:
+        if self._h:
+            load().mm2g_index_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self) -> Tuple[int, float, float, int]:
+        a, d = C.c_uint64(), C.c_uint64()
+        b, c = C.c_double(), C.c_double()
+        check(load().mm2g_index_stats(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)), "stats")
+        return a.value, b.value, c.value, d.value
+
+    def calc_mid_occ(self, frac: float) -> int:
+        out = C.c_int32()
+        check(load().mm2g_index_calc_mid_occ(self._h, frac, C.byref(out)), "calc_mid_occ")
+        return out.value
+
+    @property
+    def params(self) -> Tuple[int, int, int, int, int]:
+        w, k, b, f = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+        n = C.c_uint32()
+        check(load().mm2g_index_params(self._h, C.byref(w), C.byref(k), C.byref(b), C.byref(f), C.byref(n)), "params")
+        return w.value, k.value, b.value, f.value, n.value
+
+    def seq(self, rid: int) -> Tuple[Optional[str], int]:
+        nm, ln = C.c_char_p(), C.c_uint32()
+        check(load().mm2g_index_seq(self._h, rid, C.byref(nm), C.byref(ln)), "seq")
+        return (nm.value.decode() if nm.value is not None else None), ln.value
+
+    def get(self, minier: int):
+        """``Index::get``: None, ('Single', pos) or ('Multi', [pos, ...])."""
+        kind = C.c_int()
+        n = load().mm2g_index_get(self._h, minier, C.byref(kind), None, 0)
+        if kind.value == 0:
+            return None
+        buf = (C.c_uint64 * max(n, 1))()
+        load().mm2g_index_get(self._h, minier, C.byref(kind), buf, n)
+        if kind.value == 1:
+            return ("Single", buf[0])
+        return ("Multi", list(buf[:n]))
+
+
+class Device:
+    """One MI355X context (stream + device index + batch workspaces)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(load().mm2g_ctx_create(device, C.byref(h)), "ctx_create")
+        self._h = h
+        self.index: Optional[Index] = None
+        self.n_reads = 0
+
+    def close(self) -> None:
+        if self._h:
+            load().mm2g_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload_index(self, index: Index, mid_occ: int) -> None:
+        check(load().mm2g_ctx_upload_index(self._h, index._h, mid_occ), "upload_index")
+        self.index = index
+
+    def set_reads(self, seqs: Sequence[bytes]) -> None:
+        offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
+        if seqs:
+            offs[1:] = np.cumsum([len(s) for s in seqs], dtype=np.uint64)
+        cat = b"".join(bytes(s) for s in seqs)
+        self.set_reads_packed(np.frombuffer(cat, dtype=np.uint8) if cat else np.zeros(1, np.uint8), offs)
+
+    def set_reads_packed(self, seq: np.ndarray, offs: np.ndarray) -> None:
+        seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        n = len(offs) - 1
+        check(load().mm2g_batch_set_reads(self._h, seq.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(L._P64), n), "set_reads")
+        self.n_reads = n
+
+    def sketch_sequences(self, seqs: Sequence[bytes], w: int, k: int, rid: int = 0) -> List[np.ndarray]:
+        """``sketch_sequence`` for each sequence; returns (m, 2) uint64 arrays of (key_span, rid_pos_strand)."""
+        self.set_reads(seqs)
+        n = len(seqs)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        check(load().mm2g_batch_sketch(self._h, w, k, rid, off.ctypes.data_as(L._P64), None, None, 0), "sketch")
+        tot = int(off[-1])
+        ks = np.zeros(max(tot, 1), dtype=np.uint64)
+        rps = np.zeros(max(tot, 1), dtype=np.uint64)
+        check(load().mm2g_batch_sketch(self._h, w, k, rid, off.ctypes.data_as(L._P64), ks.ctypes.data_as(L._P64),
+                                       rps.ctypes.data_as(L._P64), tot), "sketch")
+        return [np.stack([ks[off[i]:off[i + 1]], rps[off[i]:off[i + 1]]], axis=1) for i in range(n)]
+
+    def map(self, opts: Optional[MapOpts] = None) -> "C.Array[ReadResult]":
+        """Run the whole device pipeline on the resident batch and fetch per-read results."""
+        o = opts if opts is not None else map_opts()
+        check(load().mm2g_batch_map(self._h, C.byref(o)), "batch_map")
+        res = (ReadResult * max(self.n_reads, 1))()
+        check(load().mm2g_batch_results(self._h, res, self.n_reads), "batch_results")
+        return res
+
+    def map_async(self, opts: MapOpts) -> None:
+        check(load().mm2g_batch_map(self._h, C.byref(opts)), "batch_map")
+
+    def results(self, n: Optional[int] = None):
+        n = self.n_reads if n is None else n
+        res = (ReadResult * max(n, 1))()
+        check(load().mm2g_batch_results(self._h, res, n), "batch_results")
+        return res
+
+    def paf(self, names: Sequence[str], res) -> str:
+        n = len(names)
+        arr = (C.c_char_p * max(n, 1))(*[x.encode() for x in names])
+        need = check(load().mm2g_format_paf(self.index._h, res, arr, n, None, 0), "format_paf")
+        buf = C.create_string_buffer(need + 1)
+        got = check(load().mm2g_format_paf(self.index._h, res, arr, n, buf, need + 1), "format_paf")
+        return buf.raw[:got].decode()
+
+    def set_debug(self, on: bool) -> None:
+        check(load().mm2g_ctx_set_debug(self._h, 1 if on else 0), "set_debug")
+
+    def debug_anchors(self, r: int) -> np.ndarray:
+        n = check(load().mm2g_debug_anchors(self._h, r, None, 0), "debug_anchors")
+        out = np.zeros(2 * max(n, 1), dtype=np.uint64)
+        load().mm2g_debug_anchors(self._h, r, out.ctypes.data_as(L._P64), n)
+        return out[: 2 * n].reshape(n, 2)
+
+    def debug_dp(self, r: int) -> Tuple[np.ndarray, np.ndarray]:
+        n = check(load().mm2g_debug_dp(self._h, r, None, None, 0), "debug_dp")
+        f = np.zeros(max(n, 1), dtype=np.int32)
+        p = np.zeros(max(n, 1), dtype=np.int32)
+        load().mm2g_debug_dp(self._h, r, f.ctypes.data_as(L._PI32), p.ctypes.data_as(L._PI32), n)
+        return f[:n], p[:n]
+
+    def debug_keep(self, r: int) -> np.ndarray:
+        n = check(load().mm2g_debug_keep(self._h, r, None, 0), "debug_keep")
+        out = np.zeros(max(n, 1), dtype=np.uint8)
+        load().mm2g_debug_keep(self._h, r, out.ctypes.data_as(C.POINTER(C.c_uint8)), n)
+        return out[:n]
+
+    def prof_enable(self, on: bool = True) -> None:
+        check(load().mm2g_prof_enable(self._h, 1 if on else 0), "prof_enable")
+
+    def prof_reset(self) -> None:
+        check(load().mm2g_prof_reset(self._h), "prof_reset")
+
+    def prof(self) -> dict:
+        out = {}
+        i = 0
+        while True:
+            nm, ms, calls = C.c_char_p(), C.c_double(), C.c_int64()
+            if load().mm2g_prof_get(self._h, i, C.byref(nm), C.byref(ms), C.byref(calls)) != 0:
+                break
+            out[nm.value.decode()] = (ms.value, calls.value)
+            i += 1
+        return out
+
+    def counters(self) -> dict:
+        buf = (C.c_uint64 * 6)()
+        check(load().mm2g_batch_counters(self._h, buf), "counters")
+        keys = ["bases", "minimizers", "kept_minimizers", "anchors", "rescued_anchors", "dp_pairs"]
+        return dict(zip(keys, list(buf)))
+
+
+def align(index: Index, names: Sequence[str], seqs: Sequence[bytes], frac: float = 2e-4, device: int = 0,
+          opts: Optional[MapOpts] = None, dev: Optional[Device] = None) -> str:
+    """The Align flow (main.rs:189-230) applied to every read; returns PAF text."""
+    mid = max(index.calc_mid_occ(frac), 10)
+    d = dev or Device(device)
+    if d.index is not index:
+        d.upload_index(index, mid)
+    d.set_reads(seqs)
+    res = d.map(opts)
+    return d.paf(list(names), res)

@@ -1,0 +1,686 @@
+// Host orchestration of the MI355X path and the C ABI declared in
+// include/mm2g.h.  One mm2g_ctx = one device + one HIP stream + the device
+// index + batch workspaces sized for 288 GB of HBM3E (buffers grow on demand,
+// never shrink).  The batch pipeline is a fixed sequence of kernel launches
+// with two small device->host reads (minimizer overflow/table size, anchor
+// total) used to size the workspaces.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mm2g.h"
+#include "mm2g_index.h"
+#include "mm2g_internal.h"
+
+using namespace mm2g;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+static int set_err(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap; va_start(ap, fmt); vsnprintf(buf, sizeof buf, fmt, ap); va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return set_err(MM2G_E_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); } while (0)
+#define LCHK(x) do { int e_ = (x); if (e_ != 0) return set_err(MM2G_E_HIP, "kernel launch %s: %s", #x, hipGetErrorString((hipError_t)e_)); } while (0)
+
+struct mm2g_index { HostIndex h; };
+
+// ------------------------------------------------------------------ device buffers
+struct DevBuf {
+    void* p = nullptr; size_t cap = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+};
+template <typename T>
+static int ensure(DevBuf& b, size_t n, T** out) {
+    size_t need = std::max<size_t>(n, 1) * sizeof(T);
+    if (need > b.cap) {
+        if (b.p) { (void)hipFree(b.p); b.p = nullptr; b.cap = 0; }
+        size_t nc = need + need / 4;
+        if (hipMalloc(&b.p, nc) != hipSuccess) { b.p = nullptr; return set_err(MM2G_E_NOMEM, "hipMalloc(%zu bytes) failed", nc); }
+        b.cap = nc;
+    }
+    *out = (T*)b.p;
+    return 0;
+}
+#define ENSURE(buf, T, n, ptr) do { int e_ = ensure<T>(buf, (n), &(ptr)); if (e_) return e_; } while (0)
+
+struct ProfSlot { std::string name; double ms = 0; int64_t calls = 0; };
+
+struct mm2g_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // index
+    const HostIndex* hidx = nullptr;
+    DevBuf tab, ix_pos;
+    uint32_t log2cap = 0;
+    int32_t mid_occ = 10;
+    bool have_index = false;
+    // batch
+    uint32_t n_reads = 0;
+    uint64_t total_bases = 0;
+    uint32_t max_read_len = 0;
+    std::vector<uint64_t> h_rd_off;
+    DevBuf rd_seq, rd_off;
+    DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
+    DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
+    DevBuf tab_off, tab_key, tab_cnt;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag;
+    uint64_t* h_small = nullptr;          // pinned, 16 u64
+    ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
+    bool mapped = false, dv_separate = false;
+    uint64_t n_anchors = 0;
+    KeyLayout kl{};
+    mm2g_map_opts last_opts{};
+    std::vector<int16_t> h_lut; float lut_gap = -1; int lut_n = 0;
+    bool debug = false;
+    // profiling
+    bool prof = false;
+    std::vector<ProfSlot> slots;
+    std::map<std::string, int> slot_ix;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<hipEvent_t> ev_pool; size_t ev_next = 0;
+    uint64_t counters[6] = {0, 0, 0, 0, 0, 0};
+
+    hipEvent_t ev() {
+        if (ev_next == ev_pool.size()) { hipEvent_t e; (void)hipEventCreate(&e); ev_pool.push_back(e); }
+        return ev_pool[ev_next++];
+    }
+    int prof_begin(const char* name, hipEvent_t& e0) {
+        if (!prof) return -1;
+        auto it = slot_ix.find(name);
+        int i;
+        if (it == slot_ix.end()) { i = (int)slots.size(); slots.push_back(ProfSlot{name}); slot_ix[name] = i; } else i = it->second;
+        e0 = ev(); (void)hipEventRecord(e0, stream);
+        return i;
+    }
+    void prof_end(int i, hipEvent_t e0) {
+        if (i < 0) return;
+        hipEvent_t e1 = ev(); (void)hipEventRecord(e1, stream);
+        pending.push_back({i, {e0, e1}});
+    }
+    void prof_collect() {
+        if (pending.empty()) { ev_next = 0; return; }
+        (void)hipEventSynchronize(pending.back().second.second);
+        for (auto& p : pending) {
+            float ms = 0; (void)hipEventElapsedTime(&ms, p.second.first, p.second.second);
+            slots[p.first].ms += ms; slots[p.first].calls += 1;
+        }
+        pending.clear(); ev_next = 0;
+    }
+};
+
+struct ProfScope {
+    mm2g_ctx* c; int i; hipEvent_t e0{};
+    ProfScope(mm2g_ctx* c_, const char* n) : c(c_) { i = c->prof_begin(n, e0); }
+    ~ProfScope() { c->prof_end(i, e0); }
+};
+
+static inline uint32_t bit_width(uint64_t x) { uint32_t b = 0; while (x) { ++b; x >>= 1; } return b; }
+static inline int grid_for(uint32_t n) { int b = (int)((n + 3) / 4); return std::max(1, std::min(b, 4096)); }
+
+extern "C" {
+
+int mm2g_version(void) { return 1; }
+const char* mm2g_last_error(void) { return g_err.c_str(); }
+int mm2g_device_count(void) { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) return 0; return n; }
+
+// ------------------------------------------------------------------ index API
+int mm2g_index_build_fasta(const char* path, int w, int k, int b, int flag, int n_threads, mm2g_index** out) {
+    if (!path || !out) return set_err(MM2G_E_ARG, "null argument");
+    std::vector<FastaRecord> recs; std::string err;
+    if (!read_fasta(path, recs, false, err)) return set_err(MM2G_E_IO, "%s", err.c_str());
+    std::vector<const uint8_t*> seqs; std::vector<uint64_t> lens; std::vector<std::string> names;
+    for (auto& r : recs) { seqs.push_back((const uint8_t*)r.seq.data()); lens.push_back(r.seq.size()); names.push_back(r.name); }
+    std::unique_ptr<mm2g_index> I(new mm2g_index());
+    if (!build_index(seqs, lens, &names, w, k, b, flag, n_threads, I->h, err)) return set_err(MM2G_E_ARG, "%s", err.c_str());
+    *out = I.release();
+    return 0;
+}
+
+int mm2g_index_build_seqs(uint32_t n_seq, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens,
+                          int w, int k, int b, int flag, int n_threads, mm2g_index** out) {
+    if (!out || (n_seq && (!seqs || !lens))) return set_err(MM2G_E_ARG, "null argument");
+    std::vector<const uint8_t*> s(seqs, seqs + n_seq);
+    std::vector<uint64_t> l(lens, lens + n_seq);
+    std::vector<std::string> nm;
+    if (names) for (uint32_t i = 0; i < n_seq; ++i) nm.push_back(names[i] ? names[i] : "");
+    std::unique_ptr<mm2g_index> I(new mm2g_index());
+    std::string err;
+    if (!build_index(s, l, names ? &nm : nullptr, w, k, b, flag, n_threads, I->h, err)) return set_err(MM2G_E_ARG, "%s", err.c_str());
+    *out = I.release();
+    return 0;
+}
+
+int mm2g_index_load_mmi(const char* path, mm2g_index** out) {
+    if (!path || !out) return set_err(MM2G_E_ARG, "null argument");
+    std::unique_ptr<mm2g_index> I(new mm2g_index());
+    std::string err;
+    if (!load_mmi(path, I->h, err)) return set_err(MM2G_E_IO, "%s", err.c_str());
+    *out = I.release();
+    return 0;
+}
+int mm2g_index_save_mmi(const mm2g_index* idx, const char* path) {
+    if (!idx || !path) return set_err(MM2G_E_ARG, "null argument");
+    std::string err;
+    if (!save_mmi(idx->h, path, err)) return set_err(MM2G_E_IO, "%s", err.c_str());
+    return 0;
+}
+void mm2g_index_free(mm2g_index* idx) { delete idx; }
+int mm2g_index_stats(const mm2g_index* idx, uint64_t* n_keys, double* avg_occ, double* avg_spacing, uint64_t* total_len) {
+    if (!idx) return set_err(MM2G_E_ARG, "null index");
+    uint64_t a, d; double b, c;
+    idx->h.stats(a, b, c, d);
+    if (n_keys) *n_keys = a; if (avg_occ) *avg_occ = b; if (avg_spacing) *avg_spacing = c; if (total_len) *total_len = d;
+    return 0;
+}
+int mm2g_index_calc_mid_occ(const mm2g_index* idx, float frac, int32_t* out) {
+    if (!idx || !out) return set_err(MM2G_E_ARG, "null argument");
+    *out = idx->h.calc_mid_occ(frac);
+    return 0;
+}
+int mm2g_index_params(const mm2g_index* idx, int32_t* w, int32_t* k, int32_t* b, int32_t* flag, uint32_t* n_seq) {
+    if (!idx) return set_err(MM2G_E_ARG, "null index");
+    if (w) *w = idx->h.w; if (k) *k = idx->h.k; if (b) *b = idx->h.b; if (flag) *flag = idx->h.flag; if (n_seq) *n_seq = idx->h.n_seq;
+    return 0;
+}
+int mm2g_index_seq(const mm2g_index* idx, uint32_t rid, const char** name, uint32_t* len) {
+    if (!idx || rid >= idx->h.seq.size()) return set_err(MM2G_E_ARG, "rid out of range");
+    if (name) *name = idx->h.seq[rid].has_name ? idx->h.seq[rid].name.c_str() : nullptr;
+    if (len) *len = idx->h.seq[rid].len;
+    return 0;
+}
+int64_t mm2g_index_get(const mm2g_index* idx, uint64_t minier, int* kind, uint64_t* out, int64_t cap) {
+    if (!idx || !kind) return set_err(MM2G_E_ARG, "null argument");
+    const uint64_t* pos; size_t n; uint64_t single;
+    idx->h.get(minier, *kind, pos, n, single);
+    for (size_t i = 0; i < n && (int64_t)i < cap; ++i) out[i] = pos[i];
+    return (int64_t)n;
+}
+
+// ------------------------------------------------------------------ context
+int mm2g_ctx_create(int device, mm2g_ctx** out) {
+    if (!out) return set_err(MM2G_E_ARG, "null argument");
+    int nd = 0;
+    HIPCHK(hipGetDeviceCount(&nd));
+    if (device < 0 || device >= nd) return set_err(MM2G_E_ARG, "device %d out of range (%d devices)", device, nd);
+    HIPCHK(hipSetDevice(device));
+    std::unique_ptr<mm2g_ctx> c(new mm2g_ctx());
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipHostMalloc((void**)&c->h_small, 16 * sizeof(uint64_t), hipHostMallocDefault));
+    *out = c.release();
+    return 0;
+}
+void mm2g_ctx_destroy(mm2g_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->h_out) (void)hipHostFree(c->h_out);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
+    if (!c || !idx) return set_err(MM2G_E_ARG, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    const HostIndex& H = idx->h;
+    if (H.max_len >= (1u << 31)) return set_err(MM2G_E_UNSUP, "reference sequences must be shorter than 2^31");
+    std::vector<uint64_t> keys, pos; std::vector<uint32_t> offs, ns;
+    H.flatten(keys, offs, ns, pos);
+    if (pos.size() >= (1ULL << 32)) return set_err(MM2G_E_UNSUP, "more than 2^32 index positions");
+    const uint64_t nk = keys.size();
+    uint32_t l2 = 1;
+    while ((1ULL << l2) < 2 * std::max<uint64_t>(nk, 1)) ++l2;     // load factor <= 0.5
+    if (l2 > 31) return set_err(MM2G_E_UNSUP, "index too large for the device table");
+    IxEntry* tab; uint64_t* dpos;
+    ENSURE(c->tab, IxEntry, (size_t)1 << l2, tab);
+    ENSURE(c->ix_pos, uint64_t, pos.size(), dpos);
+    HIPCHK(hipMemsetAsync(tab, 0xff, sizeof(IxEntry) << l2, c->stream));
+    if (!pos.empty()) HIPCHK(hipMemcpyAsync(dpos, pos.data(), pos.size() * 8, hipMemcpyHostToDevice, c->stream));
+    DevBuf dk, doff, dn;
+    uint64_t* k_; uint32_t* o_; uint32_t* n_;
+    ENSURE(dk, uint64_t, nk, k_); ENSURE(doff, uint32_t, nk, o_); ENSURE(dn, uint32_t, nk, n_);
+    if (nk) {
+        HIPCHK(hipMemcpyAsync(k_, keys.data(), nk * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(o_, offs.data(), nk * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(n_, ns.data(), nk * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    LCHK(launch_ix_build(k_, o_, n_, nk, tab, l2, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->log2cap = l2;
+    c->hidx = &H;
+    c->mid_occ = mid_occ;
+    c->have_index = true;
+    return 0;
+}
+
+// ------------------------------------------------------------------ batch
+void mm2g_map_opts_default(mm2g_map_opts* o) {
+    o->w = 10; o->k = 15; o->max_gap = 5000; o->bw = 500; o->bw_long = 20000;
+    o->min_cnt = 3; o->min_chain_score = 40; o->mask_level = 0.5f; o->pri_ratio = 0.8f; o->best_n = 5;
+}
+
+int mm2g_batch_set_reads(mm2g_ctx* c, const uint8_t* seq, const uint64_t* offs, uint32_t n_reads) {
+    if (!c || (n_reads && (!seq || !offs))) return set_err(MM2G_E_ARG, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    uint64_t total = n_reads ? offs[n_reads] - offs[0] : 0;
+    c->h_rd_off.assign(n_reads + 1, 0);
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < n_reads; ++i) {
+        if (offs[i + 1] < offs[i]) return set_err(MM2G_E_ARG, "offsets must be non-decreasing");
+        uint64_t L = offs[i + 1] - offs[i];
+        if (L >= (1ULL << 31)) return set_err(MM2G_E_UNSUP, "reads must be shorter than 2^31");
+        mx = std::max<uint32_t>(mx, (uint32_t)L);
+        c->h_rd_off[i + 1] = offs[i + 1] - offs[0];
+    }
+    uint8_t* dseq; uint64_t* doff;
+    ENSURE(c->rd_seq, uint8_t, total + 64, dseq);
+    ENSURE(c->rd_off, uint64_t, n_reads + 1, doff);
+    if (total) HIPCHK(hipMemcpyAsync(dseq, seq + offs[0], total, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(doff, c->h_rd_off.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->n_reads = n_reads; c->total_bases = total; c->max_read_len = mx;
+    c->mapped = false;
+    return 0;
+}
+
+// Sketch the resident batch into (base, end, x, y, cnt); exact two-pass fallback
+// when a sequence overflows its L+16 slot.
+static int run_sketch(mm2g_ctx* c, int w, int k, DevBuf& b_base, DevBuf& b_end, DevBuf& b_x, DevBuf& b_y, DevBuf& b_cnt, uint64_t* total_out) {
+    const uint32_t n = c->n_reads;
+    uint64_t *base, *end, *x; uint32_t *y, *cnt; int32_t* ovf;
+    ENSURE(b_base, uint64_t, n + 1, base); ENSURE(b_end, uint64_t, n + 1, end);
+    ENSURE(b_cnt, uint32_t, n + 1, cnt);
+    ENSURE(c->flag, int32_t, 4, ovf);
+    const uint64_t cap = c->total_bases + 16ull * n + 16;
+    ENSURE(b_x, uint64_t, cap, x); ENSURE(b_y, uint32_t, cap, y);
+    {
+        ProfScope ps(c, "mz_base");
+        LCHK(launch_mz_base(n, (const uint64_t*)c->rd_off.p, base, end, c->stream));
+    }
+    HIPCHK(hipMemsetAsync(ovf, 0, 16, c->stream));
+    SketchArgs a{(const uint8_t*)c->rd_seq.p, (const uint64_t*)c->rd_off.p, n, w, k, base, end, x, y, cnt, ovf};
+    {
+        ProfScope ps(c, "sketch");
+        LCHK(launch_sketch(a, grid_for(n), c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(c->h_small, ovf, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int32_t over = (int32_t)(c->h_small[0] & 0xffffffffu);
+    if (over) {
+        std::vector<uint32_t> hc(n);
+        HIPCHK(hipMemcpy(hc.data(), cnt, n * 4, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> hb(n + 1), he(n + 1);
+        uint64_t run = 0;
+        for (uint32_t i = 0; i < n; ++i) { hb[i] = run; run += hc[i]; he[i] = run; }
+        ENSURE(b_x, uint64_t, run + 1, x); ENSURE(b_y, uint32_t, run + 1, y);
+        HIPCHK(hipMemcpy(base, hb.data(), n * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(end, he.data(), n * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemsetAsync(ovf, 0, 16, c->stream));
+        SketchArgs b2{(const uint8_t*)c->rd_seq.p, (const uint64_t*)c->rd_off.p, n, w, k, base, end, x, y, cnt, ovf};
+        LCHK(launch_sketch(b2, grid_for(n), c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    if (total_out) *total_out = cap;
+    return 0;
+}
+
+static void build_lut(mm2g_ctx* c, int k, int n) {
+    // comput_sc penalty (src/lchain.rs:28-31) for chn_pen_skip == 0 (main.rs:116):
+    // (gap*dd + 0*dg + 0.5*log2(dd+1)) as i32, f32 op by op, glibc logf.
+    const float gap = 0.01f * 0.8f * (float)k;
+    if (gap == c->lut_gap && n <= c->lut_n) return;
+    c->h_lut.assign(n, 0);
+    for (int dd = 0; dd < n; ++dd) {
+        const float lin = gap * (float)dd + 0.0f * 1.0f;
+        float lg = 0.0f;
+        if (dd >= 1) { const int x = dd + 1; lg = x <= 1 ? 0.0f : logf((float)x) / 0.693147180559945309417232121458176568f; }
+        const float v = lin + 0.5f * lg;
+        c->h_lut[dd] = (int16_t)(int32_t)v;
+    }
+    c->lut_gap = gap; c->lut_n = n;
+}
+
+int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
+    if (!c || !o) return set_err(MM2G_E_ARG, "null argument");
+    if (!c->have_index) return set_err(MM2G_E_STATE, "no index uploaded");
+    if (!(o->w > 0 && o->w < 256 && o->k > 0 && o->k <= 28)) return set_err(MM2G_E_ARG, "invalid w/k (0 < w < 256, 0 < k <= 28)");
+    if (o->min_cnt < 2) return set_err(MM2G_E_UNSUP, "-n < 2 is outside the supported parity envelope (DESIGN.md Q4)");
+    if (o->bw < 0 || o->bw_long < 0) return set_err(MM2G_E_ARG, "negative bandwidth");
+    const int32_t mdx0 = std::max(o->max_gap, o->bw), mdx1 = std::max(o->max_gap, o->bw_long);
+    const int lut_need = std::max(o->bw, o->bw_long) + 1;
+    if (lut_need > 60000) return set_err(MM2G_E_UNSUP, "bandwidth > 59999 not supported");
+    HIPCHK(hipSetDevice(c->device));
+    const HostIndex& H = *c->hidx;
+    const uint32_t n = c->n_reads;
+    c->mapped = false;
+    c->last_opts = *o;
+    // key layout
+    KeyLayout kl;
+    kl.n_seq = H.n_seq;
+    kl.qb = std::max<uint32_t>(1, bit_width(c->max_read_len));
+    kl.rb = std::max<uint32_t>(1, bit_width(H.max_len));
+    kl.gb = std::max<uint32_t>(1, bit_width(2ull * H.n_seq));
+    if (kl.qb + kl.rb + kl.gb > 64) return set_err(MM2G_E_UNSUP, "anchor key needs %u bits (> 64)", kl.qb + kl.rb + kl.gb);
+    c->kl = kl;
+    ReadOut* out;
+    ENSURE(c->outb, ReadOut, n + 1, out);
+    HIPCHK(hipMemsetAsync(out, 0, sizeof(ReadOut) * (n + 1), c->stream));
+    if (n == 0) { c->mapped = true; c->n_anchors = 0; return 0; }
+    // 1. sketch (CLI w/k, rid 0: seeds.rs:7-11)
+    int e = run_sketch(c, o->w, o->k, c->mz_base, c->mz_end, c->mz_x, c->mz_y, c->mz_cnt, nullptr);
+    if (e) return e;
+    const uint64_t mcap = c->mz_x.cap / 8;
+    uint64_t* mz_base = (uint64_t*)c->mz_base.p; uint32_t* mz_cnt = (uint32_t*)c->mz_cnt.p;
+    // 2. query filter (seeds.rs:13-36; (10, 0.01) hard-wired at main.rs:195)
+    uint64_t* tab_off; uint8_t* keep;
+    ENSURE(c->tab_off, uint64_t, n + 1, tab_off);
+    ENSURE(c->keep, uint8_t, mcap, keep);
+    {
+        ProfScope ps(c, "scan");
+        LCHK(launch_excl_scan(mz_cnt, n, tab_off, 1, 10, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(c->h_small, tab_off + n, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint64_t tab_total = c->h_small[0];
+    uint64_t* tkey; uint32_t* tcnt;
+    ENSURE(c->tab_key, uint64_t, tab_total, tkey);
+    ENSURE(c->tab_cnt, uint32_t, tab_total, tcnt);
+    {
+        FilterArgs fa{n, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, tab_off, tkey, tcnt, keep, 10, 0.01f};
+        ProfScope ps(c, "filter");
+        LCHK(launch_filter(fa, grid_for(n), c->stream));
+    }
+    // 3. lookup + anchor count (index.rs:143-154, seeds.rs:42-57)
+    uint32_t *mz_n, *mz_poff, *a_cnt; uint64_t* a_off;
+    ENSURE(c->mz_n, uint32_t, mcap, mz_n); ENSURE(c->mz_poff, uint32_t, mcap, mz_poff);
+    ENSURE(c->a_cnt, uint32_t, n + 1, a_cnt); ENSURE(c->a_off, uint64_t, n + 1, a_off);
+    SeedArgs sa{n, (const uint64_t*)c->rd_off.p, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, (const uint32_t*)c->mz_y.p, keep,
+                (const IxEntry*)c->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k};
+    {
+        ProfScope ps(c, "seed_count");
+        LCHK(launch_seed_count(sa, grid_for(n), c->stream));
+    }
+    {
+        ProfScope ps(c, "scan");
+        LCHK(launch_excl_scan(a_cnt, n, a_off, 0, 0, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(c->h_small, a_off + n, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint64_t A = c->h_small[0];
+    c->n_anchors = A;
+    uint64_t *keys, *ktmp; int32_t *fb, *pb;
+    ENSURE(c->keys, uint64_t, A, keys); ENSURE(c->keys_tmp, uint64_t, A, ktmp);
+    ENSURE(c->fbuf, int32_t, A, fb); ENSURE(c->ppbuf, int32_t, A, pb);
+    sa.keys = keys;
+    {
+        ProfScope ps(c, "seed_write");
+        LCHK(launch_seed_write(sa, grid_for(n), c->stream));
+    }
+    // 4. anchor sort (seeds.rs:58)
+    {
+        ProfScope ps(c, "sort");
+        LCHK(launch_sort(n, a_off, keys, ktmp, c->stream));
+    }
+    // 5. chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
+    build_lut(c, o->k, lut_need);
+    int16_t* lut; uint32_t* work;
+    ENSURE(c->lut, int16_t, c->h_lut.size(), lut);
+    ENSURE(c->work, uint32_t, 4, work);
+    HIPCHK(hipMemcpyAsync(lut, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));
+    ChainKParams P{};
+    P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
+    P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
+    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work};
+    const int chain_blocks = std::max(1, std::min((int)((n + 3) / 4), 2048));
+    {
+        ProfScope ps(c, "chain_dp");
+        LCHK(launch_chain(ca, chain_blocks, c->stream));
+    }
+    ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
+    ca.P.lut_n = o->bw_long + 1; ca.work = work + 1;
+    {
+        ProfScope ps(c, "chain_dp_rescue");
+        LCHK(launch_chain(ca, chain_blocks, c->stream));
+    }
+    // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
+    const bool sep = (H.w != o->w || H.k != o->k);
+    c->dv_separate = sep;
+    if (sep) {
+        if (!(H.w > 0 && H.w < 256 && H.k > 0 && H.k <= 28)) return set_err(MM2G_E_ARG, "index w/k invalid for the dv sketch");
+        e = run_sketch(c, H.w, H.k, c->mz2_base, c->mz2_end, c->mz2_x, c->mz2_y, c->mz2_cnt, nullptr);
+        if (e) return e;
+    }
+    DvArgs da{n, a_off, keys, (const uint32_t*)ktmp, sep ? (const uint64_t*)c->mz2_base.p : mz_base,
+              sep ? (const uint32_t*)c->mz2_cnt.p : mz_cnt, sep ? (const uint32_t*)c->mz2_y.p : (const uint32_t*)c->mz_y.p, kl, o->k, out};
+    {
+        ProfScope ps(c, "dv");
+        LCHK(launch_dv(da, c->stream));
+    }
+    c->mapped = true;
+    return 0;
+}
+
+int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
+    if (!c) return set_err(MM2G_E_ARG, "null context");
+    if (!c->mapped) return set_err(MM2G_E_STATE, "batch not mapped");
+    if (n > c->n_reads) return set_err(MM2G_E_ARG, "n exceeds the batch size");
+    HIPCHK(hipSetDevice(c->device));
+    if (c->h_out_cap < c->n_reads + 1) {
+        if (c->h_out) (void)hipHostFree(c->h_out);
+        c->h_out_cap = c->n_reads + 1;
+        HIPCHK(hipHostMalloc((void**)&c->h_out, c->h_out_cap * sizeof(ReadOut), hipHostMallocDefault));
+    }
+    if (c->n_reads) HIPCHK(hipMemcpyAsync(c->h_out, c->outb.p, c->n_reads * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof_collect();
+    const HostIndex& H = *c->hidx;
+    const int kdv = c->dv_separate ? H.k : c->last_opts.k;
+    uint64_t cnt[6] = {c->total_bases, 0, 0, c->n_anchors, 0, 0};
+    for (uint32_t i = 0; i < c->n_reads; ++i) {
+        const ReadOut& o = c->h_out[i];
+        cnt[4] += (o.flags & RF_RESCUED) ? (uint64_t)o.n_anchors : 0;
+        cnt[5] += o.dp_pairs;
+        if (i >= n || !res) continue;
+        mm2g_read_result& r = res[i];
+        memset(&r, 0, sizeof r);
+        const uint64_t L = c->h_rd_off[i + 1] - c->h_rd_off[i];
+        r.qlen = (int32_t)L;
+        if (L == 0) { r.flags = MM2G_R_EMPTY; continue; }
+        r.n_anchors = o.n_anchors;
+        if (!(o.flags & RF_MAPPED)) continue;
+        r.flags = MM2G_R_MAPPED | ((o.flags & RF_RESCUED) ? MM2G_R_RESCUED : 0) | ((o.flags & RF_DV_FOUND) ? MM2G_R_DV_FOUND : 0) |
+                  ((o.flags & RF_PANIC) ? MM2G_R_PANIC : 0);
+        r.score = o.score; r.cm = o.cm; r.qs = o.qs; r.qe = o.qe; r.ts = o.ts; r.te = o.te;
+        const uint32_t g = (uint32_t)o.group;
+        if (g == 2u * H.n_seq) { r.rid = 0x7fffffff; r.rev = 1; }
+        else if (g >= H.n_seq) { r.rid = (int32_t)(g - H.n_seq); r.rev = 1; }
+        else { r.rid = (int32_t)g; r.rev = 0; }
+        r.n_match = o.n_match; r.dv_st = o.dv_st; r.dv_en = o.dv_en; r.m_dv = o.m_dv;
+        r.sum_k = (int64_t)o.m_dv * kdv;      // query spans are all k (non-HPC)
+        // dv (paf.rs:189-199): f32 op by op, glibc powf
+        r.dv = 0.0f;
+        if ((o.flags & RF_DV_FOUND) && !(o.flags & RF_PANIC)) {
+            const float avg_k = r.m_dv ? (float)(uint64_t)r.sum_k / (float)(uint64_t)r.m_dv : (float)H.k;
+            int32_t n_tot = o.dv_en - o.dv_st + 1;
+            const int32_t qlen = r.qlen;
+            const int32_t rqs = r.rev ? qlen - r.qe : r.qs, rqe = r.rev ? qlen - r.qs : r.qe;
+            const int32_t ak = (int32_t)avg_k;
+            const int32_t tlen = (int32_t)H.seq[r.rid].len;
+            if (rqs > ak && r.ts > ak) n_tot += 1;
+            if (qlen - rqe > ak && tlen - r.te > ak) n_tot += 1;
+            const float frac = (float)r.n_match / (float)n_tot;
+            r.dv = frac >= 1.0f ? 0.0f : 1.0f - powf(frac, 1.0f / fmaxf(avg_k, 1.0f));
+        }
+    }
+    // minimizer counters
+    {
+        std::vector<uint32_t> mc(c->n_reads);
+        HIPCHK(hipMemcpy(mc.data(), c->mz_cnt.p, c->n_reads * 4, hipMemcpyDeviceToHost));
+        for (auto v : mc) cnt[1] += v;
+    }
+    for (int t = 0; t < 6; ++t) c->counters[t] = cnt[t];
+    return 0;
+}
+
+static inline char* put_u(char* p, uint64_t v) {
+    char tmp[24]; int n = 0;
+    do { tmp[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    while (n) *p++ = tmp[--n];
+    return p;
+}
+
+int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, const char* const* names, uint32_t n, char* out, int64_t cap) {
+    if (!idx || (n && (!res || !names))) return set_err(MM2G_E_ARG, "null argument");
+    const HostIndex& H = idx->h;
+    int64_t o = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const mm2g_read_result& r = res[i];
+        if (!(r.flags & MM2G_R_MAPPED) || (r.flags & MM2G_R_PANIC)) continue;
+        const HostSeq& s = H.seq[r.rid];
+        const char* tname = s.has_name ? s.name.c_str() : "*";
+        const size_t qn = strlen(names[i]), tn = strlen(tname);
+        if (out && o + (int64_t)(qn + tn + 256) > cap) return set_err(MM2G_E_NOMEM, "PAF output buffer too small");
+        char line[512];
+        char* p = line;
+        const uint32_t qlen = (uint32_t)r.qlen, qs = (uint32_t)r.qs, qe = (uint32_t)r.qe;
+        const uint32_t pqs = r.rev ? qlen - qe : qs, pqe = r.rev ? qlen - qs : qe;   // write_paf (paf.rs:225-227)
+        *p++ = '\t'; p = put_u(p, qlen); *p++ = '\t'; p = put_u(p, pqs); *p++ = '\t'; p = put_u(p, pqe);
+        *p++ = '\t'; *p++ = r.rev ? '-' : '+'; *p++ = '\t';
+        char* q = line + 256;
+        *q++ = '\t'; q = put_u(q, s.len); *q++ = '\t'; q = put_u(q, (uint32_t)r.ts); *q++ = '\t'; q = put_u(q, (uint32_t)r.te);
+        *q++ = '\t'; q = put_u(q, (uint32_t)std::max(r.qe - r.qs, 0)); *q++ = '\t'; q = put_u(q, (uint32_t)std::max(r.te - r.ts, 0));
+        memcpy(q, "\t60\ttp:A:P\tcm:i:", 16); q += 16; q = put_u(q, (uint32_t)r.cm);
+        memcpy(q, "\ts1:i:", 6); q += 6; q = put_u(q, (uint32_t)std::max(r.score, 0));
+        memcpy(q, "\ts2:i:0\tdv:f:", 12); q += 12;
+        q += snprintf(q, 32, "%.4f", (double)r.dv);
+        memcpy(q, "\trl:i:0\n", 8); q += 8;
+        const int64_t len = (int64_t)qn + (p - line) + (int64_t)tn + (q - (line + 256));
+        if (out) {
+            memcpy(out + o, names[i], qn); o += (int64_t)qn;
+            memcpy(out + o, line, (size_t)(p - line)); o += p - line;
+            memcpy(out + o, tname, tn); o += (int64_t)tn;
+            memcpy(out + o, line + 256, (size_t)(q - (line + 256))); o += q - (line + 256);
+        } else o += len;
+    }
+    return o;
+}
+
+// ------------------------------------------------------------------ stages
+int mm2g_batch_sketch(mm2g_ctx* c, int w, int k, uint32_t rid, uint64_t* out_off, uint64_t* out_ks, uint64_t* out_rps, uint64_t cap) {
+    if (!c) return set_err(MM2G_E_ARG, "null context");
+    if (!(w > 0 && w < 256 && k > 0 && k <= 28)) return set_err(MM2G_E_ARG, "invalid w/k (0 < w < 256, 0 < k <= 28)");
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t n = c->n_reads;
+    for (uint32_t i = 0; i < n; ++i)
+        if (c->h_rd_off[i + 1] == c->h_rd_off[i]) return set_err(MM2G_E_ARG, "empty sequence (src/sketch.rs:40)");
+    int e = run_sketch(c, w, k, c->mz2_base, c->mz2_end, c->mz2_x, c->mz2_y, c->mz2_cnt, nullptr);
+    if (e) return e;
+    std::vector<uint32_t> hc(n); std::vector<uint64_t> hb(n);
+    if (n) {
+        HIPCHK(hipMemcpy(hc.data(), c->mz2_cnt.p, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(hb.data(), c->mz2_base.p, n * 8, hipMemcpyDeviceToHost));
+    }
+    uint64_t run = 0;
+    for (uint32_t i = 0; i < n; ++i) { if (out_off) out_off[i] = run; run += hc[i]; }
+    if (out_off) out_off[n] = run;
+    if (!out_ks && !out_rps) return 0;
+    if (run > cap) return set_err(MM2G_E_ARG, "output capacity too small");
+    std::vector<uint64_t> x; std::vector<uint32_t> y;
+    for (uint32_t i = 0; i < n; ++i) {
+        x.resize(hc[i]); y.resize(hc[i]);
+        if (hc[i]) {
+            HIPCHK(hipMemcpy(x.data(), (uint64_t*)c->mz2_x.p + hb[i], hc[i] * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(y.data(), (uint32_t*)c->mz2_y.p + hb[i], hc[i] * 4, hipMemcpyDeviceToHost));
+        }
+        const uint64_t o0 = out_off ? out_off[i] : 0;
+        for (uint32_t t = 0; t < hc[i]; ++t) {
+            if (out_ks) out_ks[o0 + t] = x[t];
+            if (out_rps) out_rps[o0 + t] = ((uint64_t)rid << 32) | y[t];
+        }
+    }
+    return 0;
+}
+
+int mm2g_ctx_set_debug(mm2g_ctx* c, int on) { if (!c) return set_err(MM2G_E_ARG, "null context"); c->debug = on != 0; return 0; }
+
+// Unpack the sorted keys of read r back into the reference's (x, y).
+int64_t mm2g_debug_anchors(mm2g_ctx* c, uint32_t r, uint64_t* xy, int64_t cap) {
+    if (!c || !c->mapped || r >= c->n_reads) return set_err(MM2G_E_STATE, "no mapped batch / bad read index");
+    HIPCHK(hipSetDevice(c->device));
+    uint64_t off[2];
+    HIPCHK(hipMemcpy(off, (uint64_t*)c->a_off.p + r, 16, hipMemcpyDeviceToHost));
+    const int64_t A = (int64_t)(off[1] - off[0]);
+    if (!xy) return A;
+    std::vector<uint64_t> k((size_t)A);
+    if (A) HIPCHK(hipMemcpy(k.data(), (uint64_t*)c->keys.p + off[0], A * 8, hipMemcpyDeviceToHost));
+    const KeyLayout& kl = c->kl;
+    const uint64_t qm = (1ULL << kl.qb) - 1, rm = (1ULL << kl.rb) - 1;
+    const uint64_t span = (uint64_t)c->last_opts.k;
+    for (int64_t i = 0; i < A && i < cap; ++i) {
+        const uint64_t g = k[i] >> (kl.rb + kl.qb), p = (k[i] >> kl.qb) & rm, q = k[i] & qm;
+        uint64_t x;
+        if (g == 2ull * kl.n_seq) x = 0xffffffff80000000ULL | p;
+        else if (g >= kl.n_seq) x = (1ULL << 63) | ((g - kl.n_seq) << 32) | p;
+        else x = (g << 32) | p;
+        xy[2 * i] = x; xy[2 * i + 1] = (span << 32) | q;
+    }
+    return A;
+}
+int64_t mm2g_debug_dp(mm2g_ctx* c, uint32_t r, int32_t* f, int32_t* pprev, int64_t cap) {
+    if (!c || !c->mapped || r >= c->n_reads) return set_err(MM2G_E_STATE, "no mapped batch / bad read index");
+    HIPCHK(hipSetDevice(c->device));
+    uint64_t off[2];
+    HIPCHK(hipMemcpy(off, (uint64_t*)c->a_off.p + r, 16, hipMemcpyDeviceToHost));
+    const int64_t A = (int64_t)(off[1] - off[0]);
+    const int64_t m = std::min<int64_t>(A, cap);
+    if (f && m) HIPCHK(hipMemcpy(f, (int32_t*)c->fbuf.p + off[0], m * 4, hipMemcpyDeviceToHost));
+    if (pprev && m) HIPCHK(hipMemcpy(pprev, (int32_t*)c->ppbuf.p + off[0], m * 4, hipMemcpyDeviceToHost));
+    return A;
+}
+int64_t mm2g_debug_keep(mm2g_ctx* c, uint32_t r, uint8_t* keep, int64_t cap) {
+    if (!c || !c->mapped || r >= c->n_reads) return set_err(MM2G_E_STATE, "no mapped batch / bad read index");
+    HIPCHK(hipSetDevice(c->device));
+    uint64_t b; uint32_t m;
+    HIPCHK(hipMemcpy(&b, (uint64_t*)c->mz_base.p + r, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&m, (uint32_t*)c->mz_cnt.p + r, 4, hipMemcpyDeviceToHost));
+    if (keep && m) HIPCHK(hipMemcpy(keep, (uint8_t*)c->keep.p + b, std::min<int64_t>(m, cap), hipMemcpyDeviceToHost));
+    return m;
+}
+
+int mm2g_prof_enable(mm2g_ctx* c, int on) { if (!c) return set_err(MM2G_E_ARG, "null context"); c->prof = on != 0; return 0; }
+int mm2g_prof_get(mm2g_ctx* c, int i, const char** name, double* ms, int64_t* calls) {
+    if (!c) return set_err(MM2G_E_ARG, "null context");
+    c->prof_collect();
+    if (i < 0 || i >= (int)c->slots.size()) return MM2G_E_ARG;
+    if (name) *name = c->slots[i].name.c_str();
+    if (ms) *ms = c->slots[i].ms;
+    if (calls) *calls = c->slots[i].calls;
+    return 0;
+}
+int mm2g_prof_reset(mm2g_ctx* c) {
+    if (!c) return set_err(MM2G_E_ARG, "null context");
+    c->prof_collect();
+    for (auto& s : c->slots) { s.ms = 0; s.calls = 0; }
+    return 0;
+}
+int mm2g_batch_counters(mm2g_ctx* c, uint64_t* out6) {
+    if (!c || !out6) return set_err(MM2G_E_ARG, "null argument");
+    for (int t = 0; t < 6; ++t) out6[t] = c->counters[t];
+    return 0;
+}
+
+}  // extern "C"

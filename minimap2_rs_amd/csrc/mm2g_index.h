@@ -1,0 +1,49 @@
+// Host-side index (src/index.rs) and FASTA input for the MI355X path.
+#pragma once
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+namespace mm2g {
+
+struct FastaRecord { std::string name; std::string seq; };
+// noodles-fasta stand-in: name = header up to the first
+// space/tab; sequence lines concatenated with '\r' stripped.
+bool read_fasta(const char* path, std::vector<FastaRecord>& out, bool first_only, std::string& err);
+
+struct HostMinimizer { uint64_t key_span, rid_pos_strand; };
+// sketch_sequence (src/sketch.rs:29-100) on the host, incl. the HPC branch
+// (index build with -H).  Returns false on the reference's assert conditions.
+bool host_sketch(const uint8_t* seq, size_t len, int w, int k, uint32_t rid, bool hpc, std::vector<HostMinimizer>& out);
+
+struct HostSeq { bool has_name; std::string name; uint64_t offset; uint32_t len; };
+
+// Bucket b of the reference Index (src/index.rs:31): `p` plus the hash table
+// `h`, kept here as (key, value) pairs sorted by key.
+struct HostBucket {
+    std::vector<uint64_t> p;
+    std::vector<std::pair<uint64_t, uint64_t>> h;
+    bool has_h = false;
+};
+
+struct HostIndex {
+    int32_t w = 0, k = 0, b = 0, flag = 0;
+    uint32_t n_seq = 0;
+    std::vector<HostSeq> seq;
+    std::vector<uint32_t> S;               // 4-bit packed reference (index.rs:14-19)
+    std::vector<HostBucket> B;
+    uint32_t max_len = 0;
+
+    bool get(uint64_t minier, int& kind, const uint64_t*& pos, size_t& n, uint64_t& single) const;
+    void stats(uint64_t& n_keys, double& avg_occ, double& avg_spacing, uint64_t& total_len) const;
+    int32_t calc_mid_occ(float frac) const;
+    // Flat (minier, off, n) + positions export for the device table.
+    void flatten(std::vector<uint64_t>& keys, std::vector<uint32_t>& offs, std::vector<uint32_t>& ns, std::vector<uint64_t>& pos) const;
+};
+
+bool build_index(const std::vector<const uint8_t*>& seqs, const std::vector<uint64_t>& lens, const std::vector<std::string>* names,
+                 int w, int k, int b, int flag, int n_threads, HostIndex& idx, std::string& err);
+bool load_mmi(const char* path, HostIndex& idx, std::string& err);
+bool save_mmi(const HostIndex& idx, const char* path, std::string& err);
+
+}  // namespace mm2g

@@ -1,0 +1,130 @@
+// Internal definitions shared by the host orchestration and the gfx950 kernels.
+#pragma once
+#include <stdint.h>
+
+namespace mm2g {
+
+constexpr uint64_t U64MAX = ~0ULL;
+constexpr int WAVE = 64;
+
+// Anchor key packing (DESIGN.md "Anchor key").  The reference anchor is
+// (x, y) = (rev<<63 | rid<<32 | rpos, span<<32 | qpos) sorted by (x, y)
+// (src/seeds.rs:58,73-76).  For queries span == k for every minimizer, so the
+// order of (x, y) equals the order of
+//      key = group << (RB+QB) | p << QB | q
+// with group = rid (forward), n_seq + rid (reverse), 2*n_seq for the Q19
+// pseudo-group (odd rid: rpos bit 31 set and `rpos as u64` sign-extended,
+// so x = 0xffffffff_8xxxxxxx for both strands), p = rpos & 0x7fffffff.
+struct KeyLayout {
+    uint32_t qb, rb, gb;   // bit widths
+    uint32_t n_seq;
+};
+
+// Per-read device outputs of the chain kernels (mirrors mm2g_read_result).
+struct ReadOut {
+    int32_t flags;
+    int32_t n_anchors;
+    int32_t score;
+    int32_t cm;
+    int32_t qs, qe, ts, te;
+    int32_t group;
+    int32_t best_i;
+    int32_t n_match;
+    int32_t dv_st, dv_en;
+    int32_t m_dv;
+    int32_t qlen;
+    int32_t pad;
+    uint64_t dp_pairs;     // inner-loop j evaluations (all passes)
+};
+static_assert(sizeof(ReadOut) == 72, "ReadOut layout");
+
+enum : int32_t {
+    RF_MAPPED = 1, RF_RESCUED = 2, RF_DV_FOUND = 4, RF_PANIC = 8, RF_EMPTY = 16,
+};
+
+struct ChainKParams {
+    int32_t max_dist_x, max_dist_y, bw, max_iter, max_skip, span;
+    int32_t rescue_size;
+    float rescue_ratio_f;   // (1.0f - rmq_rescue_ratio), computed on the host in f32
+    int32_t pass;           // 0 = first DP, 1 = rescue DP (only RF_RESCUED reads)
+    int32_t lut_n;          // entries in the pen LUT (bw + 1)
+};
+
+// Device index layout: open-addressed table of distinct minimizer hashes.
+struct IxEntry {
+    uint64_t key;   // minimizer hash (key_span >> 8); U64MAX = empty
+    uint32_t off;   // first position in ix_pos
+    uint32_t n;     // occurrences (1 = Single)
+};
+
+__host__ __device__ inline uint32_t ix_slot(uint64_t h, uint32_t log2cap) {
+    return (uint32_t)((h * 0x9E3779B97F4A7C15ULL) >> (64 - log2cap));
+}
+
+
+// ---- kernel arguments (mm2g_kernels.hip) --------------------------------
+struct SketchArgs {
+    const uint8_t* seq;
+    const uint64_t* rd_off;     // n+1 offsets into seq
+    uint32_t n;
+    int w, k;
+    const uint64_t* out_base;   // per sequence: first output slot
+    const uint64_t* out_end;    // per sequence: one past the last slot (capacity)
+    uint64_t* mz_x;             // key_span = hash<<8 | span
+    uint32_t* mz_y;             // i<<1 | z   (rid is implicit / added by caller)
+    uint32_t* mz_cnt;           // per sequence
+    int32_t* overflow;
+};
+struct FilterArgs {
+    uint32_t n;
+    const uint64_t* mz_base; const uint32_t* mz_cnt; const uint64_t* mz_x;
+    const uint64_t* tab_off;   // per read (n+1), exclusive scan of table sizes
+    uint64_t* tab_key; uint32_t* tab_cnt;
+    uint8_t* keep;
+    int q_occ_max; float q_occ_frac;
+};
+struct SeedArgs {
+    uint32_t n;
+    const uint64_t* rd_off;
+    const uint64_t* mz_base; const uint32_t* mz_cnt; const uint64_t* mz_x; const uint32_t* mz_y; const uint8_t* keep;
+    const IxEntry* tab; uint32_t log2cap; int32_t mid_occ;
+    const uint64_t* ix_pos;
+    uint32_t* mz_n; uint32_t* mz_poff;
+    uint32_t* a_cnt;
+    const uint64_t* a_off;
+    uint64_t* keys;
+    KeyLayout kl; int span;
+};
+struct ChainArgs {
+    uint32_t n;
+    const uint64_t* rd_off;
+    const uint64_t* a_off;
+    const uint64_t* keys;
+    int32_t* f; int32_t* pp; uint32_t* chain;
+    const int16_t* lut;
+    ChainKParams P; KeyLayout kl;
+    ReadOut* out;
+    uint32_t* work;
+};
+struct DvArgs {
+    uint32_t n;
+    const uint64_t* a_off; const uint64_t* keys; const uint32_t* chain;
+    const uint64_t* mz_base; const uint32_t* mz_cnt; const uint32_t* mz_y;
+    KeyLayout kl; int span;
+    ReadOut* out;
+};
+
+}  // namespace mm2g
+
+// ---- launchers (return 0 or a hipError_t) --------------------------------
+typedef struct ihipStream_t* hipStream_t;
+int launch_sketch(const mm2g::SketchArgs& a, int n_blocks, hipStream_t st);
+int launch_filter(const mm2g::FilterArgs& a, int n_blocks, hipStream_t st);
+int launch_seed_count(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
+int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
+int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, hipStream_t st);
+int launch_chain(const mm2g::ChainArgs& a, int n_blocks, hipStream_t st);
+int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
+int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st);
+int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, hipStream_t st);
+int launch_ix_build(const uint64_t* keys, const uint32_t* offs, const uint32_t* ns, uint64_t nk, mm2g::IxEntry* tab, uint32_t log2cap, hipStream_t st);

@@ -1,0 +1,873 @@
+// gfx950 (MI355X, CDNA4) kernels of the sketch -> seed -> chain path.
+//
+// Every kernel restates one function of the reference crate (file:line in
+// /root/reference) bit-exactly; DESIGN.md explains the parallel formulation
+// and the roofline of each.  Wave64 throughout: one wavefront owns one read
+// (or one contig for index builds) and loops over it; reads are handed out
+// by grid-stride or by an atomic work counter.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <limits.h>
+#include "mm2g_internal.h"
+
+using namespace mm2g;
+
+#define DEVI __device__ __forceinline__
+
+// ------------------------------------------------------------------ helpers
+DEVI int lane_id() { return (int)(threadIdx.x & 63); }
+DEVI uint64_t ballot(bool p) { return __ballot(p); }
+DEVI int ctz64(uint64_t x) { return __builtin_ctzll(x); }
+DEVI int clz64(uint64_t x) { return __builtin_clzll(x); }
+DEVI uint64_t lanemask_lt_of(int l) { return l ? (~0ULL >> (64 - l)) : 0ULL; }
+DEVI uint64_t lanemask_lt() { return lanemask_lt_of(lane_id()); }
+
+// LDS visibility inside one wavefront: LDS ops of a wave execute in order;
+// the fences stop the compiler from moving LDS accesses across this point.
+DEVI void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+DEVI void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+DEVI int32_t rdl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+DEVI uint32_t rdlu(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+DEVI uint64_t rdl64(uint64_t v, int l) {
+    uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+DEVI int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// wave_shr:1 with lane 0 <- `in0` (DPP, one VALU op)
+DEVI int32_t shr1(int32_t v, int32_t in0) { return __builtin_amdgcn_update_dpp(in0, v, 0x138, 0xf, 0xf, false); }
+
+template <typename T, typename F>
+DEVI T wave_incl_scan(T v, F op) {
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (l >= d) v = op(o, v);
+    }
+    return v;
+}
+DEVI uint32_t wave_excl_sum(uint32_t v, uint32_t& total) {
+    uint32_t inc = wave_incl_scan(v, [](uint32_t a, uint32_t b) { return a + b; });
+    total = (uint32_t)__shfl(inc, 63, 64);
+    return inc - v;
+}
+DEVI uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// src/nt4.rs:2-10 — `b | 0x20` folds exactly {A,a}->a, {C,c}->c, {G,g}->g, {T,t}->t
+DEVI uint32_t nt4d(uint32_t b) {
+    uint32_t c = b | 0x20u;
+    return c == 'a' ? 0u : c == 'c' ? 1u : c == 'g' ? 2u : c == 't' ? 3u : 4u;
+}
+
+// src/sketch.rs:4-13 (wrapping; every step masked to 2k bits).  For k <= 16 the
+// 32-bit ring gives the same low 2k bits.
+template <typename T>
+DEVI T hash64d(T key, T mask) {
+    key = ((T)~key + (key << 21)) & mask;
+    key ^= key >> 24;
+    key = (key + (key << 3) + (key << 8)) & mask;
+    key ^= key >> 14;
+    key = (key + (key << 2) + (key << 4)) & mask;
+    key ^= key >> 28;
+    key = (key + (key << 31)) & mask;
+    return key;
+}
+
+// ============================================================================
+// 1. SKETCH — sketch_sequence (src/sketch.rs:29-100), non-HPC.
+//
+// One wave per sequence, tiles of TS = 64*CH positions; lane l owns positions
+// [t0 + l*CH, +CH).  Parallel restatement (DESIGN.md "Sketch"):
+//   * info[i] is valid iff base i is ACGT, the k-mer is not symmetric and
+//     l[i] >= k, where l is the segmented count of non-symmetric valid bases
+//     since the last ambiguous base (capped at w+k: every comparison the
+//     reference makes is against k, w+k-1 or w+k).  l is a wave scan.
+//   * after every step the reference's `min` is the NEWEST slot holding the
+//     minimum x of the last w slots, so the emissions of step i depend only
+//     on info[i-w..i] and l[i]; each lane rebuilds `min` from the w slots
+//     before its chunk and replays the reference step logic (A: first-window
+//     ties, B: new minimum, C: expiry + rescan + ties) in position order.
+//   * emissions are counted, wave-scanned and written in reference order.
+// ============================================================================
+constexpr int SK_CH = 16;
+constexpr int SK_TS = 64 * SK_CH;
+
+
+template <bool K32>
+__global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int w = a.w, k = a.k;
+    const int NB = SK_TS + w;                        // history (w) + tile
+    const int wv = threadIdx.x >> 6, lane = lane_id();
+    const size_t per_wave = (((size_t)NB * 14) + 15) & ~(size_t)15;
+    uint64_t* X = (uint64_t*)(smem + per_wave * wv);
+    uint32_t* Y = (uint32_t*)(X + NB);
+    uint16_t* Lc = (uint16_t*)(Y + NB);
+    const int CAP = w + k;
+    const uint64_t mask = (k >= 32) ? U64MAX : ((1ULL << (2 * k)) - 1);
+    const uint32_t shift1 = 2u * (uint32_t)(k - 1);
+    const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wv; r < a.n; r += nwaves) {
+        const uint8_t* s = a.seq + a.rd_off[r];
+        const int64_t L = (int64_t)(a.rd_off[r + 1] - a.rd_off[r]);
+        const uint64_t obase = a.out_base[r], oend = a.out_end[r];
+        if (L == 0) { if (lane == 0) a.mz_cnt[r] = 0; continue; }
+        // history slots = positions [-w, -1]: MAX
+        for (int t = lane; t < w; t += 64) { X[t] = U64MAX; Y[t] = 0xffffffffu; Lc[t] = 0; }
+        wave_lds_sync();
+        uint64_t count = 0;
+        int32_t l_carry = 0;
+        for (int64_t t0 = 0; t0 < L; t0 += SK_TS) {
+            const int64_t hbase = t0 - w;            // LDS index = p - hbase
+            const int64_t ps = t0 + (int64_t)lane * SK_CH;
+            const int64_t pe = ps + SK_CH < L ? ps + SK_CH : L;
+            // ---- phase 1a: k-mers and per-position flags
+            bool rs = false; int32_t lc = 0;
+            if (ps < pe) {
+                uint64_t kf = 0, kr = 0;
+                // warm-up: the last k-1 ACGT bases before ps (the k-mer
+                // registers skip ambiguous bases, src/sketch.rs:75-76,86-88)
+                int64_t wsp = ps; int need = k - 1;
+                while (need > 0 && wsp > 0) { --wsp; if (nt4d(s[wsp]) < 4) --need; }
+                for (int64_t p = wsp; p < ps; ++p) {
+                    uint32_t c = nt4d(s[p]);
+                    if (c < 4) { kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1); }
+                }
+                for (int64_t p = ps; p < pe; ++p) {
+                    const int ix = (int)(p - hbase);
+                    uint32_t c = nt4d(s[p]);
+                    uint64_t x = U64MAX; uint32_t z = 0; uint16_t fl = 0;
+                    if (c < 4) {
+                        kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1);
+                        fl = 1;
+                        if (kf != kr) {
+                            z = kf < kr ? 0u : 1u;
+                            uint64_t km = z ? kr : kf;
+                            uint64_t h;
+                            if (K32) h = hash64d<uint32_t>((uint32_t)km, (uint32_t)mask);
+                            else h = hash64d<uint64_t>(km, mask);
+                            x = (h << 8) | (uint64_t)k;        // kmer_span == k whenever info is valid
+                            fl = 2;
+                        }
+                    }
+                    X[ix] = x; Y[ix] = ((uint32_t)p << 1) | z; Lc[ix] = fl;
+                    if (fl == 0) { rs = true; lc = 0; } else if (fl == 2) { lc = lc + 1 < CAP ? lc + 1 : CAP; }
+                }
+            }
+            // ---- segmented scan of l over lanes: (reset, count)
+            int32_t er = rs ? 1 : 0, ec = lc;
+            {
+                // inclusive scan then shift to exclusive
+                int32_t ir = er, ic = ec;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    int32_t orr = __shfl_up(ir, d, 64), oc = __shfl_up(ic, d, 64);
+                    if (lane >= d) { if (!ir) { ic = oc + ic < CAP ? oc + ic : CAP; ir = orr; } }
+                }
+                int32_t xr = __shfl_up(ir, 1, 64), xc = __shfl_up(ic, 1, 64);
+                if (lane == 0) { xr = 0; xc = 0; }
+                er = xr; ec = xc;
+            }
+            int32_t lin = er ? ec : (l_carry + ec < CAP ? l_carry + ec : CAP);
+            wave_lds_sync();
+            // ---- phase 1b: l per position; invalidate info where l < k
+            int32_t lv = lin;
+            for (int64_t p = ps; p < pe; ++p) {
+                const int ix = (int)(p - hbase);
+                uint16_t fl = Lc[ix];
+                if (fl == 0) lv = 0; else if (fl == 2) lv = lv + 1 < CAP ? lv + 1 : CAP;
+                Lc[ix] = (uint16_t)lv;
+                if (!(fl == 2 && lv >= k)) X[ix] = U64MAX;
+            }
+            {
+                const int64_t te = t0 + SK_TS < L ? t0 + SK_TS : L;
+                const int owner = (int)((te - 1 - t0) / SK_CH);
+                l_carry = rdl(lv, owner);
+            }
+            wave_lds_sync();
+            // ---- phase 2: reference step logic, count then write
+            uint32_t mycnt = 0, myoff = 0;
+            uint32_t tot = 0;
+            for (int pass = 0; pass < 2; ++pass) {
+                const bool WR = pass == 1;
+                uint64_t o = obase + count + myoff;
+                uint32_t n_em = 0;
+                if (ps < pe) {
+                    uint64_t mx = U64MAX; uint32_t my = 0xffffffffu; int64_t mp = ps - w - 1;
+                    for (int64_t p = ps - w; p < ps; ++p) {
+                        const int ix = (int)(p - hbase);
+                        uint64_t x = X[ix];
+                        if (mx >= x) { mx = x; my = Y[ix]; mp = p; }
+                    }
+                    for (int64_t i = ps; i < pe; ++i) {
+                        const int ii = (int)(i - hbase);
+                        const uint64_t ix_x = X[ii]; const uint32_t ix_y = Y[ii];
+                        const int32_t l = Lc[ii];
+                        if (l == w + k - 1 && mx != U64MAX) {            // sketch.rs:90-93
+                            for (int64_t p = i - w + 1; p < i; ++p) {
+                                const int q = (int)(p - hbase);
+                                if (X[q] == mx && Y[q] != my) {
+                                    if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = Y[q]; }
+                                    ++o; ++n_em;
+                                }
+                            }
+                        }
+                        if (ix_x <= mx) {                                   // sketch.rs:94-96
+                            if (l >= w + k && mx != U64MAX) {
+                                if (WR && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
+                                ++o; ++n_em;
+                            }
+                            mx = ix_x; my = ix_y; mp = i;
+                        } else if (mp == i - w) {                           // sketch.rs:97-105
+                            if (l >= w + k - 1) {
+                                if (WR && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
+                                ++o; ++n_em;
+                            }
+                            mx = U64MAX;
+                            for (int64_t p = i - w + 1; p <= i; ++p) {
+                                const int q = (int)(p - hbase);
+                                if (mx >= X[q]) { mx = X[q]; my = Y[q]; mp = p; }
+                            }
+                            if (l >= w + k - 1 && mx != U64MAX) {
+                                for (int64_t p = i - w + 1; p <= i; ++p) {
+                                    const int q = (int)(p - hbase);
+                                    if (mx == X[q] && my != Y[q]) {
+                                        if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = Y[q]; }
+                                        ++o; ++n_em;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                }
+                if (!WR) { mycnt = n_em; myoff = wave_excl_sum(mycnt, tot); }
+            }
+            count += tot;
+            // ---- move the last w slots to the history area
+            wave_lds_sync();
+            if (t0 + SK_TS < L) {
+                // source [TS, TS+w) and destination [0, w) never overlap (w < 256 < TS)
+                for (int t = lane; t < w; t += 64) { X[t] = X[SK_TS + t]; Y[t] = Y[SK_TS + t]; Lc[t] = Lc[SK_TS + t]; }
+            }
+            wave_lds_sync();
+        }
+        // end of sequence (sketch.rs:99): newest minimum of the last window
+        if (lane == 0) {
+            const int64_t tl = ((L - 1) / SK_TS) * SK_TS;   // last tile start
+            const int64_t hbase = tl - w;
+            uint64_t mx = U64MAX; uint32_t my = 0;
+            for (int64_t p = L - w; p < L; ++p) {
+                const int ix = (int)(p - hbase);
+                uint64_t x = X[ix];
+                if (mx >= x) { mx = x; my = Y[ix]; }
+            }
+            if (mx != U64MAX) {
+                uint64_t o = obase + count;
+                if (o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
+                ++count;
+            }
+            a.mz_cnt[r] = (uint32_t)(count > 0xffffffffULL ? 0xffffffffULL : count);
+            if (obase + count > oend) atomicOr(a.overflow, 1);
+        }
+        wave_lds_sync();
+    }
+}
+
+// ============================================================================
+// 2. QUERY FILTER — filter_query_minimizers(mv, 10, 0.01) (src/seeds.rs:13-36)
+// One wave per read; an open-addressed count table per read in a scratch
+// region (size nextpow2(2m) when m > q_occ_max).  keep[i] = 0 for every
+// minimizer whose hash occurs cnt > q_occ_max && cnt > (m*frac as f32) as usize.
+// ============================================================================
+
+DEVI uint32_t tab_size_for(uint32_t m, int q_occ_max) {
+    if ((int64_t)m <= (int64_t)q_occ_max || m == 0) return 0;
+    uint32_t t = 2u * m, s = 1;
+    while (s < t) s <<= 1;
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_filter(FilterArgs a) {
+    const int lane = lane_id();
+    const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < a.n; r += nwaves) {
+        const uint64_t mb = a.mz_base[r];
+        const uint32_t m = a.mz_cnt[r];
+        uint8_t* keep = a.keep + mb;
+        const uint64_t tb = a.tab_off[r];
+        const uint32_t ts = (uint32_t)(a.tab_off[r + 1] - tb);
+        if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) {   // seeds.rs:14-15
+            for (uint32_t i = lane; i < m; i += 64) keep[i] = 1;
+            continue;
+        }
+        uint64_t* tk = a.tab_key + tb; uint32_t* tc = a.tab_cnt + tb;
+        for (uint32_t i = lane; i < ts; i += 64) { tk[i] = U64MAX; tc[i] = 0; }
+        vm_drain();
+        const uint32_t tmask = ts - 1;
+        for (uint32_t i = lane; i < m; i += 64) {
+            const uint64_t h = a.mz_x[mb + i] >> 8;
+            uint32_t sl = (uint32_t)((h * 0x9E3779B97F4A7C15ULL) >> 32) & tmask;
+            for (;;) {
+                unsigned long long prev = atomicCAS((unsigned long long*)&tk[sl], (unsigned long long)U64MAX, (unsigned long long)h);
+                if (prev == U64MAX || prev == h) { atomicAdd(&tc[sl], 1u); break; }
+                sl = (sl + 1) & tmask;
+            }
+        }
+        vm_drain();
+        const float prod = (float)m * a.q_occ_frac;
+        const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
+        for (uint32_t i = lane; i < m; i += 64) {
+            const uint64_t h = a.mz_x[mb + i] >> 8;
+            uint32_t sl = (uint32_t)((h * 0x9E3779B97F4A7C15ULL) >> 32) & tmask;
+            uint32_t c = 0;
+            for (;;) {
+                uint64_t kk = __hip_atomic_load(&tk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (kk == h) { c = __hip_atomic_load(&tc[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+                if (kk == U64MAX) break;
+                sl = (sl + 1) & tmask;
+            }
+            keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
+        }
+    }
+}
+
+// ============================================================================
+// 3. LOOKUP + ANCHOR COUNT — Index::get (src/index.rs:143-154) and the
+// mid_occ skip of build_anchors_filtered (src/seeds.rs:42-57).
+// ============================================================================
+
+DEVI void ix_lookup(const IxEntry* tab, uint32_t log2cap, uint64_t h, uint32_t& off, uint32_t& n) {
+    const uint32_t cmask = (1u << log2cap) - 1;
+    uint32_t sl = ix_slot(h, log2cap);
+    n = 0; off = 0;
+    for (;;) {
+        const IxEntry e = tab[sl];
+        if (e.key == h) { off = e.off; n = e.n; return; }
+        if (e.key == U64MAX) return;
+        sl = (sl + 1) & cmask;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
+    const int lane = lane_id();
+    const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < a.n; r += nwaves) {
+        const uint64_t mb = a.mz_base[r];
+        const uint32_t m = a.mz_cnt[r];
+        uint32_t acc = 0;
+        for (uint32_t i = lane; i < m; i += 64) {
+            uint32_t n = 0, off = 0;
+            if (a.keep[mb + i]) {
+                ix_lookup(a.tab, a.log2cap, a.mz_x[mb + i] >> 8, off, n);
+                if (n > 1 && (int64_t)n > (int64_t)a.mid_occ) n = 0;   // Multi with len > mid_occ: skip
+            }
+            a.mz_n[mb + i] = n; a.mz_poff[mb + i] = off;
+            acc += n;
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) a.a_cnt[r] = acc;
+    }
+}
+
+// push_anchor (src/seeds.rs:62-79) packed into the sortable 64-bit key.
+DEVI uint64_t pack_anchor(uint64_t rr, uint32_t my, int32_t qlen, int span, const KeyLayout& kl) {
+    const uint32_t rid = (uint32_t)(rr >> 32);
+    const uint32_t rpos32 = (uint32_t)(rr >> 1);       // ((r >> 1) & 0xffffffff)
+    const uint32_t rstrand = (uint32_t)(rr & 1);
+    const uint32_t qpos = my >> 1, qstrand = my & 1;
+    const bool fwd = rstrand == qstrand;
+    const uint32_t q = fwd ? qpos : (uint32_t)(qlen - ((int32_t)qpos + 1 - span) - 1);
+    uint64_t g; uint32_t p;
+    if (rpos32 & 0x80000000u) { g = 2ull * kl.n_seq; p = rpos32 & 0x7fffffffu; }   // Q19 pseudo-group
+    else { g = fwd ? (uint64_t)rid : (uint64_t)kl.n_seq + rid; p = rpos32; }
+    return (g << (kl.rb + kl.qb)) | ((uint64_t)p << kl.qb) | (uint64_t)q;
+}
+
+__global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
+    __shared__ uint32_t s_inc[4][64];
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wv; r < a.n; r += nwaves) {
+        const uint64_t mb = a.mz_base[r];
+        const uint32_t m = a.mz_cnt[r];
+        const int32_t qlen = (int32_t)(a.rd_off[r + 1] - a.rd_off[r]);
+        uint64_t* out = a.keys + a.a_off[r];
+        uint64_t run = 0;
+        for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+            const uint32_t i = c0 + lane;
+            const uint32_t n = i < m ? a.mz_n[mb + i] : 0;
+            uint32_t tot;
+            const uint32_t ex = wave_excl_sum(n, tot);
+            s_inc[wv][lane] = ex + n;
+            wave_lds_sync();
+            for (uint32_t t = lane; t < tot; t += 64) {
+                // owner = first lane whose inclusive offset exceeds t
+                int lo = 0, hi = 63;
+                while (lo < hi) { int mid = (lo + hi) >> 1; if (s_inc[wv][mid] > t) hi = mid; else lo = mid + 1; }
+                const uint32_t mi = c0 + (uint32_t)lo;
+                const uint32_t exo = lo ? s_inc[wv][lo - 1] : 0;
+                const uint64_t rr = a.ix_pos[a.mz_poff[mb + mi] + (t - exo)];
+                out[run + t] = pack_anchor(rr, a.mz_y[mb + mi], qlen, a.span, a.kl);
+            }
+            run += tot;
+            wave_lds_sync();
+        }
+    }
+}
+
+// ============================================================================
+// 4. ANCHOR SORT — a.sort_by((x, y)) (src/seeds.rs:58) as a segmented sort of
+// the packed keys (a total order; equal keys are identical anchors).
+//   small segments (A <= 4096): LDS bitonic sort, one workgroup per read;
+//   large segments: LSD radix sort (8-bit digits over the varying bits only),
+//   one 1024-thread workgroup per read, stable ranking by wave match.
+// ============================================================================
+constexpr int SORT_SMALL = 4096;
+
+__global__ __launch_bounds__(256) void k_sort_small(uint32_t n, const uint64_t* a_off, uint64_t* keys) {
+    __shared__ uint64_t s[SORT_SMALL];
+    const uint32_t r = blockIdx.x;
+    if (r >= n) return;
+    const uint64_t base = a_off[r];
+    const uint32_t A = (uint32_t)(a_off[r + 1] - base);
+    if (A <= 1 || A > SORT_SMALL) return;
+    uint32_t np = 1; while (np < A) np <<= 1;
+    uint64_t* K = keys + base;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < A ? K[i] : U64MAX;
+    __syncthreads();
+    for (uint32_t kk = 2; kk <= np; kk <<= 1) {
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t x = s[i], y = s[ixj];
+                    const bool up = (i & kk) == 0;
+                    if ((x > y) == up) { s[i] = y; s[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) K[i] = s[i];
+}
+
+__global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t woff[16][256];
+    __shared__ uint64_t red_or[16], red_and[16];
+    const uint32_t r = blockIdx.x;
+    if (r >= n) return;
+    const uint64_t base = a_off[r];
+    const uint32_t A = (uint32_t)(a_off[r + 1] - base);
+    if (A <= SORT_SMALL) return;
+    const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+    uint64_t* src = keys + base;
+    uint64_t* dst = tmp + base;
+    // bits that vary across the segment
+    uint64_t vo = 0, va = U64MAX;
+    for (uint32_t i = tid; i < A; i += 1024) { uint64_t x = src[i]; vo |= x; va &= x; }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { vo |= __shfl_xor(vo, d, 64); va &= __shfl_xor(va, d, 64); }
+    if (lane == 0) { red_or[wv] = vo; red_and[wv] = va; }
+    __syncthreads();
+    vo = 0; va = U64MAX;
+    for (int t = 0; t < 16; ++t) { vo |= red_or[t]; va &= red_and[t]; }
+    const uint64_t vary = vo ^ va;
+    const int top = vary ? 64 - clz64(vary) : 0;
+    bool in_tmp = false;
+    for (int shift = 0; shift < top; shift += 8) {
+        if (((vary >> shift) & 0xffULL) == 0) continue;       // digit constant: order unchanged
+        if (tid < 256) hist[tid] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < A; i += 1024) atomicAdd(&hist[(uint32_t)(src[i] >> shift) & 255u], 1u);
+        __syncthreads();
+        if (tid == 0) {   // exclusive scan of 256 bins (serial, tiny)
+            uint32_t run = 0;
+            for (int d = 0; d < 256; ++d) { uint32_t c = hist[d]; hist[d] = run; run += c; }
+        }
+        __syncthreads();
+        for (uint32_t t0 = 0; t0 < A; t0 += 1024) {
+            const uint32_t i = t0 + tid;
+            const bool valid = i < A;
+            const uint64_t x = valid ? src[i] : 0;
+            const uint32_t d = (uint32_t)(x >> shift) & 255u;
+            for (int t = tid; t < 16 * 256; t += 1024) (&woff[0][0])[t] = 0;
+            __syncthreads();
+            uint64_t peers = ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t mb = ballot(bit);
+                peers &= bit ? mb : ~mb;
+            }
+            const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+            if (valid && (peers & lanemask_lt()) == 0) woff[wv][d] = (uint32_t)__popcll(peers);
+            __syncthreads();
+            if (tid < 256) {
+                uint32_t run = hist[tid];
+                for (int t = 0; t < 16; ++t) { uint32_t c = woff[t][tid]; woff[t][tid] = run; run += c; }
+                hist[tid] = run;
+            }
+            __syncthreads();
+            if (valid) dst[woff[wv][d] + rank] = x;
+            __syncthreads();
+        }
+        uint64_t* t = src; src = dst; dst = t;
+        in_tmp = !in_tmp;
+    }
+    if (in_tmp) {
+        for (uint32_t i = tid; i < A; i += 1024) dst[i] = src[i];   // src is tmp here, dst is keys
+    }
+}
+
+// ============================================================================
+// 5. CHAIN DP — chain_dp_all (src/lchain.rs:59-91) + the fallback chain
+// (lchain.rs:162-173) + chain_qrange/trange (178-200) + the rescue test of
+// rescue_long_join (316-330).
+//
+// One wave per read, anchors i in order.  For each i the j-loop runs 64
+// predecessors per step (lane l <-> j = jtop - l, reference processing order):
+//   valid_j   comput_sc (lchain.rs:17-34) with the integer pen LUT (DESIGN Q6)
+//   marks     t[pprev[j]] = i  -> one bit in an LDS ring (targets >= lo only)
+//   max_f     strict '>' => exclusive prefix-max scan seeded with max_f
+//   n_skip    ops x->max(x-1,0) | x->x+1 | id compose as x->max(x+a,b):
+//             inclusive scan, break = first '+1' lane with n_skip > max_skip
+// The 64 newest anchors (j = i-1-lane) live in registers (wave_shr each i);
+// deeper steps read keys/f/pprev from HBM (f/pprev flushed every 64 anchors).
+// ============================================================================
+
+constexpr int DP_NW = 4;          // waves per workgroup
+constexpr int RING_WORDS = 256;   // 8192-bit mark ring (max_iter <= 8000)
+
+__global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const ChainKParams P = a.P;
+    int16_t* lut = (int16_t*)smem;
+    const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
+    uint32_t* rings = (uint32_t*)(smem + lut_bytes);
+    for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
+    for (int i = threadIdx.x; i < DP_NW * RING_WORDS; i += blockDim.x) rings[i] = 0;
+    __syncthreads();
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    uint32_t* ring = rings + wv * RING_WORDS;
+    const uint32_t qb = a.kl.qb, rb = a.kl.rb;
+    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
+    const uint32_t gsh = rb + qb;
+    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    for (;;) {
+        uint32_t r = 0;
+        if (lane == 0) r = atomicAdd(a.work, 1u);
+        r = (uint32_t)uni((int32_t)r);
+        if (r >= a.n) break;
+        const int32_t flags0 = a.out[r].flags;
+        if (P.pass == 1 && !(flags0 & RF_RESCUED)) continue;
+        const uint64_t base = a.a_off[r];
+        const int32_t A = (int32_t)(a.a_off[r + 1] - base);
+        const int32_t qlen = (int32_t)(a.rd_off[r + 1] - a.rd_off[r]);
+        if (A == 0) {
+            if (lane == 0) {
+                ReadOut o = {}; o.flags = flags0 & RF_EMPTY; o.qlen = qlen; o.best_i = -1;
+                a.out[r] = o;
+            }
+            continue;
+        }
+        const uint64_t* K = a.keys + base;
+        int32_t* F = a.f + base; int32_t* PP = a.pp + base;
+        uint64_t ak = lane < A ? K[lane] : 0;
+        int32_t stb = 0, st = 0;
+        uint64_t sk = ak;
+        int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
+        int32_t best_f = INT_MIN, best_i = -1;
+        uint64_t pairs = 0;
+        for (int32_t i = 0; i < A; ++i) {
+            if ((i & 63) == 0 && i) ak = (i + lane < A) ? K[i + lane] : 0;
+            const uint64_t ki = rdl64(ak, i & 63);
+            const uint32_t gi = (uint32_t)(ki >> gsh);
+            const int32_t pi = (int32_t)((ki >> qb) & rmask);
+            const int32_t qi = (int32_t)(ki & qmask);
+            // ---- st (lchain.rs:75): first j in i's group with rpos_i <= rpos_j + max_dist_x
+            for (;;) {
+                const int32_t j = stb + lane;
+                const uint32_t gj = (uint32_t)(sk >> gsh);
+                const int32_t pj = (int32_t)((sk >> qb) & rmask);
+                const bool cand = j >= st && j <= i;
+                const bool stop = cand && (j == i || (gj == gi && !(pi > (int32_t)((uint32_t)pj + (uint32_t)maxdx))));
+                const uint64_t m = ballot(stop);
+                if (m) { st = stb + ctz64(m); break; }
+                stb += 64;
+                sk = (stb + lane < A) ? K[stb + lane] : 0;
+            }
+            const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
+            int32_t max_f = span, max_j = -1, n_skip = 0;
+            int32_t jtop = i - 1;
+            int nsteps = 0;
+            while (jtop >= lo) {
+                const int32_t j = jtop - lane;
+                const bool inr = j >= lo;
+                int32_t pj, qj, fj, ppj;
+                if (nsteps == 0) { pj = wp; qj = wq; fj = wf; ppj = wpp; }
+                else {
+                    if (nsteps == 1) vm_drain();      // f/pprev flushes of recent iterations
+                    if (inr) {
+                        const uint64_t kj = K[j];
+                        pj = (int32_t)((kj >> qb) & rmask); qj = (int32_t)(kj & qmask);
+                        fj = F[j]; ppj = PP[j];
+                    } else { pj = 0; qj = 0; fj = 0; ppj = -1; }
+                }
+                // comput_sc (lchain.rs:17-34); rid/rev equal for every j >= st
+                const int32_t dq = qi - qj, dr = pi - pj;
+                bool ok = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
+                const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                ok = ok && dd <= bw;
+                const int32_t dg = dr < dq ? dr : dq;
+                const int32_t sc = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
+                const int32_t s = sc + fj;
+                // t[pprev[j]] = i  (lchain.rs:86), targets below lo are never read
+                if (ok && ppj >= lo) atomicOr(&ring[(ppj >> 5) & (RING_WORDS - 1)], 1u << (ppj & 31));
+                wave_lds_sync();
+                const bool marked = ok && ((ring[(j >> 5) & (RING_WORDS - 1)] >> (j & 31)) & 1u);
+                // strict new maximum in processing order
+                const int32_t v = ok ? s : INT_MIN;
+                const int32_t incl = wave_incl_scan(v, [](int32_t x, int32_t y) { return x > y ? x : y; });
+                int32_t excl = __shfl_up(incl, 1, 64);
+                if (lane == 0) excl = INT_MIN;
+                const int32_t pb = max_f > excl ? max_f : excl;
+                const bool nm = ok && s > pb;
+                // n_skip: compose x -> max(x + a, b)
+                int32_t sa = nm ? -1 : ((ok && marked) ? 1 : 0), sb = 0;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int32_t oa = __shfl_up(sa, d, 64), ob = __shfl_up(sb, d, 64);
+                    if (lane >= d) { const int32_t t = ob + sa; sb = t > sb ? t : sb; sa = oa + sa; }
+                }
+                const int32_t na = (n_skip + sa) > sb ? (n_skip + sa) : sb;
+                const uint64_t brk = ballot(ok && !nm && marked && na > P.max_skip);
+                const uint64_t eff = brk ? (lanemask_lt_of(ctz64(brk))) : ~0ULL;
+                const uint64_t nmm = ballot(nm) & eff;
+                if (nmm) { const int L = 63 - clz64(nmm); max_f = rdl(s, L); max_j = jtop - L; }
+                {
+                    const uint64_t inr_m = ballot(inr);
+                    const uint64_t seen = brk ? (inr_m & (eff | (1ULL << ctz64(brk)))) : inr_m;
+                    pairs += (uint64_t)__popcll(seen);
+                }
+                ++nsteps;
+                if (brk) break;
+                n_skip = rdl(na, 63);
+                jtop -= 64;
+            }
+            // clear this i's marks (all targets lie in [lo, i-1])
+            if (i - 1 >= lo) {
+                const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
+                for (int32_t wd = w0 + lane; wd <= w1; wd += 64) ring[wd & (RING_WORDS - 1)] = 0;
+                wave_lds_sync();
+            }
+            // f[i], pprev[i]; fallback best_i = LAST index with max f
+            if (max_f >= best_f) { best_f = max_f; best_i = i; }
+            wp = shr1(wp, pi); wq = shr1(wq, qi); wf = shr1(wf, max_f); wpp = shr1(wpp, max_j);
+            if (((i + 1) & 63) == 0) { const int32_t j = i - lane; F[j] = wf; PP[j] = wpp; }
+        }
+        {
+            const int32_t rem = A & 63;
+            if (lane < rem) { const int32_t j = A - 1 - lane; F[j] = wf; PP[j] = wpp; }
+        }
+        vm_drain();
+        pairs = (uint64_t)uni((int32_t)(uint32_t)pairs) | ((uint64_t)(uint32_t)uni((int32_t)(pairs >> 32)) << 32);
+        // ---- fallback chain walk (lchain.rs:162-171), chain ranges, rescue test
+        if (lane == 0) {
+            uint32_t* CB = a.chain + base;
+            int32_t idx = best_i, root = best_i, cm = 0;
+            while (idx >= 0 && cm < A) { CB[cm++] = (uint32_t)idx; root = idx; idx = PP[idx]; }
+            const uint64_t kb = K[best_i], kr = K[root];
+            const uint32_t g = (uint32_t)(kb >> gsh);
+            const int32_t qe = (int32_t)(kb & qmask) + 1;
+            int32_t qs = (int32_t)(kr & qmask) - (span - 1); if (qs < 0) qs = 0;
+            int32_t ts, te;
+            if (g == 2u * a.kl.n_seq) { ts = 0; te = -1; }    // Q19: rpos = p - 2^31 < 0
+            else {
+                te = (int32_t)((kb >> qb) & rmask) + 1;
+                ts = (int32_t)((kr >> qb) & rmask) - (span - 1); if (ts < 0) ts = 0;
+            }
+            ReadOut o = a.out[r];
+            if (P.pass == 0) { o = ReadOut{}; o.dp_pairs = 0; }
+            o.n_anchors = A; o.qlen = qlen;
+            o.score = best_f; o.cm = cm; o.qs = qs; o.qe = qe; o.ts = ts; o.te = te;
+            o.group = (int32_t)g; o.best_i = best_i;
+            int32_t fl = RF_MAPPED | (o.flags & RF_RESCUED);
+            if (g == 2u * a.kl.n_seq) fl |= RF_PANIC;
+            if (P.pass == 0) {
+                int32_t cov = qe - qs; if (cov < 0) cov = 0;
+                int32_t unc = qlen - cov; if (unc < 0) unc = 0;
+                if (unc > P.rescue_size || (float)cov < (float)qlen * P.rescue_ratio_f) fl |= RF_RESCUED;
+            }
+            o.flags = fl;
+            o.dp_pairs += pairs;
+            a.out[r] = o;
+        }
+    }
+}
+
+// ============================================================================
+// 6. dv inputs — paf_from_chain_with_primary (src/paf.rs:156-199): binary
+// search (Rust >= 1.82 slice::binary_search) of the first chain position among
+// the minimizer positions of the (idx.w, idx.k) sketch, then the greedy match.
+// ============================================================================
+
+__global__ __launch_bounds__(256) void k_dv(DvArgs a) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.n) return;
+    ReadOut o = a.out[r];
+    const uint32_t m = a.mz_cnt[r];
+    o.m_dv = (int32_t)m;
+    o.flags &= ~RF_DV_FOUND;
+    if (!(o.flags & RF_MAPPED) || (o.flags & RF_PANIC) || m == 0 || o.cm <= 0) { a.out[r] = o; return; }
+    const uint32_t* Y = a.mz_y + a.mz_base[r];
+    const uint32_t* CB = a.chain + a.a_off[r];
+    const uint64_t* K = a.keys + a.a_off[r];
+    const uint64_t qmask = (1ULL << a.kl.qb) - 1;
+    const bool rev = (uint32_t)o.group >= a.kl.n_seq;
+    const int32_t cm = o.cm, qlen = o.qlen, span = a.span;
+    auto fwdq = [&](int32_t t) -> int32_t {   // t-th chain anchor in forward-query order
+        if (!rev) { const int32_t q = (int32_t)(K[CB[cm - 1 - t]] & qmask); return q; }
+        const int32_t q = (int32_t)(K[CB[t]] & qmask);
+        return qlen - 1 - (q + 1 - span);
+    };
+    auto mpos = [&](uint32_t j) -> int32_t { return (int32_t)(Y[j] >> 1); };
+    const int32_t first = fwdq(0);
+    uint32_t size = m, b = 0;
+    while (size > 1) { const uint32_t half = size / 2, mid = b + half; if (!(mpos(mid) > first)) b = mid; size -= half; }
+    if (mpos(b) != first) { a.out[r] = o; return; }
+    uint32_t st = b;
+    while (st > 0 && mpos(st - 1) == first) --st;
+    uint32_t j = st, en = st; int32_t kk = 1, n_match = 1;
+    while (j + 1 < m && kk < cm) {
+        ++j;
+        if (mpos(j) == fwdq(kk)) { ++n_match; en = j; ++kk; }
+    }
+    o.flags |= RF_DV_FOUND; o.n_match = n_match; o.dv_st = (int32_t)st; o.dv_en = (int32_t)en;
+    a.out[r] = o;
+}
+
+// ============================================================================
+// misc: scans and per-read setup
+// ============================================================================
+// out[i] = sum_{t<i} f(in[t]) for i in [0, n]; mode 0: identity, mode 1: filter
+// table size.  Single workgroup, 1024 threads, chunked with carry.
+__global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry_s;
+    const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < n; c0 += 1024) {
+        const uint32_t i = c0 + tid;
+        uint64_t v = 0;
+        if (i < n) { uint32_t x = in[i]; v = mode == 1 ? (uint64_t)tab_size_for(x, q_occ_max) : (uint64_t)x; }
+        uint64_t inc = wave_incl_scan(v, [](uint64_t x, uint64_t y) { return x + y; });
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        uint64_t woff = 0;
+        for (int t = 0; t < wv; ++t) woff += wsum[t];
+        const uint64_t carry = carry_s;
+        if (i < n) out[i] = carry + woff + inc - v;
+        __syncthreads();
+        if (tid == 1023) carry_s = carry + woff + inc;
+        __syncthreads();
+    }
+    if (tid == 0) out[n] = carry_s;
+}
+
+__global__ void k_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    base[r] = rd_off[r] + 16ull * r;
+    end[r] = rd_off[r + 1] + 16ull * (r + 1);
+}
+
+// Build the device index table from (key, off, n) triples (insert with CAS).
+__global__ void k_ix_build(const uint64_t* keys, const uint32_t* offs, const uint32_t* ns, uint64_t nk, IxEntry* tab, uint32_t log2cap) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nk) return;
+    const uint64_t h = keys[t];
+    const uint32_t cmask = (1u << log2cap) - 1;
+    uint32_t sl = ix_slot(h, log2cap);
+    for (;;) {
+        unsigned long long prev = atomicCAS((unsigned long long*)&tab[sl].key, (unsigned long long)U64MAX, (unsigned long long)h);
+        if (prev == U64MAX) { tab[sl].off = offs[t]; tab[sl].n = ns[t]; return; }
+        sl = (sl + 1) & cmask;
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+#define LAUNCH_CHECK() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+int launch_sketch(const SketchArgs& a, int n_blocks, hipStream_t st) {
+    const size_t per_wave = (((size_t)(SK_TS + a.w) * 14) + 15) & ~(size_t)15;
+    const size_t lds = per_wave * 4;
+    if (a.k <= 16) hipLaunchKernelGGL(k_sketch<true>, dim3(n_blocks), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL(k_sketch<false>, dim3(n_blocks), dim3(256), lds, st, a);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_filter(const FilterArgs& a, int n_blocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_filter, dim3(n_blocks), dim3(256), 0, st, a);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_seed_count(const SeedArgs& a, int n_blocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_seed_count, dim3(n_blocks), dim3(256), 0, st, a);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_seed_write, dim3(n_blocks), dim3(256), 0, st, a);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, hipStream_t st) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_sort_small, dim3(n), dim3(256), 0, st, n, a_off, keys);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sort_large, dim3(n), dim3(1024), 0, st, n, a_off, keys, tmp);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_chain(const ChainArgs& a, int n_blocks, hipStream_t st) {
+    const size_t lds = (size_t)(((a.P.lut_n * 2) + 15) & ~15) + (size_t)DP_NW * RING_WORDS * 4;
+    hipLaunchKernelGGL(k_chain_dp, dim3(n_blocks), dim3(DP_NW * 64), lds, st, a);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_dv(const DvArgs& a, hipStream_t st) {
+    if (a.n == 0) return 0;
+    hipLaunchKernelGGL(k_dv, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st) {
+    hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(1024), 0, st, in, n, out, mode, q_occ_max);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, hipStream_t st) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_mz_base, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, base, end);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_ix_build(const uint64_t* keys, const uint32_t* offs, const uint32_t* ns, uint64_t nk, IxEntry* tab, uint32_t log2cap, hipStream_t st) {
+    if (nk == 0) return 0;
+    hipLaunchKernelGGL(k_ix_build, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, st, keys, offs, ns, nk, tab, log2cap);
+    LAUNCH_CHECK();
+    return 0;
+}

@@ -1,0 +1,131 @@
+"""GPU parity: every stage of the MI355X path against the CPU oracle, bit-exact.
+
+All calls go through libmm2g.so's C ABI (minimap2_rs_amd wraps it with
+ctypes); the oracle is only the checker."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import minimap2_rs_amd as M
+from oracle import oracle as O
+from tools import simdata
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    d = M.Device(0)
+    yield d
+    d.close()
+
+
+def _rand_seq(rng, n, p_n=0.0, p_low=0.1, alphabet=b"ACGT"):
+    s = bytearray(rng.choice(alphabet) for _ in range(n))
+    for i in range(n):
+        r = rng.random()
+        if r < p_n:
+            s[i] = ord(rng.choice("NnRYKM-*"))
+        elif r < p_n + p_low:
+            s[i] = s[i] | 0x20 if chr(s[i]).isalpha() else s[i]
+    return bytes(s)
+
+
+def _edge_seqs(rng):
+    seqs = [b"A", b"ACGT", b"N" * 50, b"ACGTACGTACGTACGTACGTACGTACGT", b"A" * 300, b"AC" * 200, b"ACGTTGCA" * 80]
+    for n in [5, 14, 15, 16, 24, 25, 26, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 2049, 5000]:
+        seqs.append(_rand_seq(rng, n, p_n=0.0))
+    for n in [200, 3000, 9000]:
+        seqs.append(_rand_seq(rng, n, p_n=0.01))
+        seqs.append(_rand_seq(rng, n, p_n=0.2))
+    s = bytearray(_rand_seq(rng, 6000))
+    s[1000:1020] = b"N" * 20
+    s[3000:3600] = b"N" * 600
+    seqs.append(bytes(s))
+    # low complexity / periodic (ties, C-case rescans)
+    seqs.append((b"ACGTTA" * 900)[:5000])
+    seqs.append(b"".join(rng.choice([b"AAAAAAA", b"CCCC", b"GT", b"TTTTTTTTTT"]) for _ in range(800)))
+    return seqs
+
+
+@pytest.mark.parametrize("w,k", [(10, 15), (10, 19), (11, 21), (5, 16), (3, 4), (1, 1), (1, 2), (50, 7), (255, 28), (7, 28), (2, 10), (64, 12), (65, 13)])
+def test_sketch_parity(dev, w, k):
+    rng = random.Random(1000 * w + k)
+    seqs = _edge_seqs(rng)
+    got = dev.sketch_sequences(seqs, w, k, rid=0)
+    for i, s in enumerate(seqs):
+        want = O.sketch(s, w, k, 0, False)
+        g = got[i]
+        assert g.shape == want.shape, (i, len(s), g.shape, want.shape)
+        assert np.array_equal(g, want), (i, len(s))
+
+
+def test_sketch_rid(dev):
+    rng = random.Random(5)
+    seqs = [_rand_seq(rng, 3000, p_n=0.01) for _ in range(3)]
+    got = dev.sketch_sequences(seqs, 10, 15, rid=7)
+    for i, s in enumerate(seqs):
+        assert np.array_equal(got[i], O.sketch(s, 10, 15, 7, False))
+
+
+@pytest.fixture(scope="module")
+def small_world(tmp_path_factory):
+    td = tmp_path_factory.mktemp("world")
+    ref = str(td / "ref.fa")
+    simdata.write_genome("hg38", 0.0008, 21, ref)        # 24 contigs, ~2.5 Mb, hg38-shaped repeats
+    names, seqs = simdata.read_fasta_seqs(ref)
+    lens = np.array([len(s) for s in seqs], dtype=np.int64)
+    g = np.frombuffer(b"".join(seqs), dtype=np.uint8)
+    rb, offs, _ = simdata.reads(g, lens, 150, 6000, 22)
+    rnames = [f"r{i}" for i in range(150)]
+    rseqs = [rb[offs[i]:offs[i + 1]].tobytes() for i in range(150)]
+    rng = random.Random(3)
+    extra = [(b"ACGT" * 3), _rand_seq(rng, 5000), _rand_seq(rng, 30), b"N" * 100,
+             seqs[0][20000:21000], seqs[1][30000:30500].lower(), seqs[2][40000:52000]]
+    for i, s in enumerate(extra):
+        rnames.append(f"x{i}")
+        rseqs.append(s)
+    reads = str(td / "reads.fa")
+    simdata.write_fasta(reads, rnames, rseqs)
+    return ref, reads, rnames, rseqs
+
+
+def test_pipeline_parity(dev, small_world, tmp_path):
+    ref, reads, rnames, rseqs = small_world
+    oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+    idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+    mid = max(idx.calc_mid_occ(2e-4), 10)
+    assert mid == max(oi.mid_occ(2e-4), 10)
+    dev.upload_index(idx, mid)
+    dev.set_debug(True)
+    dev.set_reads(rseqs)
+    res = dev.map(M.map_opts())
+    n_checked = 0
+    for r, q in enumerate(rseqs):
+        want_a, _ = oi.anchors(q, 10, 15, mid)
+        got_a = dev.debug_anchors(r)
+        assert np.array_equal(got_a, want_a), f"anchors differ for read {r}"
+        if len(want_a) == 0:
+            assert not (res[r].flags & 1)
+            continue
+        rescued = bool(res[r].flags & 2)
+        f, pp, chain, score, _ = O.chain_dp(want_a, 15, bw=(20000 if rescued else 500))
+        gf, gpp = dev.debug_dp(r)
+        assert np.array_equal(gf, f), f"f differs for read {r}"
+        assert np.array_equal(gpp.astype(np.int64), pp), f"pprev differs for read {r}"
+        n_checked += 1
+    assert n_checked > 100
+    want_paf = str(tmp_path / "want.paf")
+    oi.align_fasta(reads, want_paf)
+    got = dev.paf(rnames, res)
+    assert got == open(want_paf).read()
+
+
+def test_pipeline_determinism(dev, small_world):
+    ref, reads, rnames, rseqs = small_world
+    idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+    p1 = M.align(idx, rnames, rseqs, dev=dev)
+    p2 = M.align(idx, rnames, rseqs, dev=dev)
+    assert p1 == p2 and p1.count("\n") > 50
