@@ -12,7 +12,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD_DIR = os.path.join(HERE, "build")
-LIB_PATH = os.path.join(BUILD_DIR, "libmm2g.so")
+LIB_PATH = os.environ.get("MM2G_LIB") or os.path.join(BUILD_DIR, "libmm2g.so")
 CLI_PATH = os.path.join(BUILD_DIR, "mm2rs")
 
 MM2G_R_MAPPED = 1

@@ -119,14 +119,34 @@ struct mm2g_ctx {
     }
 };
 
+// MM2G_SYNC=1: synchronise after every stage and report the first failing
+// stage (and, in MM2G_CHECKED builds, the first out-of-range index).
+static bool g_sync_each = getenv("MM2G_SYNC") && atoi(getenv("MM2G_SYNC")) != 0;
 struct ProfScope {
-    mm2g_ctx* c; int i; hipEvent_t e0{};
-    ProfScope(mm2g_ctx* c_, const char* n) : c(c_) { i = c->prof_begin(n, e0); }
-    ~ProfScope() { c->prof_end(i, e0); }
+    mm2g_ctx* c; int i; hipEvent_t e0{}; const char* name;
+    ProfScope(mm2g_ctx* c_, const char* n) : c(c_), name(n) { i = c->prof_begin(n, e0); }
+    ~ProfScope() {
+        c->prof_end(i, e0);
+        if (g_sync_each) {
+            unsigned long long ck[4] = {0, 0, 0, 0};
+            int e = mm2g_checked_read(ck, c->stream);
+            if (e != 0 || ck[0] != 0) {
+                fprintf(stderr, "[mm2g] stage %s: hip=%d (%s) check line=%llu idx=%llu cap=%llu\n", name, e,
+                        hipGetErrorString((hipError_t)e), ck[0], ck[1], ck[2]);
+                fflush(stderr);
+            }
+        }
+    }
 };
 
 static inline uint32_t bit_width(uint64_t x) { uint32_t b = 0; while (x) { ++b; x >>= 1; } return b; }
 static inline int grid_for(uint32_t n) { int b = (int)((n + 3) / 4); return std::max(1, std::min(b, 4096)); }
+
+template <size_t N>
+static inline char* put_lit(char* p, const char (&lit)[N]) {
+    memcpy(p, lit, N - 1);
+    return p + (N - 1);
+}
 
 extern "C" {
 
@@ -408,7 +428,8 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->mz_n, uint32_t, mcap, mz_n); ENSURE(c->mz_poff, uint32_t, mcap, mz_poff);
     ENSURE(c->a_cnt, uint32_t, n + 1, a_cnt); ENSURE(c->a_off, uint64_t, n + 1, a_off);
     SeedArgs sa{n, (const uint64_t*)c->rd_off.p, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, (const uint32_t*)c->mz_y.p, keep,
-                (const IxEntry*)c->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k};
+                (const IxEntry*)c->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k,
+                0, c->ix_pos.cap / 8, mcap};
     {
         ProfScope ps(c, "seed_count");
         LCHK(launch_seed_count(sa, grid_for(n), c->stream));
@@ -424,7 +445,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     uint64_t *keys, *ktmp; int32_t *fb, *pb;
     ENSURE(c->keys, uint64_t, A, keys); ENSURE(c->keys_tmp, uint64_t, A, ktmp);
     ENSURE(c->fbuf, int32_t, A, fb); ENSURE(c->ppbuf, int32_t, A, pb);
-    sa.keys = keys;
+    sa.keys = keys; sa.cap_keys = c->keys.cap / 8;
     {
         ProfScope ps(c, "seed_write");
         LCHK(launch_seed_write(sa, grid_for(n), c->stream));
@@ -432,7 +453,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     // 4. anchor sort (seeds.rs:58)
     {
         ProfScope ps(c, "sort");
-        LCHK(launch_sort(n, a_off, keys, ktmp, c->stream));
+        LCHK(launch_sort(n, a_off, keys, ktmp, c->keys.cap / 8, c->stream));
     }
     // 5. chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
     build_lut(c, o->k, lut_need);
@@ -444,11 +465,39 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ChainKParams P{};
     P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
     P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
-    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work};
     const int chain_blocks = std::max(1, std::min((int)((n + 3) / 4), 2048));
+    uint32_t* trace_h = nullptr; uint32_t* trace_d = nullptr;
+#ifdef MM2G_CHECKED
+    if (g_sync_each) {
+        const size_t tb = (size_t)chain_blocks * 4 * 4 * sizeof(uint32_t);
+        HIPCHK(hipHostMalloc((void**)&trace_h, tb, hipHostMallocMapped));
+        memset(trace_h, 0xff, tb);
+        HIPCHK(hipHostGetDevicePointer((void**)&trace_d, trace_h, 0));
+    }
+#endif
+    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work, std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, trace_d};
+    auto dump_trace = [&](const char* what) {
+        if (!trace_h) return;
+        std::vector<uint64_t> ho(n + 1);
+        fprintf(stderr, "[mm2g] trace after %s (waves not at phase 9/1-done):\n", what);
+        for (int wv = 0; wv < chain_blocks * 4; ++wv) {
+            const uint32_t* t = trace_h + 4 * wv;
+            if (t[2] != 9 && !(t[2] == 1 && t[0] >= n) && t[2] != 0xffffffffu)
+                fprintf(stderr, "  wave %d: read %u i %u phase %u aux %u\n", wv, t[0], t[1], t[2], t[3]);
+        }
+        fflush(stderr);
+    };
     {
         ProfScope ps(c, "chain_dp");
         LCHK(launch_chain(ca, chain_blocks, c->stream));
+    }
+    if (trace_h) {
+        hipError_t e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            dump_trace("chain_dp");
+            // anchor counts of the in-flight reads (host copy of a_off is not available after a fault)
+            return set_err(MM2G_E_HIP, "chain_dp failed: %s", hipGetErrorString(e));
+        }
     }
     ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
     ca.P.lut_n = o->bw_long + 1; ca.work = work + 1;
@@ -465,7 +514,8 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         if (e) return e;
     }
     DvArgs da{n, a_off, keys, (const uint32_t*)ktmp, sep ? (const uint64_t*)c->mz2_base.p : mz_base,
-              sep ? (const uint32_t*)c->mz2_cnt.p : mz_cnt, sep ? (const uint32_t*)c->mz2_y.p : (const uint32_t*)c->mz_y.p, kl, o->k, out};
+              sep ? (const uint32_t*)c->mz2_cnt.p : mz_cnt, sep ? (const uint32_t*)c->mz2_y.p : (const uint32_t*)c->mz_y.p, kl, o->k, out,
+              c->keys.cap / 8, (sep ? c->mz2_y.cap : c->mz_y.cap) / 4};
     {
         ProfScope ps(c, "dv");
         LCHK(launch_dv(da, c->stream));
@@ -553,7 +603,6 @@ int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, cons
         const HostSeq& s = H.seq[r.rid];
         const char* tname = s.has_name ? s.name.c_str() : "*";
         const size_t qn = strlen(names[i]), tn = strlen(tname);
-        if (out && o + (int64_t)(qn + tn + 256) > cap) return set_err(MM2G_E_NOMEM, "PAF output buffer too small");
         char line[512];
         char* p = line;
         const uint32_t qlen = (uint32_t)r.qlen, qs = (uint32_t)r.qs, qe = (uint32_t)r.qe;
@@ -563,13 +612,14 @@ int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, cons
         char* q = line + 256;
         *q++ = '\t'; q = put_u(q, s.len); *q++ = '\t'; q = put_u(q, (uint32_t)r.ts); *q++ = '\t'; q = put_u(q, (uint32_t)r.te);
         *q++ = '\t'; q = put_u(q, (uint32_t)std::max(r.qe - r.qs, 0)); *q++ = '\t'; q = put_u(q, (uint32_t)std::max(r.te - r.ts, 0));
-        memcpy(q, "\t60\ttp:A:P\tcm:i:", 16); q += 16; q = put_u(q, (uint32_t)r.cm);
-        memcpy(q, "\ts1:i:", 6); q += 6; q = put_u(q, (uint32_t)std::max(r.score, 0));
-        memcpy(q, "\ts2:i:0\tdv:f:", 12); q += 12;
+        q = put_lit(q, "\t60\ttp:A:P\tcm:i:"); q = put_u(q, (uint32_t)r.cm);
+        q = put_lit(q, "\ts1:i:"); q = put_u(q, (uint32_t)std::max(r.score, 0));
+        q = put_lit(q, "\ts2:i:0\tdv:f:");
         q += snprintf(q, 32, "%.4f", (double)r.dv);
-        memcpy(q, "\trl:i:0\n", 8); q += 8;
+        q = put_lit(q, "\trl:i:0\n");
         const int64_t len = (int64_t)qn + (p - line) + (int64_t)tn + (q - (line + 256));
         if (out) {
+            if (o + len > cap) return set_err(MM2G_E_NOMEM, "PAF output buffer too small");
             memcpy(out + o, names[i], qn); o += (int64_t)qn;
             memcpy(out + o, line, (size_t)(p - line)); o += p - line;
             memcpy(out + o, tname, tn); o += (int64_t)tn;

@@ -94,6 +94,7 @@ struct SeedArgs {
     const uint64_t* a_off;
     uint64_t* keys;
     KeyLayout kl; int span;
+    uint64_t cap_keys, cap_pos, cap_mz;   // bounds for the MM2G_CHECKED build
 };
 struct ChainArgs {
     uint32_t n;
@@ -105,6 +106,8 @@ struct ChainArgs {
     ChainKParams P; KeyLayout kl;
     ReadOut* out;
     uint32_t* work;
+    uint64_t cap_keys;
+    uint32_t* trace;    // MM2G_CHECKED: host-mapped per-wave progress {read, i, phase, aux}
 };
 struct DvArgs {
     uint32_t n;
@@ -112,6 +115,7 @@ struct DvArgs {
     const uint64_t* mz_base; const uint32_t* mz_cnt; const uint32_t* mz_y;
     KeyLayout kl; int span;
     ReadOut* out;
+    uint64_t cap_keys, cap_mz;
 };
 
 }  // namespace mm2g
@@ -122,7 +126,9 @@ int launch_sketch(const mm2g::SketchArgs& a, int n_blocks, hipStream_t st);
 int launch_filter(const mm2g::FilterArgs& a, int n_blocks, hipStream_t st);
 int launch_seed_count(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
-int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, hipStream_t st);
+int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st);
+// MM2G_CHECKED builds: first recorded bounds violation {line, index, cap}; 0 = none
+int mm2g_checked_read(unsigned long long out[4], hipStream_t st);
 int launch_chain(const mm2g::ChainArgs& a, int n_blocks, hipStream_t st);
 int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st);

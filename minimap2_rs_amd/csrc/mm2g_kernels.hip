@@ -14,6 +14,22 @@ using namespace mm2g;
 
 #define DEVI __device__ __forceinline__
 
+// Bounds-checked build (-DMM2G_CHECKED): an out-of-range index is recorded
+// (first violation wins) and replaced by 0 instead of faulting the GPU.
+#ifdef MM2G_CHECKED
+__device__ unsigned long long g_chk[4];
+DEVI uint64_t ck_idx(uint64_t i, uint64_t cap, int line) {
+    if (i < cap) return i;
+    if (atomicCAS(&g_chk[0], 0ULL, (unsigned long long)line) == 0ULL) { g_chk[1] = i; g_chk[2] = cap; }
+    return 0;
+}
+#define CK(i, cap) ck_idx((uint64_t)(i), (uint64_t)(cap), __LINE__)
+#define TRACE(tr, slot, v) do { if (tr) __hip_atomic_store(&(tr)[slot], (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+#else
+#define TRACE(tr, slot, v) do {} while (0)
+#define CK(i, cap) (i)
+#endif
+
 // ------------------------------------------------------------------ helpers
 DEVI int lane_id() { return (int)(threadIdx.x & 63); }
 DEVI uint64_t ballot(bool p) { return __ballot(p); }
@@ -40,8 +56,11 @@ DEVI uint64_t rdl64(uint64_t v, int l) {
 }
 DEVI int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// wave_shr:1 with lane 0 <- `in0` (DPP, one VALU op)
-DEVI int32_t shr1(int32_t v, int32_t in0) { return __builtin_amdgcn_update_dpp(in0, v, 0x138, 0xf, 0xf, false); }
+// Shift the wave right by one lane, lane 0 <- `in0` (ds_bpermute based).
+DEVI int32_t shr1(int32_t v, int32_t in0) {
+    const int32_t t = __shfl_up(v, 1, 64);
+    return lane_id() == 0 ? in0 : t;
+}
 
 template <typename T, typename F>
 DEVI T wave_incl_scan(T v, F op) {
@@ -55,7 +74,7 @@ DEVI T wave_incl_scan(T v, F op) {
 }
 DEVI uint32_t wave_excl_sum(uint32_t v, uint32_t& total) {
     uint32_t inc = wave_incl_scan(v, [](uint32_t a, uint32_t b) { return a + b; });
-    total = (uint32_t)__shfl(inc, 63, 64);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);   // SGPR: wave-uniform
     return inc - v;
 }
 DEVI uint32_t wave_sum(uint32_t v) {
@@ -84,6 +103,24 @@ DEVI T hash64d(T key, T mask) {
     return key;
 }
 
+// ------------------------------------------------------------------ control-flow rule
+// HIP gives no maximal-reconvergence guarantee: the compiler may restructure a
+// lane-divergent LOOP at the end of an outer loop body into a divergent loop
+// exit, letting some lanes start the next iteration early (observed on
+// gfx950/ROCm 7.2 in a first version of k_chain_dp).  Every kernel that talks
+// across lanes (ballot/shuffle/readlane/LDS hand-off) therefore follows one rule:
+// every loop has a wave-uniform trip count (fixed, or `while (any(...))`),
+// per-read scalars are made provably uniform with readfirstlane, and
+// lane-divergence appears only in straight-line code.
+DEVI bool any(bool p) { return ballot(p) != 0ULL; }
+// wave index inside the workgroup, provably uniform for divergence analysis
+DEVI int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+DEVI uint64_t uni64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // ============================================================================
 // 1. SKETCH — sketch_sequence (src/sketch.rs:29-100), non-HPC.
 //
@@ -103,13 +140,12 @@ DEVI T hash64d(T key, T mask) {
 constexpr int SK_CH = 16;
 constexpr int SK_TS = 64 * SK_CH;
 
-
 template <bool K32>
 __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int w = a.w, k = a.k;
     const int NB = SK_TS + w;                        // history (w) + tile
-    const int wv = threadIdx.x >> 6, lane = lane_id();
+    const int wv = wave_id(), lane = lane_id();
     const size_t per_wave = (((size_t)NB * 14) + 15) & ~(size_t)15;
     uint64_t* X = (uint64_t*)(smem + per_wave * wv);
     uint32_t* Y = (uint32_t*)(X + NB);
@@ -119,12 +155,16 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
     const uint32_t shift1 = 2u * (uint32_t)(k - 1);
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wv; r < a.n; r += nwaves) {
-        const uint8_t* s = a.seq + a.rd_off[r];
-        const int64_t L = (int64_t)(a.rd_off[r + 1] - a.rd_off[r]);
-        const uint64_t obase = a.out_base[r], oend = a.out_end[r];
+        const uint64_t roff = uni64(a.rd_off[r]);
+        const uint8_t* s = a.seq + roff;
+        const int64_t L = (int64_t)(uni64(a.rd_off[r + 1]) - roff);
+        const uint64_t obase = uni64(a.out_base[r]), oend = uni64(a.out_end[r]);
         if (L == 0) { if (lane == 0) a.mz_cnt[r] = 0; continue; }
         // history slots = positions [-w, -1]: MAX
-        for (int t = lane; t < w; t += 64) { X[t] = U64MAX; Y[t] = 0xffffffffu; Lc[t] = 0; }
+        for (int t0 = 0; t0 < w; t0 += 64) {
+            const int t = t0 + lane;
+            if (t < w) { X[t] = U64MAX; Y[t] = 0xffffffffu; Lc[t] = 0; }
+        }
         wave_lds_sync();
         uint64_t count = 0;
         int32_t l_carry = 0;
@@ -133,27 +173,35 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
             const int64_t ps = t0 + (int64_t)lane * SK_CH;
             const int64_t pe = ps + SK_CH < L ? ps + SK_CH : L;
             // ---- phase 1a: k-mers and per-position flags
-            bool rs = false; int32_t lc = 0;
-            if (ps < pe) {
-                uint64_t kf = 0, kr = 0;
-                // warm-up: the last k-1 ACGT bases before ps (the k-mer
-                // registers skip ambiguous bases, src/sketch.rs:75-76,86-88)
-                int64_t wsp = ps; int need = k - 1;
-                while (need > 0 && wsp > 0) { --wsp; if (nt4d(s[wsp]) < 4) --need; }
-                for (int64_t p = wsp; p < ps; ++p) {
-                    uint32_t c = nt4d(s[p]);
+            // warm-up: the last k-1 ACGT bases before ps (the k-mer registers
+            // skip ambiguous bases, src/sketch.rs:75-76,86-88)
+            uint64_t kf = 0, kr = 0;
+            int64_t wsp = ps;
+            int need = ps < pe ? k - 1 : 0;
+            while (any(need > 0 && wsp > 0)) {
+                if (need > 0 && wsp > 0) { --wsp; if (nt4d(s[wsp]) < 4) --need; }
+            }
+            int64_t pw = wsp;
+            while (any(pw < ps)) {
+                if (pw < ps) {
+                    const uint32_t c = nt4d(s[pw]);
                     if (c < 4) { kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1); }
+                    ++pw;
                 }
-                for (int64_t p = ps; p < pe; ++p) {
+            }
+            bool rs = false; int32_t lc = 0;
+            for (int t = 0; t < SK_CH; ++t) {
+                const int64_t p = ps + t;
+                if (p < pe) {
                     const int ix = (int)(p - hbase);
-                    uint32_t c = nt4d(s[p]);
+                    const uint32_t c = nt4d(s[p]);
                     uint64_t x = U64MAX; uint32_t z = 0; uint16_t fl = 0;
                     if (c < 4) {
                         kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1);
                         fl = 1;
                         if (kf != kr) {
                             z = kf < kr ? 0u : 1u;
-                            uint64_t km = z ? kr : kf;
+                            const uint64_t km = z ? kr : kf;
                             uint64_t h;
                             if (K32) h = hash64d<uint32_t>((uint32_t)km, (uint32_t)mask);
                             else h = hash64d<uint64_t>(km, mask);
@@ -166,29 +214,30 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                 }
             }
             // ---- segmented scan of l over lanes: (reset, count)
-            int32_t er = rs ? 1 : 0, ec = lc;
+            int32_t er, ec;
             {
-                // inclusive scan then shift to exclusive
-                int32_t ir = er, ic = ec;
+                int32_t ir = rs ? 1 : 0, ic = lc;
 #pragma unroll
                 for (int d = 1; d < 64; d <<= 1) {
-                    int32_t orr = __shfl_up(ir, d, 64), oc = __shfl_up(ic, d, 64);
-                    if (lane >= d) { if (!ir) { ic = oc + ic < CAP ? oc + ic : CAP; ir = orr; } }
+                    const int32_t orr = __shfl_up(ir, d, 64), oc = __shfl_up(ic, d, 64);
+                    if (lane >= d && !ir) { ic = oc + ic < CAP ? oc + ic : CAP; ir = orr; }
                 }
-                int32_t xr = __shfl_up(ir, 1, 64), xc = __shfl_up(ic, 1, 64);
-                if (lane == 0) { xr = 0; xc = 0; }
-                er = xr; ec = xc;
+                er = __shfl_up(ir, 1, 64); ec = __shfl_up(ic, 1, 64);
+                if (lane == 0) { er = 0; ec = 0; }
             }
-            int32_t lin = er ? ec : (l_carry + ec < CAP ? l_carry + ec : CAP);
+            const int32_t lin = er ? ec : (l_carry + ec < CAP ? l_carry + ec : CAP);
             wave_lds_sync();
             // ---- phase 1b: l per position; invalidate info where l < k
             int32_t lv = lin;
-            for (int64_t p = ps; p < pe; ++p) {
-                const int ix = (int)(p - hbase);
-                uint16_t fl = Lc[ix];
-                if (fl == 0) lv = 0; else if (fl == 2) lv = lv + 1 < CAP ? lv + 1 : CAP;
-                Lc[ix] = (uint16_t)lv;
-                if (!(fl == 2 && lv >= k)) X[ix] = U64MAX;
+            for (int t = 0; t < SK_CH; ++t) {
+                const int64_t p = ps + t;
+                if (p < pe) {
+                    const int ix = (int)(p - hbase);
+                    const uint16_t fl = Lc[ix];
+                    if (fl == 0) lv = 0; else if (fl == 2) lv = lv + 1 < CAP ? lv + 1 : CAP;
+                    Lc[ix] = (uint16_t)lv;
+                    if (!(fl == 2 && lv >= k)) X[ix] = U64MAX;
+                }
             }
             {
                 const int64_t te = t0 + SK_TS < L ? t0 + SK_TS : L;
@@ -197,88 +246,99 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
             }
             wave_lds_sync();
             // ---- phase 2: reference step logic, count then write
-            uint32_t mycnt = 0, myoff = 0;
-            uint32_t tot = 0;
+            uint32_t myoff = 0, tot = 0;
             for (int pass = 0; pass < 2; ++pass) {
                 const bool WR = pass == 1;
                 uint64_t o = obase + count + myoff;
                 uint32_t n_em = 0;
-                if (ps < pe) {
-                    uint64_t mx = U64MAX; uint32_t my = 0xffffffffu; int64_t mp = ps - w - 1;
-                    for (int64_t p = ps - w; p < ps; ++p) {
-                        const int ix = (int)(p - hbase);
-                        uint64_t x = X[ix];
-                        if (mx >= x) { mx = x; my = Y[ix]; mp = p; }
+                // newest minimum of the w slots before the chunk (same for every lane count)
+                uint64_t mx = U64MAX; uint32_t my = 0xffffffffu; int64_t mp = ps - w - 1;
+                for (int d = 0; d < w; ++d) {
+                    const int64_t p = ps - w + d;
+                    const int q = (int)(p - hbase);
+                    const uint64_t x = X[q];
+                    if (mx >= x) { mx = x; my = Y[q]; mp = p; }
+                }
+                for (int t = 0; t < SK_CH; ++t) {
+                    const int64_t i = ps + t;
+                    const bool act = i < pe;
+                    const int ii = (int)(i - hbase);
+                    const uint64_t ix_x = act ? X[ii] : U64MAX;
+                    const uint32_t ix_y = act ? Y[ii] : 0xffffffffu;
+                    const int32_t l = act ? (int32_t)Lc[ii] : 0;
+                    // A: first window (sketch.rs:90-93)
+                    const bool doA = act && l == w + k - 1 && mx != U64MAX;
+                    if (any(doA)) {
+                        for (int d = 1; d < w; ++d) {
+                            const int q = ii - w + d;
+                            if (doA && X[q] == mx && Y[q] != my) {
+                                if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = Y[q]; }
+                                ++o; ++n_em;
+                            }
+                        }
                     }
-                    for (int64_t i = ps; i < pe; ++i) {
-                        const int ii = (int)(i - hbase);
-                        const uint64_t ix_x = X[ii]; const uint32_t ix_y = Y[ii];
-                        const int32_t l = Lc[ii];
-                        if (l == w + k - 1 && mx != U64MAX) {            // sketch.rs:90-93
-                            for (int64_t p = i - w + 1; p < i; ++p) {
-                                const int q = (int)(p - hbase);
-                                if (X[q] == mx && Y[q] != my) {
+                    // B: new minimum (sketch.rs:94-96)
+                    const bool doB = act && ix_x <= mx;
+                    // C: the minimum's slot is overwritten (sketch.rs:97-105)
+                    const bool doC = act && !doB && mp == i - w;
+                    if ((doB && l >= w + k && mx != U64MAX) || (doC && l >= w + k - 1)) {
+                        if (WR && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
+                        ++o; ++n_em;
+                    }
+                    if (doB) { mx = ix_x; my = ix_y; mp = i; }
+                    if (any(doC)) {
+                        uint64_t nx = U64MAX; uint32_t ny = 0; int64_t np = mp;
+                        for (int d = 1; d <= w; ++d) {
+                            const int q = ii - w + d;
+                            const uint64_t x = X[q];
+                            if (nx >= x) { nx = x; ny = Y[q]; np = i - w + d; }
+                        }
+                        if (doC) { mx = nx; my = ny; mp = np; }
+                        const bool doT = doC && l >= w + k - 1 && mx != U64MAX;
+                        if (any(doT)) {
+                            for (int d = 1; d <= w; ++d) {
+                                const int q = ii - w + d;
+                                if (doT && mx == X[q] && my != Y[q]) {
                                     if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = Y[q]; }
                                     ++o; ++n_em;
                                 }
                             }
                         }
-                        if (ix_x <= mx) {                                   // sketch.rs:94-96
-                            if (l >= w + k && mx != U64MAX) {
-                                if (WR && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
-                                ++o; ++n_em;
-                            }
-                            mx = ix_x; my = ix_y; mp = i;
-                        } else if (mp == i - w) {                           // sketch.rs:97-105
-                            if (l >= w + k - 1) {
-                                if (WR && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
-                                ++o; ++n_em;
-                            }
-                            mx = U64MAX;
-                            for (int64_t p = i - w + 1; p <= i; ++p) {
-                                const int q = (int)(p - hbase);
-                                if (mx >= X[q]) { mx = X[q]; my = Y[q]; mp = p; }
-                            }
-                            if (l >= w + k - 1 && mx != U64MAX) {
-                                for (int64_t p = i - w + 1; p <= i; ++p) {
-                                    const int q = (int)(p - hbase);
-                                    if (mx == X[q] && my != Y[q]) {
-                                        if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = Y[q]; }
-                                        ++o; ++n_em;
-                                    }
-                                }
-                            }
-                        }
                     }
                 }
-                if (!WR) { mycnt = n_em; myoff = wave_excl_sum(mycnt, tot); }
+                if (!WR) myoff = wave_excl_sum(n_em, tot);
             }
             count += tot;
             // ---- move the last w slots to the history area
             wave_lds_sync();
             if (t0 + SK_TS < L) {
                 // source [TS, TS+w) and destination [0, w) never overlap (w < 256 < TS)
-                for (int t = lane; t < w; t += 64) { X[t] = X[SK_TS + t]; Y[t] = Y[SK_TS + t]; Lc[t] = Lc[SK_TS + t]; }
+                for (int b0 = 0; b0 < w; b0 += 64) {
+                    const int t = b0 + lane;
+                    if (t < w) { X[t] = X[SK_TS + t]; Y[t] = Y[SK_TS + t]; Lc[t] = Lc[SK_TS + t]; }
+                }
             }
             wave_lds_sync();
         }
         // end of sequence (sketch.rs:99): newest minimum of the last window
-        if (lane == 0) {
+        {
             const int64_t tl = ((L - 1) / SK_TS) * SK_TS;   // last tile start
             const int64_t hbase = tl - w;
             uint64_t mx = U64MAX; uint32_t my = 0;
-            for (int64_t p = L - w; p < L; ++p) {
-                const int ix = (int)(p - hbase);
-                uint64_t x = X[ix];
-                if (mx >= x) { mx = x; my = Y[ix]; }
+            for (int d = 0; d < w; ++d) {
+                const int q = (int)(L - w + d - hbase);
+                const uint64_t x = X[q];
+                if (mx >= x) { mx = x; my = Y[q]; }
             }
             if (mx != U64MAX) {
-                uint64_t o = obase + count;
-                if (o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
+                const uint64_t o = obase + count;
+                if (lane == 0 && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
                 ++count;
             }
-            a.mz_cnt[r] = (uint32_t)(count > 0xffffffffULL ? 0xffffffffULL : count);
-            if (obase + count > oend) atomicOr(a.overflow, 1);
+            if (lane == 0) {
+                a.mz_cnt[r] = (uint32_t)(count > 0xffffffffULL ? 0xffffffffULL : count);
+                if (obase + count > oend) atomicOr(a.overflow, 1);
+            }
         }
         wave_lds_sync();
     }
@@ -290,89 +350,93 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
 // region (size nextpow2(2m) when m > q_occ_max).  keep[i] = 0 for every
 // minimizer whose hash occurs cnt > q_occ_max && cnt > (m*frac as f32) as usize.
 // ============================================================================
-
 DEVI uint32_t tab_size_for(uint32_t m, int q_occ_max) {
     if ((int64_t)m <= (int64_t)q_occ_max || m == 0) return 0;
     uint32_t t = 2u * m, s = 1;
     while (s < t) s <<= 1;
     return s;
 }
+DEVI uint32_t fslot(uint64_t h, uint32_t tmask) { return (uint32_t)((h * 0x9E3779B97F4A7C15ULL) >> 32) & tmask; }
 
 __global__ __launch_bounds__(256) void k_filter(FilterArgs a) {
     const int lane = lane_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < a.n; r += nwaves) {
-        const uint64_t mb = a.mz_base[r];
-        const uint32_t m = a.mz_cnt[r];
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
+        const uint64_t mb = uni64(a.mz_base[r]);
+        const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
         uint8_t* keep = a.keep + mb;
-        const uint64_t tb = a.tab_off[r];
-        const uint32_t ts = (uint32_t)(a.tab_off[r + 1] - tb);
+        const uint64_t tb = uni64(a.tab_off[r]);
+        const uint32_t ts = (uint32_t)(uni64(a.tab_off[r + 1]) - tb);
         if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) {   // seeds.rs:14-15
-            for (uint32_t i = lane; i < m; i += 64) keep[i] = 1;
+            for (uint32_t b0 = 0; b0 < m; b0 += 64) { const uint32_t i = b0 + lane; if (i < m) keep[i] = 1; }
             continue;
         }
         uint64_t* tk = a.tab_key + tb; uint32_t* tc = a.tab_cnt + tb;
-        for (uint32_t i = lane; i < ts; i += 64) { tk[i] = U64MAX; tc[i] = 0; }
+        for (uint32_t b0 = 0; b0 < ts; b0 += 64) { const uint32_t i = b0 + lane; if (i < ts) { tk[i] = U64MAX; tc[i] = 0; } }
         vm_drain();
         const uint32_t tmask = ts - 1;
-        for (uint32_t i = lane; i < m; i += 64) {
-            const uint64_t h = a.mz_x[mb + i] >> 8;
-            uint32_t sl = (uint32_t)((h * 0x9E3779B97F4A7C15ULL) >> 32) & tmask;
-            for (;;) {
-                unsigned long long prev = atomicCAS((unsigned long long*)&tk[sl], (unsigned long long)U64MAX, (unsigned long long)h);
-                if (prev == U64MAX || prev == h) { atomicAdd(&tc[sl], 1u); break; }
-                sl = (sl + 1) & tmask;
+        for (uint32_t b0 = 0; b0 < m; b0 += 64) {
+            const uint32_t i = b0 + lane;
+            bool done = i >= m;
+            const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
+            uint32_t sl = fslot(h, tmask);
+            while (any(!done)) {
+                if (!done) {
+                    const unsigned long long prev = atomicCAS((unsigned long long*)&tk[sl], (unsigned long long)U64MAX, (unsigned long long)h);
+                    if (prev == U64MAX || prev == h) { atomicAdd(&tc[sl], 1u); done = true; }
+                    else sl = (sl + 1) & tmask;
+                }
             }
         }
         vm_drain();
         const float prod = (float)m * a.q_occ_frac;
         const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
-        for (uint32_t i = lane; i < m; i += 64) {
-            const uint64_t h = a.mz_x[mb + i] >> 8;
-            uint32_t sl = (uint32_t)((h * 0x9E3779B97F4A7C15ULL) >> 32) & tmask;
-            uint32_t c = 0;
-            for (;;) {
-                uint64_t kk = __hip_atomic_load(&tk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (kk == h) { c = __hip_atomic_load(&tc[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
-                if (kk == U64MAX) break;
-                sl = (sl + 1) & tmask;
+        for (uint32_t b0 = 0; b0 < m; b0 += 64) {
+            const uint32_t i = b0 + lane;
+            bool done = i >= m;
+            const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
+            uint32_t sl = fslot(h, tmask), c = 0;
+            while (any(!done)) {
+                if (!done) {
+                    const uint64_t kk = __hip_atomic_load(&tk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (kk == h) { c = __hip_atomic_load(&tc[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); done = true; }
+                    else if (kk == U64MAX) done = true;
+                    else sl = (sl + 1) & tmask;
+                }
             }
-            keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
+            if (i < m) keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
         }
     }
 }
 
 // ============================================================================
-// 3. LOOKUP + ANCHOR COUNT — Index::get (src/index.rs:143-154) and the
-// mid_occ skip of build_anchors_filtered (src/seeds.rs:42-57).
+// 3. LOOKUP + ANCHORS — Index::get (src/index.rs:143-154), the mid_occ skip of
+// build_anchors_filtered (src/seeds.rs:42-57) and push_anchor (seeds.rs:62-79).
 // ============================================================================
-
-DEVI void ix_lookup(const IxEntry* tab, uint32_t log2cap, uint64_t h, uint32_t& off, uint32_t& n) {
-    const uint32_t cmask = (1u << log2cap) - 1;
-    uint32_t sl = ix_slot(h, log2cap);
-    n = 0; off = 0;
-    for (;;) {
-        const IxEntry e = tab[sl];
-        if (e.key == h) { off = e.off; n = e.n; return; }
-        if (e.key == U64MAX) return;
-        sl = (sl + 1) & cmask;
-    }
-}
-
 __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
     const int lane = lane_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < a.n; r += nwaves) {
-        const uint64_t mb = a.mz_base[r];
-        const uint32_t m = a.mz_cnt[r];
+    const uint32_t cmask = (1u << a.log2cap) - 1;
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
+        const uint64_t mb = uni64(a.mz_base[r]);
+        const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
         uint32_t acc = 0;
-        for (uint32_t i = lane; i < m; i += 64) {
-            uint32_t n = 0, off = 0;
-            if (a.keep[mb + i]) {
-                ix_lookup(a.tab, a.log2cap, a.mz_x[mb + i] >> 8, off, n);
-                if (n > 1 && (int64_t)n > (int64_t)a.mid_occ) n = 0;   // Multi with len > mid_occ: skip
+        for (uint32_t b0 = 0; b0 < m; b0 += 64) {
+            const uint32_t i = b0 + lane;
+            const bool act = i < m;
+            bool done = !(act && a.keep[mb + i]);
+            const uint64_t h = act ? (a.mz_x[mb + i] >> 8) : 0;
+            uint32_t sl = ix_slot(h, a.log2cap), n = 0, off = 0;
+            while (any(!done)) {
+                if (!done) {
+                    const IxEntry e = a.tab[sl];
+                    if (e.key == h) { off = e.off; n = e.n; done = true; }
+                    else if (e.key == U64MAX) done = true;
+                    else sl = (sl + 1) & cmask;
+                }
             }
-            a.mz_n[mb + i] = n; a.mz_poff[mb + i] = off;
+            if (n > 1 && (int64_t)n > (int64_t)a.mid_occ) n = 0;   // Multi with len > mid_occ: skip
+            if (act) { a.mz_n[mb + i] = n; a.mz_poff[mb + i] = off; }
             acc += n;
         }
         acc = wave_sum(acc);
@@ -396,29 +460,35 @@ DEVI uint64_t pack_anchor(uint64_t rr, uint32_t my, int32_t qlen, int span, cons
 
 __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
     __shared__ uint32_t s_inc[4][64];
-    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const int lane = lane_id(), wv = wave_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wv; r < a.n; r += nwaves) {
-        const uint64_t mb = a.mz_base[r];
-        const uint32_t m = a.mz_cnt[r];
-        const int32_t qlen = (int32_t)(a.rd_off[r + 1] - a.rd_off[r]);
-        uint64_t* out = a.keys + a.a_off[r];
+        const uint64_t mb = uni64(a.mz_base[r]);
+        const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
+        const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
+        const uint64_t obase = uni64(a.a_off[r]);
+        uint64_t* out = a.keys;
         uint64_t run = 0;
         for (uint32_t c0 = 0; c0 < m; c0 += 64) {
             const uint32_t i = c0 + lane;
-            const uint32_t n = i < m ? a.mz_n[mb + i] : 0;
+            const uint32_t n = i < m ? a.mz_n[CK(mb + i, a.cap_mz)] : 0;
             uint32_t tot;
             const uint32_t ex = wave_excl_sum(n, tot);
             s_inc[wv][lane] = ex + n;
             wave_lds_sync();
-            for (uint32_t t = lane; t < tot; t += 64) {
-                // owner = first lane whose inclusive offset exceeds t
-                int lo = 0, hi = 63;
-                while (lo < hi) { int mid = (lo + hi) >> 1; if (s_inc[wv][mid] > t) hi = mid; else lo = mid + 1; }
-                const uint32_t mi = c0 + (uint32_t)lo;
-                const uint32_t exo = lo ? s_inc[wv][lo - 1] : 0;
-                const uint64_t rr = a.ix_pos[a.mz_poff[mb + mi] + (t - exo)];
-                out[run + t] = pack_anchor(rr, a.mz_y[mb + mi], qlen, a.span, a.kl);
+            for (uint32_t tb = 0; tb < tot; tb += 64) {
+                const uint32_t t = tb + lane;
+                if (t < tot) {
+                    // owner = number of inclusive offsets <= t (first lane whose offset exceeds t)
+                    uint32_t lo = 0;
+#pragma unroll
+                    for (uint32_t step = 32; step >= 1; step >>= 1)
+                        if (s_inc[wv][lo + step - 1] <= t) lo += step;
+                    const uint32_t mi = c0 + lo;
+                    const uint32_t exo = lo ? s_inc[wv][lo - 1] : 0;
+                    const uint64_t rr = a.ix_pos[CK((uint64_t)a.mz_poff[CK(mb + mi, a.cap_mz)] + (t - exo), a.cap_pos)];
+                    out[CK(obase + run + t, a.cap_keys)] = pack_anchor(rr, a.mz_y[CK(mb + mi, a.cap_mz)], qlen, a.span, a.kl);
+                }
             }
             run += tot;
             wave_lds_sync();
@@ -426,7 +496,6 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
     }
 }
 
-// ============================================================================
 // 4. ANCHOR SORT — a.sort_by((x, y)) (src/seeds.rs:58) as a segmented sort of
 // the packed keys (a total order; equal keys are identical anchors).
 //   small segments (A <= 4096): LDS bitonic sort, one workgroup per read;
@@ -435,7 +504,7 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
 // ============================================================================
 constexpr int SORT_SMALL = 4096;
 
-__global__ __launch_bounds__(256) void k_sort_small(uint32_t n, const uint64_t* a_off, uint64_t* keys) {
+__global__ __launch_bounds__(256) void k_sort_small(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t cap_keys) {
     __shared__ uint64_t s[SORT_SMALL];
     const uint32_t r = blockIdx.x;
     if (r >= n) return;
@@ -443,8 +512,8 @@ __global__ __launch_bounds__(256) void k_sort_small(uint32_t n, const uint64_t* 
     const uint32_t A = (uint32_t)(a_off[r + 1] - base);
     if (A <= 1 || A > SORT_SMALL) return;
     uint32_t np = 1; while (np < A) np <<= 1;
-    uint64_t* K = keys + base;
-    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < A ? K[i] : U64MAX;
+    uint64_t* K = keys;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < A ? K[CK(base + i, cap_keys)] : U64MAX;
     __syncthreads();
     for (uint32_t kk = 2; kk <= np; kk <<= 1) {
         for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
@@ -459,10 +528,10 @@ __global__ __launch_bounds__(256) void k_sort_small(uint32_t n, const uint64_t* 
             __syncthreads();
         }
     }
-    for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) K[i] = s[i];
+    for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) K[CK(base + i, cap_keys)] = s[i];
 }
 
-__global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp) {
+__global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t woff[16][256];
     __shared__ uint64_t red_or[16], red_and[16];
@@ -471,6 +540,9 @@ __global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t*
     const uint64_t base = a_off[r];
     const uint32_t A = (uint32_t)(a_off[r + 1] - base);
     if (A <= SORT_SMALL) return;
+#ifdef MM2G_CHECKED
+    if (base + A > cap_keys) { if (threadIdx.x == 0) CK(base + A, cap_keys); return; }
+#endif
     const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
     uint64_t* src = keys + base;
     uint64_t* dst = tmp + base;
@@ -520,7 +592,7 @@ __global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t*
                 hist[tid] = run;
             }
             __syncthreads();
-            if (valid) dst[woff[wv][d] + rank] = x;
+            if (valid) dst[CK(woff[wv][d] + rank, A)] = x;
             __syncthreads();
         }
         uint64_t* t = src; src = dst; dst = t;
@@ -531,6 +603,7 @@ __global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t*
     }
 }
 
+// ============================================================================
 // ============================================================================
 // 5. CHAIN DP — chain_dp_all (src/lchain.rs:59-91) + the fallback chain
 // (lchain.rs:162-173) + chain_qrange/trange (178-200) + the rescue test of
@@ -543,10 +616,9 @@ __global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t*
 //   max_f     strict '>' => exclusive prefix-max scan seeded with max_f
 //   n_skip    ops x->max(x-1,0) | x->x+1 | id compose as x->max(x+a,b):
 //             inclusive scan, break = first '+1' lane with n_skip > max_skip
-// The 64 newest anchors (j = i-1-lane) live in registers (wave_shr each i);
-// deeper steps read keys/f/pprev from HBM (f/pprev flushed every 64 anchors).
+// The 64 newest anchors (j = i-1-lane) live in registers (shifted one lane per
+// i); deeper steps read keys/f/pprev from HBM (f/pprev flushed every 64 i).
 // ============================================================================
-
 constexpr int DP_NW = 4;          // waves per workgroup
 constexpr int RING_WORDS = 256;   // 8192-bit mark ring (max_iter <= 8000)
 
@@ -559,29 +631,36 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
     for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
     for (int i = threadIdx.x; i < DP_NW * RING_WORDS; i += blockDim.x) rings[i] = 0;
     __syncthreads();
-    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const int lane = lane_id(), wv = wave_id();
     uint32_t* ring = rings + wv * RING_WORDS;
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const uint32_t gsh = rb + qb;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
-    for (;;) {
-        uint32_t r = 0;
-        if (lane == 0) r = atomicAdd(a.work, 1u);
-        r = (uint32_t)uni((int32_t)r);
-        if (r >= a.n) break;
-        const int32_t flags0 = a.out[r].flags;
+    uint32_t* tr = (a.trace && lane == 0) ? a.trace + 4 * (blockIdx.x * DP_NW + wv) : nullptr;
+    (void)tr;
+    // Static, wave-uniform assignment of reads (r is an SGPR-derived loop
+    // counter; a lane-0 atomic work queue here was mis-structured by the
+    // compiler, see the control-flow rule above).
+    const uint32_t nwaves = gridDim.x * DP_NW;
+    for (uint32_t r = blockIdx.x * DP_NW + wv; r < a.n; r += nwaves) {
+        TRACE(tr, 0, r); TRACE(tr, 2, 1);
+        const int32_t flags0 = uni(a.out[r].flags);
         if (P.pass == 1 && !(flags0 & RF_RESCUED)) continue;
-        const uint64_t base = a.a_off[r];
-        const int32_t A = (int32_t)(a.a_off[r + 1] - base);
-        const int32_t qlen = (int32_t)(a.rd_off[r + 1] - a.rd_off[r]);
+        const uint64_t base = uni64(a.a_off[r]);
+        const int32_t A = (int32_t)(uni64(a.a_off[r + 1]) - base);
+        const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
         if (A == 0) {
             if (lane == 0) {
-                ReadOut o = {}; o.flags = flags0 & RF_EMPTY; o.qlen = qlen; o.best_i = -1;
-                a.out[r] = o;
+                ReadOut* O = a.out + r;
+                O->flags = flags0 & RF_EMPTY; O->n_anchors = 0; O->score = 0; O->cm = 0;
+                O->qs = O->qe = O->ts = O->te = 0; O->group = 0; O->best_i = -1; O->qlen = qlen;
             }
             continue;
         }
+#ifdef MM2G_CHECKED
+        if (base + (uint64_t)A > a.cap_keys) { if (lane == 0) CK(base + A, a.cap_keys); continue; }
+#endif
         const uint64_t* K = a.keys + base;
         int32_t* F = a.f + base; int32_t* PP = a.pp + base;
         uint64_t ak = lane < A ? K[lane] : 0;
@@ -592,6 +671,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
         uint64_t pairs = 0;
         for (int32_t i = 0; i < A; ++i) {
             if ((i & 63) == 0 && i) ak = (i + lane < A) ? K[i + lane] : 0;
+            TRACE(tr, 1, i); TRACE(tr, 2, 2);
             const uint64_t ki = rdl64(ak, i & 63);
             const uint32_t gi = (uint32_t)(ki >> gsh);
             const int32_t pi = (int32_t)((ki >> qb) & rmask);
@@ -608,6 +688,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
                 stb += 64;
                 sk = (stb + lane < A) ? K[stb + lane] : 0;
             }
+            TRACE(tr, 2, 3); TRACE(tr, 3, st);
             const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
             int32_t max_f = span, max_j = -1, n_skip = 0;
             int32_t jtop = i - 1;
@@ -618,12 +699,14 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
                 int32_t pj, qj, fj, ppj;
                 if (nsteps == 0) { pj = wp; qj = wq; fj = wf; ppj = wpp; }
                 else {
+                    TRACE(tr, 2, 4); TRACE(tr, 3, jtop);
                     if (nsteps == 1) vm_drain();      // f/pprev flushes of recent iterations
+                    pj = 0; qj = 0; fj = 0; ppj = -1;
                     if (inr) {
-                        const uint64_t kj = K[j];
+                        const uint64_t kj = K[CK(j, A)];
                         pj = (int32_t)((kj >> qb) & rmask); qj = (int32_t)(kj & qmask);
-                        fj = F[j]; ppj = PP[j];
-                    } else { pj = 0; qj = 0; fj = 0; ppj = -1; }
+                        fj = F[CK(j, A)]; ppj = PP[CK(j, A)];
+                    }
                 }
                 // comput_sc (lchain.rs:17-34); rid/rev equal for every j >= st
                 const int32_t dq = qi - qj, dr = pi - pj;
@@ -666,58 +749,66 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
                 n_skip = rdl(na, 63);
                 jtop -= 64;
             }
+            TRACE(tr, 2, 5);
             // clear this i's marks (all targets lie in [lo, i-1])
             if (i - 1 >= lo) {
                 const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
-                for (int32_t wd = w0 + lane; wd <= w1; wd += 64) ring[wd & (RING_WORDS - 1)] = 0;
+#pragma clang loop vectorize(disable) unroll(disable)
+                for (int32_t b0 = w0; b0 <= w1; b0 += 64) {
+                    const int32_t wd = b0 + lane;
+                    if (wd <= w1) ring[wd & (RING_WORDS - 1)] = 0;
+                }
                 wave_lds_sync();
             }
             // f[i], pprev[i]; fallback best_i = LAST index with max f
             if (max_f >= best_f) { best_f = max_f; best_i = i; }
             wp = shr1(wp, pi); wq = shr1(wq, qi); wf = shr1(wf, max_f); wpp = shr1(wpp, max_j);
-            if (((i + 1) & 63) == 0) { const int32_t j = i - lane; F[j] = wf; PP[j] = wpp; }
+            if (((i + 1) & 63) == 0) { const int32_t j = i - lane; F[CK(j, A)] = wf; PP[CK(j, A)] = wpp; }
         }
         {
             const int32_t rem = A & 63;
-            if (lane < rem) { const int32_t j = A - 1 - lane; F[j] = wf; PP[j] = wpp; }
+            if (lane < rem) { const int32_t j = A - 1 - lane; F[CK(j, A)] = wf; PP[CK(j, A)] = wpp; }
         }
         vm_drain();
-        pairs = (uint64_t)uni((int32_t)(uint32_t)pairs) | ((uint64_t)(uint32_t)uni((int32_t)(pairs >> 32)) << 32);
-        // ---- fallback chain walk (lchain.rs:162-171), chain ranges, rescue test
-        if (lane == 0) {
-            uint32_t* CB = a.chain + base;
-            int32_t idx = best_i, root = best_i, cm = 0;
-            while (idx >= 0 && cm < A) { CB[cm++] = (uint32_t)idx; root = idx; idx = PP[idx]; }
-            const uint64_t kb = K[best_i], kr = K[root];
-            const uint32_t g = (uint32_t)(kb >> gsh);
-            const int32_t qe = (int32_t)(kb & qmask) + 1;
-            int32_t qs = (int32_t)(kr & qmask) - (span - 1); if (qs < 0) qs = 0;
-            int32_t ts, te;
-            if (g == 2u * a.kl.n_seq) { ts = 0; te = -1; }    // Q19: rpos = p - 2^31 < 0
-            else {
-                te = (int32_t)((kb >> qb) & rmask) + 1;
-                ts = (int32_t)((kr >> qb) & rmask) - (span - 1); if (ts < 0) ts = 0;
-            }
-            ReadOut o = a.out[r];
-            if (P.pass == 0) { o = ReadOut{}; o.dp_pairs = 0; }
-            o.n_anchors = A; o.qlen = qlen;
-            o.score = best_f; o.cm = cm; o.qs = qs; o.qe = qe; o.ts = ts; o.te = te;
-            o.group = (int32_t)g; o.best_i = best_i;
-            int32_t fl = RF_MAPPED | (o.flags & RF_RESCUED);
-            if (g == 2u * a.kl.n_seq) fl |= RF_PANIC;
-            if (P.pass == 0) {
-                int32_t cov = qe - qs; if (cov < 0) cov = 0;
-                int32_t unc = qlen - cov; if (unc < 0) unc = 0;
-                if (unc > P.rescue_size || (float)cov < (float)qlen * P.rescue_ratio_f) fl |= RF_RESCUED;
-            }
-            o.flags = fl;
-            o.dp_pairs += pairs;
-            a.out[r] = o;
+        TRACE(tr, 2, 7);
+        // ---- fallback chain walk (lchain.rs:162-171), chain ranges, rescue test.
+        // All lanes walk together (same address each step, uniform loop).
+        uint32_t* CB = a.chain + base;
+        int32_t idx = best_i, root = best_i, cm = 0;
+        while (idx >= 0 && cm < A) {
+            if (lane == 0) CB[cm] = (uint32_t)idx;
+            ++cm; root = idx;
+            idx = uni(PP[CK(idx, A)]);
         }
+        const uint64_t kb = uni64(K[CK(best_i, A)]), kr = uni64(K[CK(root, A)]);
+        const uint32_t g = (uint32_t)(kb >> gsh);
+        const int32_t qe = (int32_t)(kb & qmask) + 1;
+        int32_t qs = (int32_t)(kr & qmask) - (span - 1); if (qs < 0) qs = 0;
+        int32_t ts, te;
+        if (g == 2u * a.kl.n_seq) { ts = 0; te = -1; }    // Q19: rpos = p - 2^31 < 0
+        else {
+            te = (int32_t)((kb >> qb) & rmask) + 1;
+            ts = (int32_t)((kr >> qb) & rmask) - (span - 1); if (ts < 0) ts = 0;
+        }
+        int32_t fl = RF_MAPPED | (flags0 & RF_RESCUED);
+        if (g == 2u * a.kl.n_seq) fl |= RF_PANIC;
+        if (P.pass == 0) {
+            int32_t cov = qe - qs; if (cov < 0) cov = 0;
+            int32_t unc = qlen - cov; if (unc < 0) unc = 0;
+            if (unc > P.rescue_size || (float)cov < (float)qlen * P.rescue_ratio_f) fl |= RF_RESCUED;
+        }
+        const uint64_t prev_pairs = P.pass == 0 ? 0ULL : uni64(a.out[r].dp_pairs);
+        if (lane == 0) {
+            ReadOut* O = a.out + r;
+            O->flags = fl; O->n_anchors = A; O->qlen = qlen;
+            O->score = best_f; O->cm = cm; O->qs = qs; O->qe = qe; O->ts = ts; O->te = te;
+            O->group = (int32_t)g; O->best_i = best_i;
+            O->dp_pairs = prev_pairs + pairs;
+        }
+        TRACE(tr, 2, 9);
     }
 }
 
-// ============================================================================
 // 6. dv inputs — paf_from_chain_with_primary (src/paf.rs:156-199): binary
 // search (Rust >= 1.82 slice::binary_search) of the first chain position among
 // the minimizer positions of the (idx.w, idx.k) sketch, then the greedy match.
@@ -731,18 +822,23 @@ __global__ __launch_bounds__(256) void k_dv(DvArgs a) {
     o.m_dv = (int32_t)m;
     o.flags &= ~RF_DV_FOUND;
     if (!(o.flags & RF_MAPPED) || (o.flags & RF_PANIC) || m == 0 || o.cm <= 0) { a.out[r] = o; return; }
+#ifdef MM2G_CHECKED
+    if (a.mz_base[r] + m > a.cap_mz || a.a_off[r] + (uint64_t)o.cm > a.cap_keys) { CK(a.mz_base[r] + m, 0); a.out[r] = o; return; }
+#endif
     const uint32_t* Y = a.mz_y + a.mz_base[r];
     const uint32_t* CB = a.chain + a.a_off[r];
     const uint64_t* K = a.keys + a.a_off[r];
+    const uint64_t An = a.a_off[r + 1] - a.a_off[r];
+    (void)An;
     const uint64_t qmask = (1ULL << a.kl.qb) - 1;
     const bool rev = (uint32_t)o.group >= a.kl.n_seq;
     const int32_t cm = o.cm, qlen = o.qlen, span = a.span;
     auto fwdq = [&](int32_t t) -> int32_t {   // t-th chain anchor in forward-query order
-        if (!rev) { const int32_t q = (int32_t)(K[CB[cm - 1 - t]] & qmask); return q; }
-        const int32_t q = (int32_t)(K[CB[t]] & qmask);
+        if (!rev) { const int32_t q = (int32_t)(K[CK(CB[cm - 1 - t], An)] & qmask); return q; }
+        const int32_t q = (int32_t)(K[CK(CB[t], An)] & qmask);
         return qlen - 1 - (q + 1 - span);
     };
-    auto mpos = [&](uint32_t j) -> int32_t { return (int32_t)(Y[j] >> 1); };
+    auto mpos = [&](uint32_t j) -> int32_t { return (int32_t)(Y[CK(j, m)] >> 1); };
     const int32_t first = fwdq(0);
     uint32_t size = m, b = 0;
     while (size > 1) { const uint32_t half = size / 2, mid = b + half; if (!(mpos(mid) > first)) b = mid; size -= half; }
@@ -834,11 +930,11 @@ int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
     LAUNCH_CHECK();
     return 0;
 }
-int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, hipStream_t st) {
+int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st) {
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_sort_small, dim3(n), dim3(256), 0, st, n, a_off, keys);
+    hipLaunchKernelGGL(k_sort_small, dim3(n), dim3(256), 0, st, n, a_off, keys, cap_keys);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_sort_large, dim3(n), dim3(1024), 0, st, n, a_off, keys, tmp);
+    hipLaunchKernelGGL(k_sort_large, dim3(n), dim3(1024), 0, st, n, a_off, keys, tmp, cap_keys);
     LAUNCH_CHECK();
     return 0;
 }
@@ -870,4 +966,16 @@ int launch_ix_build(const uint64_t* keys, const uint32_t* offs, const uint32_t* 
     hipLaunchKernelGGL(k_ix_build, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, st, keys, offs, ns, nk, tab, log2cap);
     LAUNCH_CHECK();
     return 0;
+}
+
+int mm2g_checked_read(unsigned long long out[4], hipStream_t st) {
+#ifdef MM2G_CHECKED
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return (int)e;
+    e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chk), sizeof(unsigned long long) * 4, 0, hipMemcpyDeviceToHost);
+    return (int)e;
+#else
+    (void)st; out[0] = out[1] = out[2] = out[3] = 0;
+    return 0;
+#endif
 }

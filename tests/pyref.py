@@ -1,0 +1,321 @@
+"""Independent pure-Python restatement of the reference Rust (small inputs only).
+
+TEST INFRASTRUCTURE: a second, separately written reading of
+/root/reference/src/*.rs used to cross-check the C++ oracle
+(oracle/mm2rs_oracle.cpp).  Integers are masked to the Rust widths where
+the Rust wraps; f32 arithmetic is emulated with numpy.float32 op by op.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+U64 = (1 << 64) - 1
+MAXU = U64
+f32 = np.float32
+
+
+def nt4(b: int) -> int:  # nt4.rs:2-10
+    return {ord("A"): 0, ord("a"): 0, ord("C"): 1, ord("c"): 1, ord("G"): 2, ord("g"): 2, ord("T"): 3, ord("t"): 3}.get(b, 4)
+
+
+def hash64(key: int, mask: int) -> int:  # sketch.rs:4-13
+    key = ((~key & U64) + (key << 21)) & U64 & mask
+    key ^= key >> 24
+    key = (key + (key << 3) + (key << 8)) & U64 & mask
+    key ^= key >> 14
+    key = (key + (key << 2) + (key << 4)) & U64 & mask
+    key ^= key >> 28
+    key = (key + (key << 31)) & U64 & mask
+    return key
+
+
+def sketch_sequence(seq: bytes, w: int, k: int, rid: int, is_hpc: bool):  # sketch.rs:29-100
+    assert len(seq) > 0 and 0 < w < 256 and 0 < k <= 28
+    out = []
+    shift1 = 2 * (k - 1)
+    mask = (1 << (2 * k)) - 1
+    kmer = [0, 0]
+    l = 0
+    buf_pos = 0
+    min_pos = 0
+    kmer_span = 0
+    buf = [(MAXU, MAXU)] * w
+    mn = (MAXU, MAXU)
+    tq = []
+    for i in range(len(seq)):
+        c = nt4(seq[i])
+        info = (MAXU, MAXU)
+        if c < 4:
+            if is_hpc:
+                skip_len = 1
+                if i + 1 < len(seq) and nt4(seq[i + 1]) == c:
+                    t = i + 2
+                    while t < len(seq) and nt4(seq[t]) == c:
+                        t += 1
+                    skip_len = t - i
+                tq.append(skip_len)
+                kmer_span += skip_len
+                if len(tq) > k:
+                    kmer_span -= tq.pop(0)
+            else:
+                kmer_span = l + 1 if l + 1 < k else k
+            kmer[0] = ((kmer[0] << 2) | c) & mask
+            kmer[1] = (kmer[1] >> 2) | ((3 ^ c) << shift1)
+            if kmer[0] != kmer[1]:
+                z = 0 if kmer[0] < kmer[1] else 1
+                l += 1
+                if l >= k and kmer_span < 256:
+                    info = ((hash64(kmer[z], mask) << 8) | kmer_span, (rid << 32) | (i << 1) | z)
+        else:
+            l = 0
+            tq = []
+            kmer_span = 0
+        buf[buf_pos] = info
+        if l == w + k - 1 and mn[0] != MAXU:
+            for j in list(range(buf_pos + 1, w)) + list(range(0, buf_pos)):
+                if mn[0] == buf[j][0] and buf[j][1] != mn[1]:
+                    out.append(buf[j])
+        if info[0] <= mn[0]:
+            if l >= w + k and mn[0] != MAXU:
+                out.append(mn)
+            mn = info
+            min_pos = buf_pos
+        elif buf_pos == min_pos:
+            if l >= w + k - 1 and mn[0] != MAXU:
+                out.append(mn)
+            mn = (MAXU, mn[1])
+            for j in list(range(buf_pos + 1, w)) + list(range(0, buf_pos + 1)):
+                if mn[0] >= buf[j][0]:
+                    mn = buf[j]
+                    min_pos = j
+            if l >= w + k - 1 and mn[0] != MAXU:
+                for j in list(range(buf_pos + 1, w)) + list(range(0, buf_pos + 1)):
+                    if mn[0] == buf[j][0] and mn[1] != buf[j][1]:
+                        out.append(buf[j])
+        buf_pos += 1
+        if buf_pos == w:
+            buf_pos = 0
+    if mn[0] != MAXU:
+        out.append(mn)
+    return out
+
+
+def filter_query_minimizers(mv, q_occ_max=10, q_occ_frac=0.01):  # seeds.rs:13-36
+    if len(mv) == 0 or q_occ_frac <= 0 or q_occ_max <= 0:
+        return list(mv)
+    if len(mv) <= q_occ_max:
+        return list(mv)
+    counts = {}
+    for m in mv:
+        counts[m[0] >> 8] = counts.get(m[0] >> 8, 0) + 1
+    cutoff = int(f32(len(mv)) * f32(q_occ_frac))
+    return [m for m in mv if not (counts[m[0] >> 8] > q_occ_max and counts[m[0] >> 8] > cutoff)]
+
+
+class Index:  # index.rs:28-154 (buckets with a dict as the HashMap)
+    def __init__(self, w, k, b, flag):
+        self.w, self.k, self.b, self.flag = w, k, b, flag
+        self.seq = []
+        self.B = [{"a": [], "p": [], "h": None} for _ in range(1 << b)]
+
+    @classmethod
+    def build(cls, records, w, k, b, flag):  # index.rs:427-475
+        idx = cls(w, k, b, flag)
+        mask = (1 << b) - 1
+        for rid, (name, s) in enumerate(records):
+            mv = sketch_sequence(s, w, k, rid, (flag & 1) != 0) if len(s) else []
+            idx.seq.append((name, len(s)))
+            for m in mv:
+                idx.B[(m[0] >> 8) & mask]["a"].append(m)
+        for bk in idx.B:
+            a = bk["a"]
+            if not a:
+                continue
+            a.sort(key=lambda m: m[0] >> 8)  # stable
+            h = {}
+            j = 0
+            while j < len(a):
+                e = j + 1
+                while e < len(a) and (a[e][0] >> 8) == (a[j][0] >> 8):
+                    e += 1
+                key_top = ((a[j][0] >> 8) >> b) << 1
+                if e - j == 1:
+                    h[key_top | 1] = a[j][1]
+                else:
+                    start = len(bk["p"])
+                    bk["p"].extend(sorted(m[1] for m in a[j:e]))
+                    h[key_top] = (start << 32) | (e - j)
+                j = e
+            bk["h"] = h
+            bk["a"] = []
+        return idx
+
+    def get(self, minier):
+        bk = self.B[minier & ((1 << self.b) - 1)]
+        if bk["h"] is None:
+            return None
+        key = (minier >> self.b) << 1
+        if key | 1 in bk["h"]:
+            return ("Single", bk["h"][key | 1])
+        if key in bk["h"]:
+            v = bk["h"][key]
+            off, n = v >> 32, v & 0xFFFFFFFF
+            return ("Multi", bk["p"][off:off + n])
+        return None
+
+    def calc_mid_occ(self, frac):
+        counts = []
+        for bk in self.B:
+            if bk["h"] is not None:
+                for kk, v in bk["h"].items():
+                    counts.append(1 if kk & 1 else v & 0xFFFFFFFF)
+        if not counts:
+            return 2 ** 31 - 1
+        counts.sort()
+        n = len(counts)
+        idx = min(int((1.0 - float(f32(frac))) * n), n - 1)
+        return counts[idx] + 1
+
+
+def i32(x):
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >> 31 else x
+
+
+def as_u64_from_i32(x):
+    return x & U64
+
+
+def push_anchor(r, m, qlen):  # seeds.rs:62-79
+    rid = (r >> 32) & 0xFFFFFFFF
+    rpos = i32((r >> 1) & 0xFFFFFFFF)
+    rstrand = r & 1
+    qpos = i32((m[1] >> 1) & 0xFFFFFFFF)
+    qstrand = m[1] & 1
+    qspan = m[0] & 0xFF
+    forward = rstrand == qstrand
+    x = ((rid << 32) | as_u64_from_i32(rpos)) if forward else ((1 << 63) | (rid << 32) | as_u64_from_i32(rpos))
+    if forward:
+        y = (qspan << 32) | as_u64_from_i32(qpos)
+    else:
+        y = (qspan << 32) | as_u64_from_i32(i32(qlen - (qpos + 1 - qspan) - 1))
+    return (x & U64, y & U64)
+
+
+def build_anchors_filtered(idx, mv, qlen, mid_occ):  # seeds.rs:42-60
+    a = []
+    for m in mv:
+        occ = idx.get(m[0] >> 8)
+        if occ is None:
+            continue
+        if occ[0] == "Single":
+            a.append(push_anchor(occ[1], m, qlen))
+        else:
+            if len(occ[1]) > mid_occ:
+                continue
+            for r in occ[1]:
+                a.append(push_anchor(r, m, qlen))
+    a.sort()
+    return a
+
+
+def qpos(a):
+    return i32(a[1] & 0xFFFFFFFF)
+
+
+def qspan(a):
+    return (a[1] >> 32) & 0xFF
+
+
+def rpos(a):
+    return i32(a[0] & 0xFFFFFFFF)
+
+
+def rev(a):
+    return (a[0] >> 63) != 0
+
+
+def rid(a):
+    return (a[0] >> 32) & 0x7FFFFFFF
+
+
+def mg_log2(x):
+    if x <= 1:
+        return f32(0.0)
+    return f32(np.log(f32(x))) / f32(math.log(2.0))
+
+
+def comput_sc(ai, aj, max_dist_x, max_dist_y, bw, gap, skip):  # lchain.rs:17-34
+    dq = i32(qpos(ai) - qpos(aj))
+    if dq <= 0 or dq > max_dist_x:
+        return None
+    dr = i32(rpos(ai) - rpos(aj))
+    if dr == 0 or dq > max_dist_y:
+        return None
+    dd = abs(dr - dq)
+    if dd > bw:
+        return None
+    dg = min(dr, dq)
+    q_span = qspan(aj)
+    sc = min(q_span, dg)
+    if dd != 0 or dg > q_span:
+        lin_pen = f32(gap) * f32(dd) + f32(skip) * f32(dg)
+        log_pen = mg_log2(dd + 1) if dd >= 1 else f32(0.0)
+        sc -= int(f32(lin_pen + f32(0.5) * log_pen))
+    return sc
+
+
+def chain_dp_all_dp(anchors, max_dist_x=5000, max_dist_y=5000, bw=500, max_iter=5000, gap=None, k=15, max_skip=25):
+    """The DP fill of chain_dp_all (lchain.rs:59-91): returns f, pprev, v."""
+    if gap is None:
+        gap = f32(f32(0.01) * f32(0.8)) * f32(k)
+    n = len(anchors)
+    max_dist_x = max(max_dist_x, bw)
+    max_dist_y = max(max_dist_y, bw)
+    f = [0] * n
+    v = [0] * n
+    t = [0] * n
+    pprev = [-1] * n
+    st = 0
+    for i in range(n):
+        while st < i and (rid(anchors[st]) != rid(anchors[i]) or rev(anchors[st]) != rev(anchors[i])
+                          or rpos(anchors[i]) > rpos(anchors[st]) + max_dist_x):
+            st += 1
+        max_j = -1
+        max_f = qspan(anchors[i])
+        start_j = i - max_iter if i - max_iter > st else st
+        n_skip = 0
+        for j in range(i - 1, start_j - 1, -1):
+            if rid(anchors[j]) != rid(anchors[i]) or rev(anchors[j]) != rev(anchors[i]):
+                continue
+            sc0 = comput_sc(anchors[i], anchors[j], max_dist_x, max_dist_y, bw, gap, 0.0)
+            if sc0 is not None:
+                sc = sc0 + f[j]
+                if sc > max_f:
+                    max_f = sc
+                    max_j = j
+                    if n_skip > 0:
+                        n_skip -= 1
+                elif t[j] == i:
+                    n_skip += 1
+                    if n_skip > max_skip:
+                        break
+                if pprev[j] >= 0:
+                    t[pprev[j]] = i
+        f[i] = max_f
+        pprev[i] = max_j
+        v[i] = v[max_j] if (max_j >= 0 and v[max_j] > max_f) else max_f
+    return f, pprev, v
+
+
+def fallback_chain(f, pprev, v):
+    """lchain.rs:162-173 (the only chain under min_cnt >= 2): last argmax."""
+    best_i = max(range(len(f)), key=lambda i: (f[i], i))
+    ch = []
+    i = best_i
+    while i >= 0:
+        ch.append(i)
+        i = pprev[i]
+    return ch[::-1], v[best_i]
