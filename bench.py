@@ -1,0 +1,290 @@
+"""bench.py — aligned Gbases/s (PAF out) of the MI355X mapping path.
+
+Workload (BASELINE.json metric): ONT-shaped 10 kb reads vs an hg38-shaped
+synthetic reference (24 contigs with GRCh38 primary lengths, Σ≈3.1 Gb,
+repeat families injected), index resident in HBM.  One step
+= the whole hot path over one batch of reads already resident in HBM:
+sketch -> query filter -> index lookup -> anchors -> sort -> chain DP
+(+rescue) -> epilogue -> results to host -> PAF text.  Index build/upload
+and mid_occ are outside the timed region.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py
+--gpus N): one process per GPU, each with its own replicated index and its
+own reads (weak scaling, no collective on the data path); barrier +
+synchronize around the timed region, max-over-ranks time, value = all
+ranks' bases / that time.
+
+Output: ONE JSON line on rank 0 with the driver contract fields plus
+"roofline" (dominant kernel, HIP events on the library stream) and
+"cpu_baseline" (the C++ oracle restatement of the reference align on a
+bounded sample of the same reads, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_COPY_GBS = 6290.0          # measured copy bandwidth (same guide)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--reads", type=int, default=10000, help="reads per GPU per step (metric: 10k x 10 kb)")
+    p.add_argument("--read-len", type=int, default=10000)
+    p.add_argument("--scale", type=float, default=1.0, help="reference size relative to hg38 (1.0 = 3.1 Gb)")
+    p.add_argument("--ref-seed", type=int, default=38)
+    p.add_argument("--read-seed", type=int, default=3)
+    p.add_argument("--threads", type=int, default=0, help="host threads for index build (0 = auto)")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    return p.parse_args()
+
+
+def host_threads(world: int) -> int:
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if n <= 0:
+        try:
+            n = len(os.sched_getaffinity(0))
+        except AttributeError:
+            n = os.cpu_count() or 8
+    return max(1, min(n, 64) // max(world, 1))
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import minimap2_rs_amd as M
+    from minimap2_rs_amd import _lib as L
+    from tools import simdata
+
+    lib = L.load()                               # libmm2g.so (fails loudly if missing)
+    if lib.mm2g_device_count() <= 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    thr = args.threads or host_threads(world)
+
+    # ---- reference + index (outside the timed region) ----------------------
+    t0 = time.time()
+    names, lens, gbuf = simdata.genome("hg38", args.scale, args.ref_seed, threads=thr)
+    log(f"rank {rank}: reference {lens.sum() / 1e9:.3f} Gb, {len(lens)} contigs in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr)
+    mid = max(idx.calc_mid_occ(2e-4), 10)       # main.rs:196-197
+    log(f"rank {rank}: index built in {time.time() - t0:.1f}s, stats {idx.stats()}, mid_occ {mid}")
+
+    # ---- reads (per rank: distinct seed) -----------------------------------
+    rbuf, roffs, _ = simdata.reads(gbuf, lens, args.reads, args.read_len, args.read_seed + rank)
+    rnames = [f"r{i}" for i in range(args.reads)]
+    n_bases = int(roffs[-1])
+
+    dev = M.Device(local)
+    t0 = time.time()
+    dev.upload_index(idx, mid)
+    t_up = time.time() - t0
+    t0 = time.time()
+    dev.set_reads_packed(rbuf, roffs)            # reads resident in HBM before the timed region
+    t_h2d = time.time() - t0
+    log(f"rank {rank}: index upload {t_up:.1f}s, reads H2D {t_h2d * 1e3:.1f} ms ({n_bases / 1e9:.3f} Gb)")
+
+    opts = M.map_opts()
+    res = (L.ReadResult * args.reads)()
+    nm_arr = (C.c_char_p * args.reads)(*[x.encode() for x in rnames])
+    paf_cap = 256 * args.reads + (1 << 20)
+    paf_buf = C.create_string_buffer(paf_cap)
+    h = dev._h
+    ih = idx._h
+
+    def step() -> int:
+        L.check(lib.mm2g_batch_map(h, C.byref(opts)), "batch_map")
+        L.check(lib.mm2g_batch_results(h, res, args.reads), "batch_results")
+        return L.check(lib.mm2g_format_paf(ih, res, nm_arr, args.reads, paf_buf, paf_cap), "format_paf")
+
+    for _ in range(args.warmup):
+        step()
+    paf_len = step() if args.warmup == 0 else None
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    dev.prof_enable(True)
+    dev.prof_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        paf_len = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = dev.prof()
+    dev.prof_enable(False)
+    cnt = dev.counters()                          # per batch (identical every step)
+
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        bt = torch.tensor([n_bases], dtype=torch.float64, device="cuda")
+        dist.all_reduce(bt, op=dist.ReduceOp.SUM)
+        total_bases = float(bt.item()) * args.steps
+    else:
+        total_bases = float(n_bases) * args.steps
+
+    value = total_bases / elapsed / 1e9
+    ms_per_step = elapsed / max(args.steps, 1) * 1e3
+    n_lines = paf_buf.raw[:paf_len].count(b"\n") if paf_len else 0
+
+    # ---- roofline of the dominant kernel (HIP events on the library stream) --
+    # Algorithmic bytes per unit (DESIGN.md "Roofline accounting").
+    A, Ar, m, mk = cnt["anchors"], cnt["rescued_anchors"], cnt["minimizers"], cnt["kept_minimizers"]
+    L_tot = cnt["bases"]
+    kernel_bytes = {
+        "sketch": L_tot + 12 * m,                       # ASCII in; (x 8 B, y 4 B) per minimizer out
+        "filter": 9 * m,                                # x in, keep out
+        "seed_count": 9 * m + 16 * mk + 8 * m,          # keep+x in, 16 B table entry per kept, (n, poff) out
+        "seed_write": 12 * m + 16 * A,                  # (n, poff, y) in; 8 B position in + 8 B key out per anchor
+        "sort": 16 * A,                                 # each 8 B key read once and written once
+        "chain_dp": 24 * A,                             # 16 B anchor in + 8 B f/pprev out per anchor
+        "chain_dp_rescue": 24 * Ar,
+    }
+    per_kernel = {}
+    for name, (ms, calls) in prof.items():
+        if calls <= 0:
+            continue
+        per_kernel[name] = {"ms_per_step": ms / args.steps, "launches_per_step": calls / args.steps}
+    # k_chain_dp = both DP passes (one kernel symbol, as rocprofv3 sees it)
+    chain_ms = prof.get("chain_dp", (0.0, 0))[0] + prof.get("chain_dp_rescue", (0.0, 0))[0]
+    chain_calls = prof.get("chain_dp", (0.0, 0))[1] + prof.get("chain_dp_rescue", (0.0, 0))[1]
+    groups = {"k_chain_dp": (chain_ms, chain_calls, (kernel_bytes["chain_dp"] + kernel_bytes["chain_dp_rescue"]) * args.steps)}
+    for nm in ("sketch", "filter", "seed_count", "seed_write", "sort"):
+        ms, calls = prof.get(nm, (0.0, 0))
+        groups[nm] = (ms, calls, kernel_bytes[nm] * args.steps)
+    dom = max(groups, key=lambda g: groups[g][0])
+    d_ms, d_calls, d_bytes = groups[dom]
+    avg_s = d_ms / 1e3 / max(d_calls, 1)
+    bytes_per_launch = d_bytes / max(d_calls, 1)
+    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    roofline = {
+        "bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+        "avg_launch_ms": round(avg_s * 1e3, 4), "alg_bytes_per_launch": int(bytes_per_launch),
+    }
+    # whole-path algorithmic bytes (SURVEY.md §8d B(read) summed) over the step time
+    B_path = (L_tot + 3) // 4 + 16 * mk + 48 * A + 24 * Ar
+    path_gbs = B_path * args.steps / elapsed / 1e9 if world == 1 else None
+    dp_pairs_s = cnt["dp_pairs"] * args.steps / elapsed if world == 1 else None
+
+    # ---- CPU baseline: the oracle restatement on a bounded sample (rank 0, N=1) ---
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu, parity = cpu_baseline(args, names, lens, gbuf, rbuf, roffs, rnames, mid, thr, paf_buf.raw[:paf_len])
+
+    if rank == 0:
+        line = {
+            "metric": "aligned Gbases/sec (PAF out), 10k×10kb ONT reads vs hg38, 1/2/4/8 GPUs",
+            "value": round(value, 6),
+            "unit": "Gbases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (hg38-shaped reference, seeded ONT-shaped reads; SURVEY.md §8d)",
+            "config": {
+                "workload": f"hg38-shaped {lens.sum() / 1e9:.2f} Gb reference index in HBM + "
+                            f"{args.reads}x{args.read_len // 1000} kb ONT reads per GPU per step",
+                "reads_per_gpu_step": args.reads, "read_len": args.read_len, "ref_bases": int(lens.sum()),
+                "mid_occ": mid, "parallelism": f"reads sharded x{world} (index replicated)",
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "extra": {
+                "paf_lines_per_step": n_lines,
+                "per_kernel": per_kernel,
+                "counters_per_step": cnt,
+                "path_alg_GBps": round(path_gbs, 3) if path_gbs else None,
+                "path_frac_of_8TBps": round(path_gbs / HBM_PEAK_GBS, 6) if path_gbs else None,
+                "dp_pairs_per_s": dp_pairs_s,
+                "index_upload_s": round(t_up, 3),
+                "reads_h2d_ms": round(t_h2d * 1e3, 3),
+                "pcie_inclusive_gbases_s": round(n_bases / (ms_per_step / 1e3 + t_h2d) / 1e9, 6) if world == 1 else None,
+                "parity_vs_oracle": parity,
+            },
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, names, lens, gbuf, rbuf, roffs, rnames, mid, thr, gpu_paf: bytes):
+    """Time oracle/ (the C++ restatement of the reference align, 1 thread) on
+    the first reads of the same batch; check its PAF against the GPU's."""
+    from oracle import oracle as O
+    import tempfile
+
+    O.set_quiet(True)
+    t0 = time.time()
+    oi = O.OIndex.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr)
+    log(f"oracle index built in {time.time() - t0:.1f}s")
+    # calibrate on a few reads, then size the sample to ~cpu_seconds
+    n_cal = min(10, args.reads)
+    _, _, t_cal = oi.align_buffer(rnames[:n_cal], rbuf, roffs[: n_cal + 1], None, mid_occ=mid, threads=1)
+    per_read = max(t_cal / n_cal, 1e-4)
+    n_s = int(min(args.reads, max(n_cal, args.cpu_seconds / per_read)))
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "cpu.paf")
+        n_lines, counts, t1 = oi.align_buffer(rnames[:n_s], rbuf, roffs[: n_s + 1], out, mid_occ=mid, threads=1)
+        cpu_lines = open(out, "rb").read().splitlines()
+    bases = int(roffs[n_s] - roffs[0])
+    v1 = bases / t1 / 1e9
+    # all-cores variant (OpenMP-style dynamic over reads): same sample
+    _, _, tN = oi.align_buffer(rnames[:n_s], rbuf, roffs[: n_s + 1], None, mid_occ=mid, threads=thr)
+    vN = bases / tN / 1e9
+    log(f"cpu baseline: {n_s} reads, 1 thread {t1:.1f}s ({v1 * 1e3:.3f} Mb/s); {thr} threads {tN:.1f}s")
+    # parity: GPU PAF lines for the sampled reads vs the oracle's
+    want = set(rnames[:n_s])
+    gpu_lines = [ln for ln in gpu_paf.splitlines() if ln.split(b"\t", 1)[0].decode() in want]
+    parity = {"reads": n_s, "gpu_lines": len(gpu_lines), "cpu_lines": len(cpu_lines),
+              "identical": gpu_lines == cpu_lines, "cpu_panics": counts.get("panics")}
+    oi.close()
+    cpu = {"value": round(v1, 9), "unit": "Gbases/s", "cores": 1, "kind": "port",
+           "sample": f"first {n_s} of the step's {args.reads} reads ({bases / 1e6:.1f} Mb), oracle/ C++ restatement "
+                     f"of mm2rs align, 1 thread, index build excluded",
+           "all_cores": {"value": round(vN, 9), "cores": thr}}
+    return cpu, parity
+
+
+if __name__ == "__main__":
+    main()

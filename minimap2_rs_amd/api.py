@@ -74,6 +74,22 @@ class Index:
         return cls(h.value)
 
     @classmethod
+    def build_from_buffer(cls, names: Optional[Sequence[str]], buf: np.ndarray, lens: np.ndarray, w: int = 10, k: int = 15,
+                          b: int = 14, flag: int = 0, threads: int = 8) -> "Index":
+        """Index from sequences concatenated in one uint8 buffer (pointers into it; no copies)."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        lv = np.ascontiguousarray(lens, dtype=np.uint64)
+        n = len(lv)
+        starts = np.concatenate([[0], np.cumsum(lv)[:-1]]).astype(np.uint64) if n else np.zeros(0, np.uint64)
+        base = buf.ctypes.data
+        ptrs = (C.c_void_p * max(n, 1))(*[base + int(x) for x in starts])
+        nm = (C.c_char_p * max(n, 1))(*[x.encode() for x in names]) if names is not None else None
+        h = C.c_void_p()
+        check(load().mm2g_index_build_seqs(n, nm, ptrs, lv.ctypes.data_as(L._P64), w, k, b, flag, threads, C.byref(h)),
+              "build_from_buffer")
+        return cls(h.value)
+
+    @classmethod
     def load_from_mmi(cls, path: str) -> "Index":
         h = C.c_void_p()
         check(load().mm2g_index_load_mmi(path.encode(), C.byref(h)), "load_from_mmi")

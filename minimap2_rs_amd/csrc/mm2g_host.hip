@@ -429,7 +429,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->a_cnt, uint32_t, n + 1, a_cnt); ENSURE(c->a_off, uint64_t, n + 1, a_off);
     SeedArgs sa{n, (const uint64_t*)c->rd_off.p, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, (const uint32_t*)c->mz_y.p, keep,
                 (const IxEntry*)c->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k,
-                0, c->ix_pos.cap / 8, mcap};
+                0, c->ix_pos.cap / 8, mcap, out};
     {
         ProfScope ps(c, "seed_count");
         LCHK(launch_seed_count(sa, grid_for(n), c->stream));
@@ -544,6 +544,7 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
         const ReadOut& o = c->h_out[i];
         cnt[4] += (o.flags & RF_RESCUED) ? (uint64_t)o.n_anchors : 0;
         cnt[5] += o.dp_pairs;
+        cnt[2] += (uint64_t)o.m_kept;
         if (i >= n || !res) continue;
         mm2g_read_result& r = res[i];
         memset(&r, 0, sizeof r);

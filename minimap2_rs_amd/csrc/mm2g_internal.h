@@ -33,7 +33,7 @@ struct ReadOut {
     int32_t dv_st, dv_en;
     int32_t m_dv;
     int32_t qlen;
-    int32_t pad;
+    int32_t m_kept;        // minimizers kept by the query filter
     uint64_t dp_pairs;     // inner-loop j evaluations (all passes)
 };
 static_assert(sizeof(ReadOut) == 72, "ReadOut layout");
@@ -95,6 +95,7 @@ struct SeedArgs {
     uint64_t* keys;
     KeyLayout kl; int span;
     uint64_t cap_keys, cap_pos, cap_mz;   // bounds for the MM2G_CHECKED build
+    ReadOut* out;                         // m_kept
 };
 struct ChainArgs {
     uint32_t n;

@@ -420,11 +420,12 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
         const uint64_t mb = uni64(a.mz_base[r]);
         const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
-        uint32_t acc = 0;
+        uint32_t acc = 0, kept = 0;
         for (uint32_t b0 = 0; b0 < m; b0 += 64) {
             const uint32_t i = b0 + lane;
             const bool act = i < m;
             bool done = !(act && a.keep[mb + i]);
+            kept += done ? 0u : 1u;
             const uint64_t h = act ? (a.mz_x[mb + i] >> 8) : 0;
             uint32_t sl = ix_slot(h, a.log2cap), n = 0, off = 0;
             while (any(!done)) {
@@ -440,7 +441,8 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
             acc += n;
         }
         acc = wave_sum(acc);
-        if (lane == 0) a.a_cnt[r] = acc;
+        kept = wave_sum(kept);
+        if (lane == 0) { a.a_cnt[r] = acc; a.out[r].m_kept = (int32_t)kept; }
     }
 }
 

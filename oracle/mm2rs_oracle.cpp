@@ -33,6 +33,7 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+#include <atomic>
 #include <chrono>
 
 namespace orc {
@@ -846,6 +847,7 @@ static ChainParams default_chain_params(int32_t k) {
 }
 
 // Per-read accounting the bench uses for algorithmic bytes
+static bool g_quiet = false;   // orc_set_quiet: silence per-read panic notes (bench)
 struct ReadCounts { u64 m_all = 0, m_kept = 0, anchors = 0, rescued = 0, inner_iters = 0, lines = 0, panics = 0; };
 
 struct AlignOpts {
@@ -890,7 +892,7 @@ static void align_one(const Index& idx, int32_t mid_occ, const AlignOpts& o, con
         } else if (rec.panic) {
             // The reference aborts the whole process here; per-read concatenation
             // semantics: this read yields no line (and is counted).
-            fprintf(stderr, "oracle: read %s: reference panics (index out of bounds: rid 2147483647)\n", qname.c_str());
+            if (!g_quiet) fprintf(stderr, "oracle: read %s: reference panics (index out of bounds: rid 2147483647)\n", qname.c_str());
             if (rc) rc->panics += 1;
             break;
         }
@@ -1043,6 +1045,69 @@ long long orc_align_fasta(void* idx, const char* reads_fa, const char* out_path,
     }
     if (counts) { counts[0] = rc.m_all; counts[1] = rc.m_kept; counts[2] = rc.anchors; counts[3] = rc.rescued; counts[4] = rc.inner_iters; counts[5] = rc.lines; counts[6] = rc.panics; }
     return (long long)lines.size();
+}
+
+void orc_set_quiet(int q) { g_quiet = q != 0; }
+
+// build_index_from_fasta (src/index.rs:427-475) on in-memory records
+// (bench.py: avoids a multi-GB FASTA round trip for the hg38-shaped genome).
+void* orc_index_build_seqs(int n, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens, int w, int k, int b,
+                           int flag, int nthreads) {
+    std::vector<FastaRec> recs((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        recs[i].name = names && names[i] ? names[i] : "";
+        recs[i].seq.assign((const char*)seqs[i], (size_t)lens[i]);
+    }
+    return build_index_from_recs(recs, w, k, b, flag, nthreads);
+}
+
+// The Align flow (src/main.rs:189-230) over in-memory reads; the mapping loop
+// alone is timed (index and mid_occ excluded).  nthreads > 1
+// hands reads out dynamically (the reference align is single-threaded; this
+// is the all-cores variant of the CPU baseline).  Lines go to out_path when
+// given (in read order).
+long long orc_align_seqs(void* idx, int n, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens,
+                         const char* out_path, const int* oi, const float* of, int mid_occ, int nthreads, uint64_t* counts,
+                         double* time_s) {
+    Index* I = (Index*)idx;
+    AlignOpts o;
+    o.w = oi[0]; o.k = oi[1]; o.max_gap = oi[2]; o.bw = oi[3]; o.bw_long = oi[4]; o.min_cnt = oi[5]; o.min_chain_score = oi[6]; o.best_n = (size_t)oi[7];
+    o.frac = of[0]; o.mask_level = of[1]; o.pri_ratio = of[2];
+    if (mid_occ < 0) { mid_occ = I->calc_mid_occ(o.frac); if (mid_occ < 10) mid_occ = 10; }
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::vector<std::string>> per(n > 0 ? (size_t)n : 0);
+    std::vector<ReadCounts> rcs((size_t)nthreads);
+    std::atomic<int> next{0};
+    auto worker = [&](int t) {
+        for (;;) {
+            const int r = next.fetch_add(1);
+            if (r >= n) break;
+            if (lens[r] == 0) continue;   // reference asserts (sketch.rs:40)
+            align_one(*I, mid_occ, o, names ? std::string(names[r]) : std::string("*"), seqs[r], (size_t)lens[r], per[r], &rcs[t]);
+        }
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    if (nthreads == 1) worker(0);
+    else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; ++t) th.emplace_back(worker, t);
+        for (auto& x : th) x.join();
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    if (time_s) *time_s = std::chrono::duration<double>(t1 - t0).count();
+    ReadCounts rc;
+    long long nl = 0;
+    for (auto& c : rcs) {
+        rc.m_all += c.m_all; rc.m_kept += c.m_kept; rc.anchors += c.anchors; rc.rescued += c.rescued;
+        rc.inner_iters += c.inner_iters; rc.lines += c.lines; rc.panics += c.panics;
+    }
+    FILE* f = nullptr;
+    if (out_path) { f = (strcmp(out_path, "-") == 0) ? stdout : fopen(out_path, "w"); if (!f) return -1; }
+    for (auto& v : per)
+        for (auto& l : v) { ++nl; if (f) { fputs(l.c_str(), f); fputc('\n', f); } }
+    if (f && f != stdout) fclose(f);
+    if (counts) { counts[0] = rc.m_all; counts[1] = rc.m_kept; counts[2] = rc.anchors; counts[3] = rc.rescued; counts[4] = rc.inner_iters; counts[5] = rc.lines; counts[6] = rc.panics; }
+    return nl;
 }
 
 // Pen LUT value as the reference computes it inline (comput_sc), for LUT parity tests.

@@ -58,6 +58,12 @@ def lib() -> C.CDLL:
         L.orc_align_fasta.restype = C.c_longlong
         L.orc_align_fasta.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_float), C.c_int,
                                       _P64, C.POINTER(C.c_double)]
+        L.orc_index_build_seqs.restype = C.c_void_p
+        L.orc_index_build_seqs.argtypes = [C.c_int, C.c_void_p, C.c_void_p, _P64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_align_seqs.restype = C.c_longlong
+        L.orc_align_seqs.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, _P64, C.c_char_p, C.POINTER(C.c_int),
+                                     C.POINTER(C.c_float), C.c_int, C.c_int, _P64, C.POINTER(C.c_double)]
+        L.orc_set_quiet.argtypes = [C.c_int]
         L.orc_pen.restype = C.c_int
         L.orc_pen.argtypes = [C.c_int, C.c_int, C.c_int, C.c_float]
         L.orc_default_gap.restype = C.c_float
@@ -91,6 +97,16 @@ class OIndex:
     @classmethod
     def build(cls, fasta: str, w: int = 10, k: int = 15, b: int = 14, flag: int = 0, threads: int = 8) -> "OIndex":
         h = lib().orc_index_build(fasta.encode(), w, k, b, flag, threads)
+        if not h:
+            raise RuntimeError("oracle index build failed")
+        return cls(h)
+
+    @classmethod
+    def build_from_buffer(cls, names, buf: np.ndarray, lens: np.ndarray, w: int = 10, k: int = 15, b: int = 14, flag: int = 0,
+                          threads: int = 8) -> "OIndex":
+        """Index from sequences concatenated in one uint8 buffer (no copies on the Python side)."""
+        ptrs, lv, nm, _keep = _seq_views(names, buf, lens)
+        h = lib().orc_index_build_seqs(len(lv), nm, ptrs, lv.ctypes.data_as(_P64), w, k, b, flag, threads)
         if not h:
             raise RuntimeError("oracle index build failed")
         return cls(h)
@@ -172,6 +188,40 @@ class OIndex:
                                   C.byref(t))
         keys = ["m_all", "m_kept", "anchors", "rescued_anchors", "inner_iters", "lines", "panics"]
         return n, dict(zip(keys, list(cnt))), t.value
+
+
+    def align_buffer(self, names, buf: np.ndarray, offs: np.ndarray, out_path: Optional[str] = None, w: int = 10, k: int = 15,
+                     mid_occ: int = -1, threads: int = 1, max_gap: int = 5000, bw: int = -1, bw_long: int = -1, min_cnt: int = 3,
+                     min_chain_score: int = 40, best_n: int = 5, frac: float = 2e-4, mask_level: float = 0.5, pri_ratio: float = 0.8):
+        """Align flow over reads concatenated in buf (offsets offs[n+1]) -> (#lines, counts, seconds of mapping)."""
+        offs = np.asarray(offs, dtype=np.uint64)
+        lens = (offs[1:] - offs[:-1]).astype(np.uint64)
+        ptrs, lv, nm, _keep = _seq_views(names, buf, lens, offs[:-1])
+        oi = (C.c_int * 10)(w, k, max_gap, bw, bw_long, min_cnt, min_chain_score, best_n, 0, 0)
+        of = (C.c_float * 3)(frac, mask_level, pri_ratio)
+        cnt = (C.c_uint64 * 7)()
+        t = C.c_double()
+        n = lib().orc_align_seqs(self.h, len(lv), nm, ptrs, lv.ctypes.data_as(_P64), out_path.encode() if out_path else None,
+                                 oi, of, mid_occ, threads, cnt, C.byref(t))
+        keys = ["m_all", "m_kept", "anchors", "rescued_anchors", "inner_iters", "lines", "panics"]
+        return n, dict(zip(keys, list(cnt))), t.value
+
+
+def set_quiet(q: bool = True) -> None:
+    lib().orc_set_quiet(1 if q else 0)
+
+
+def _seq_views(names, buf: np.ndarray, lens, starts=None):
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    lv = np.ascontiguousarray(lens, dtype=np.uint64)
+    if starts is None:
+        starts = np.concatenate([[0], np.cumsum(lv)[:-1]]).astype(np.uint64) if len(lv) else np.zeros(0, np.uint64)
+    base = buf.ctypes.data
+    ptrs = (C.c_void_p * max(len(lv), 1))(*[base + int(s) for s in starts])
+    nm = None
+    if names is not None:
+        nm = (C.c_char_p * max(len(lv), 1))(*[x.encode() for x in names])
+    return ptrs, lv, nm, (buf,)
 
 
 def chain_dp(anchors_xy: np.ndarray, k: int = 15, max_gap: int = 5000, bw: int = 500, max_iter: int = 5000,
