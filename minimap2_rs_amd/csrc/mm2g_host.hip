@@ -74,7 +74,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, dv_separate = false;
@@ -382,6 +382,9 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     const int32_t mdx0 = std::max(o->max_gap, o->bw), mdx1 = std::max(o->max_gap, o->bw_long);
     const int lut_need = std::max(o->bw, o->bw_long) + 1;
     if (lut_need > 60000) return set_err(MM2G_E_UNSUP, "bandwidth > 59999 not supported");
+    // rpos_j + max_dist_x is i32 in the reference; keep it from wrapping (DESIGN.md Q-envelope)
+    if ((uint64_t)c->hidx->max_len + (uint64_t)std::max(mdx0, mdx1) >= (1ULL << 31))
+        return set_err(MM2G_E_UNSUP, "reference length + max gap must stay below 2^31");
     HIPCHK(hipSetDevice(c->device));
     const HostIndex& H = *c->hidx;
     const uint32_t n = c->n_reads;
@@ -465,7 +468,13 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ChainKParams P{};
     P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
     P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
-    const int chain_blocks = std::max(1, std::min((int)((n + 3) / 4), 2048));
+    // heaviest reads first; grid = what is co-resident (one wave per read, static hand-out)
+    uint32_t* order;
+    ENSURE(c->order, uint32_t, n, order);
+    LCHK(launch_read_order(n, a_cnt, order, c->stream));
+    int max_blocks = chain_max_blocks(P.lut_n);
+    if (max_blocks <= 0) max_blocks = 2048;
+    const int chain_blocks = std::max(1, std::min((int)((n + 3) / 4), max_blocks));
     uint32_t* trace_h = nullptr; uint32_t* trace_d = nullptr;
 #ifdef MM2G_CHECKED
     if (g_sync_each) {
@@ -475,7 +484,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         HIPCHK(hipHostGetDevicePointer((void**)&trace_d, trace_h, 0));
     }
 #endif
-    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work, std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, trace_d};
+    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work, std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, trace_d, order};
     auto dump_trace = [&](const char* what) {
         if (!trace_h) return;
         std::vector<uint64_t> ho(n + 1);

@@ -109,6 +109,7 @@ struct ChainArgs {
     uint32_t* work;
     uint64_t cap_keys;
     uint32_t* trace;    // MM2G_CHECKED: host-mapped per-wave progress {read, i, phase, aux}
+    const uint32_t* order;   // reads in hand-out order (heaviest first); null = identity
 };
 struct DvArgs {
     uint32_t n;
@@ -131,6 +132,8 @@ int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp
 // MM2G_CHECKED builds: first recorded bounds violation {line, index, cap}; 0 = none
 int mm2g_checked_read(unsigned long long out[4], hipStream_t st);
 int launch_chain(const mm2g::ChainArgs& a, int n_blocks, hipStream_t st);
+int chain_max_blocks(int lut_n);   // co-resident workgroups of k_chain_dp on the current device
+int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStream_t st);
 int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st);
 int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, hipStream_t st);

@@ -606,23 +606,58 @@ __global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t*
 }
 
 // ============================================================================
-// ============================================================================
 // 5. CHAIN DP — chain_dp_all (src/lchain.rs:59-91) + the fallback chain
 // (lchain.rs:162-173) + chain_qrange/trange (178-200) + the rescue test of
 // rescue_long_join (316-330).
 //
-// One wave per read, anchors i in order.  For each i the j-loop runs 64
-// predecessors per step (lane l <-> j = jtop - l, reference processing order):
-//   valid_j   comput_sc (lchain.rs:17-34) with the integer pen LUT (DESIGN Q6)
-//   marks     t[pprev[j]] = i  -> one bit in an LDS ring (targets >= lo only)
-//   max_f     strict '>' => exclusive prefix-max scan seeded with max_f
-//   n_skip    ops x->max(x-1,0) | x->x+1 | id compose as x->max(x+a,b):
-//             inclusive scan, break = first '+1' lane with n_skip > max_skip
-// The 64 newest anchors (j = i-1-lane) live in registers (shifted one lane per
-// i); deeper steps read keys/f/pprev from HBM (f/pprev flushed every 64 i).
+// One wave per read; anchors are taken in blocks of 64.
+//   isolated  anchor i has no candidate predecessor (st(i) == i) iff i == 0,
+//             or i-1 lies in another (rid, strand) group, or
+//             rpos_i > rpos_{i-1} + max_dist_x (keys are sorted by group and
+//             rpos, so i-1 is the closest candidate).  Then the reference's
+//             j-loop is empty: f = span, pprev = -1, no marks.  A ballot
+//             finds these per block and resolves them in bulk.
+//   others    sequential, in order.  For each i the j-loop runs 64
+//             predecessors per step (lane l <-> j = jtop - l, the reference's
+//             processing order):
+//     valid_j   comput_sc (lchain.rs:17-34) with the integer pen LUT (DESIGN Q6)
+//     marks     t[pprev[j]] = i  -> one bit in an LDS ring (targets >= lo only)
+//     max_f     strict '>' => exclusive prefix-max (DPP scan) seeded with max_f
+//     n_skip    ops x->max(x-1,0) | x->x+1 | id compose as x->max(x+a,b):
+//               DPP scan only when some lane is a '+1'; break = first '+1'
+//               lane with n_skip > max_skip
+// The newest RK anchors (key, f, pprev) live in a per-wave LDS ring; older
+// predecessors (deep windows) are read from HBM, where f/pprev are flushed at
+// the end of every block.  Keys are prefetched one block ahead.
 // ============================================================================
 constexpr int DP_NW = 4;          // waves per workgroup
 constexpr int RING_WORDS = 256;   // 8192-bit mark ring (max_iter <= 8000)
+constexpr int RK = 256;           // anchor ring entries per wave (power of two, >= 256)
+static_assert((RK & (RK - 1)) == 0 && RK >= 256, "anchor ring size");
+
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+DEVI int32_t dpp(int32_t old, int32_t src) { return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, BANK_MASK, false); }
+// inclusive max-scan over the wave (row_shr 1/2/4/8, row_bcast 15/31)
+DEVI int32_t scan_max(int32_t v) {
+    v = max(v, dpp<0x111>(INT_MIN, v)); v = max(v, dpp<0x112>(INT_MIN, v));
+    v = max(v, dpp<0x114>(INT_MIN, v)); v = max(v, dpp<0x118>(INT_MIN, v));
+    v = max(v, dpp<0x142, 0xa>(INT_MIN, v)); v = max(v, dpp<0x143, 0xc>(INT_MIN, v));
+    return v;
+}
+// lane l <- lane l-1, lane 0 <- old0 (wave_shr:1)
+DEVI int32_t shr1_dpp(int32_t v, int32_t old0) { return dpp<0x138>(old0, v); }
+// composition scan of x -> max(x + a, b) in lane order (earlier applied first)
+DEVI void scan_nskip(int32_t& a, int32_t& b) {
+    constexpr int32_t NEG = -(1 << 29);
+#define NS_STEP(CTRL, RM)                                                   \
+    {                                                                       \
+        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
+        b = max(ob + a, b); a = oa + a;                                     \
+    }
+    NS_STEP(0x111, 0xf) NS_STEP(0x112, 0xf) NS_STEP(0x114, 0xf) NS_STEP(0x118, 0xf)
+    NS_STEP(0x142, 0xa) NS_STEP(0x143, 0xc)
+#undef NS_STEP
+}
 
 __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -630,22 +665,25 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
     int16_t* lut = (int16_t*)smem;
     const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
     uint32_t* rings = (uint32_t*)(smem + lut_bytes);
+    uint64_t* rkeys = (uint64_t*)(rings + DP_NW * RING_WORDS);
+    int2* rfps = (int2*)(rkeys + DP_NW * RK);
     for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
     for (int i = threadIdx.x; i < DP_NW * RING_WORDS; i += blockDim.x) rings[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wv = wave_id();
     uint32_t* ring = rings + wv * RING_WORDS;
+    uint64_t* rkey = rkeys + wv * RK;
+    int2* rfp = rfps + wv * RK;
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const uint32_t gsh = rb + qb;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
     uint32_t* tr = (a.trace && lane == 0) ? a.trace + 4 * (blockIdx.x * DP_NW + wv) : nullptr;
     (void)tr;
-    // Static, wave-uniform assignment of reads (r is an SGPR-derived loop
-    // counter; a lane-0 atomic work queue here was mis-structured by the
-    // compiler, see the control-flow rule above).
+    // Static, wave-uniform assignment of reads in `order` (heaviest first).
     const uint32_t nwaves = gridDim.x * DP_NW;
-    for (uint32_t r = blockIdx.x * DP_NW + wv; r < a.n; r += nwaves) {
+    for (uint32_t t = blockIdx.x * DP_NW + wv; t < a.n; t += nwaves) {
+        const uint32_t r = a.order ? (uint32_t)uni((int32_t)a.order[t]) : t;
         TRACE(tr, 0, r); TRACE(tr, 2, 1);
         const int32_t flags0 = uni(a.out[r].flags);
         if (P.pass == 1 && !(flags0 & RF_RESCUED)) continue;
@@ -665,111 +703,141 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
 #endif
         const uint64_t* K = a.keys + base;
         int32_t* F = a.f + base; int32_t* PP = a.pp + base;
-        uint64_t ak = lane < A ? K[lane] : 0;
-        int32_t stb = 0, st = 0;
-        uint64_t sk = ak;
-        int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
+        int32_t st = 0, stb = INT_MIN / 2, skv = INT_MIN / 2;   // st window [stb, stb+63], keys valid up to skv
+        uint64_t sk = 0;
         int32_t best_f = INT_MIN, best_i = -1;
         uint64_t pairs = 0;
-        for (int32_t i = 0; i < A; ++i) {
-            if ((i & 63) == 0 && i) ak = (i + lane < A) ? K[i + lane] : 0;
-            TRACE(tr, 1, i); TRACE(tr, 2, 2);
-            const uint64_t ki = rdl64(ak, i & 63);
-            const uint32_t gi = (uint32_t)(ki >> gsh);
-            const int32_t pi = (int32_t)((ki >> qb) & rmask);
-            const int32_t qi = (int32_t)(ki & qmask);
-            // ---- st (lchain.rs:75): first j in i's group with rpos_i <= rpos_j + max_dist_x
-            for (;;) {
-                const int32_t j = stb + lane;
-                const uint32_t gj = (uint32_t)(sk >> gsh);
-                const int32_t pj = (int32_t)((sk >> qb) & rmask);
-                const bool cand = j >= st && j <= i;
-                const bool stop = cand && (j == i || (gj == gi && !(pi > (int32_t)((uint32_t)pj + (uint32_t)maxdx))));
-                const uint64_t m = ballot(stop);
-                if (m) { st = stb + ctz64(m); break; }
-                stb += 64;
-                sk = (stb + lane < A) ? K[stb + lane] : 0;
-            }
-            TRACE(tr, 2, 3); TRACE(tr, 3, st);
-            const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
-            int32_t max_f = span, max_j = -1, n_skip = 0;
-            int32_t jtop = i - 1;
-            int nsteps = 0;
-            while (jtop >= lo) {
-                const int32_t j = jtop - lane;
-                const bool inr = j >= lo;
-                int32_t pj, qj, fj, ppj;
-                if (nsteps == 0) { pj = wp; qj = wq; fj = wf; ppj = wpp; }
-                else {
-                    TRACE(tr, 2, 4); TRACE(tr, 3, jtop);
-                    if (nsteps == 1) vm_drain();      // f/pprev flushes of recent iterations
-                    pj = 0; qj = 0; fj = 0; ppj = -1;
+        uint32_t prev_lo = 0, prev_hi = 0;        // key of anchor i0-1 (uniform)
+        uint64_t nk = lane < A ? K[lane] : 0;     // block prefetch
+        for (int32_t i0 = 0; i0 < A; i0 += 64) {
+            const uint64_t ak = nk;
+            const int32_t il = i0 + lane;
+            const bool valid = il < A;
+            nk = (il + 64 < A) ? K[il + 64] : 0;
+            const int32_t ring_lo = i0 + 64 - RK;   // ring holds anchors [ring_lo, i0+63]
+            TRACE(tr, 1, i0); TRACE(tr, 2, 2);
+            // ---- isolated anchors (st(i) == i)
+            const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)prev_hi) << 32) |
+                                (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)prev_lo);
+            const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
+            const int32_t p = (int32_t)((ak >> qb) & rmask), pprv = (int32_t)((pk >> qb) & rmask);
+            const bool iso = valid && (il == 0 || g != gp || p > (int32_t)((uint32_t)pprv + (uint32_t)maxdx));
+            const uint64_t isoM = ballot(iso), validM = ballot(valid);
+            rkey[il & (RK - 1)] = ak;
+            if (iso) rfp[il & (RK - 1)] = make_int2(span, -1);
+            wave_lds_sync();
+            bool drained = false;
+            uint64_t todo = validM & ~isoM;
+            while (todo) {
+                const int b = ctz64(todo);
+                todo &= todo - 1;
+                const int32_t i = i0 + b;
+                {   // st never falls below an isolated anchor at or before i
+                    const uint64_t below = isoM & lanemask_lt_of(b);
+                    if (below) { const int32_t li = i0 + 63 - clz64(below); st = st > li ? st : li; }
+                }
+                const uint64_t ki = rdl64(ak, b);
+                const uint32_t gi = (uint32_t)(ki >> gsh);
+                const int32_t pi = (int32_t)((ki >> qb) & rmask);
+                const int32_t qi = (int32_t)(ki & qmask);
+                // ---- st (lchain.rs:75): first j in i's group with rpos_i <= rpos_j + max_dist_x
+                for (;;) {
+                    // (re)load the window; ring slots above this block are not yet written
+                    if (st < stb || st >= stb + 64 || (i > skv && skv < stb + 63)) {
+                        stb = st;
+                        skv = i0 + 63;
+                        const int32_t j = stb + lane;
+                        sk = 0;
+                        if (j < A) sk = j >= ring_lo ? rkey[j & (RK - 1)] : K[j];
+                    }
+                    const int32_t j = stb + lane;
+                    const uint32_t gj = (uint32_t)(sk >> gsh);
+                    const int32_t pj = (int32_t)((sk >> qb) & rmask);
+                    const bool cand = j >= st && j <= i;
+                    const bool stop = cand && (j == i || (gj == gi && !(pi > (int32_t)((uint32_t)pj + (uint32_t)maxdx))));
+                    const uint64_t m = ballot(stop);
+                    if (m) { st = stb + ctz64(m); break; }
+                    st = stb + 64;
+                }
+                TRACE(tr, 2, 3); TRACE(tr, 3, st);
+                const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
+                int32_t max_f = span, max_j = -1, n_skip = 0;
+                bool marks = false;
+                for (int32_t jtop = i - 1; jtop >= lo; jtop -= 64) {
+                    const int32_t j = jtop - lane;
+                    const bool inr = j >= lo;
+                    const bool deep = inr && j < ring_lo;
+                    if (any(deep) && !drained) { vm_drain(); drained = true; }   // f/pprev flushes
+                    uint64_t kj = 0;
+                    int2 fpj = make_int2(0, -1);
                     if (inr) {
-                        const uint64_t kj = K[CK(j, A)];
-                        pj = (int32_t)((kj >> qb) & rmask); qj = (int32_t)(kj & qmask);
-                        fj = F[CK(j, A)]; ppj = PP[CK(j, A)];
+                        if (!deep) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
+                        else { kj = K[CK(j, A)]; fpj = make_int2(F[CK(j, A)], PP[CK(j, A)]); }
+                    }
+                    const int32_t pj = (int32_t)((kj >> qb) & rmask), qj = (int32_t)(kj & qmask);
+                    const int32_t fj = fpj.x, ppj = fpj.y;
+                    // comput_sc (lchain.rs:17-34); rid/rev equal for every j >= st
+                    const int32_t dq = qi - qj, dr = pi - pj;
+                    bool ok = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
+                    const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                    ok = ok && dd <= bw;
+                    const int32_t dg = dr < dq ? dr : dq;
+                    const int32_t sc = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
+                    const int32_t sv = sc + fj;
+                    // t[pprev[j]] = i  (lchain.rs:86); targets below lo are never read
+                    const bool mk = ok && ppj >= lo;
+                    if (any(mk)) {
+                        if (mk) atomicOr(&ring[(ppj >> 5) & (RING_WORDS - 1)], 1u << (ppj & 31));
+                        marks = true;
+                        wave_lds_sync();
+                    }
+                    bool marked = false;
+                    if (marks) marked = ok && ((ring[(j >> 5) & (RING_WORDS - 1)] >> (j & 31)) & 1u);
+                    // strict new maximum in processing order
+                    const int32_t v = ok ? sv : INT_MIN;
+                    const int32_t excl = shr1_dpp(scan_max(v), INT_MIN);
+                    const int32_t pb = max_f > excl ? max_f : excl;
+                    const bool nm = ok && sv > pb;
+                    const bool plus = ok && !nm && marked;
+                    const uint64_t nmM = ballot(nm), plusM = ballot(plus), inrM = ballot(inr);
+                    uint64_t eff = ~0ULL, brkM = 0;
+                    if (plusM) {
+                        int32_t sa = nm ? -1 : (plus ? 1 : 0), sb = 0;
+                        scan_nskip(sa, sb);
+                        const int32_t na = (n_skip + sa) > sb ? (n_skip + sa) : sb;
+                        brkM = ballot(plus && na > P.max_skip);
+                        if (brkM) eff = lanemask_lt_of(ctz64(brkM));
+                        else n_skip = rdl(na, 63);
+                    } else {
+                        n_skip -= __popcll(nmM);
+                        n_skip = n_skip > 0 ? n_skip : 0;
+                    }
+                    const uint64_t nmm = nmM & eff;
+                    if (nmm) { const int L = 63 - clz64(nmm); max_f = rdl(sv, L); max_j = jtop - L; }
+                    pairs += (uint64_t)__popcll(brkM ? (inrM & (eff | (1ULL << ctz64(brkM)))) : inrM);
+                    if (brkM) break;
+                }
+                TRACE(tr, 2, 5);
+                // clear this i's marks (all targets lie in [lo, i-1])
+                if (marks) {
+                    const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
+#pragma clang loop vectorize(disable) unroll(disable)
+                    for (int32_t b0 = w0; b0 <= w1; b0 += 64) {
+                        const int32_t wd = b0 + lane;
+                        if (wd <= w1) ring[wd & (RING_WORDS - 1)] = 0;
                     }
                 }
-                // comput_sc (lchain.rs:17-34); rid/rev equal for every j >= st
-                const int32_t dq = qi - qj, dr = pi - pj;
-                bool ok = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
-                const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-                ok = ok && dd <= bw;
-                const int32_t dg = dr < dq ? dr : dq;
-                const int32_t sc = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
-                const int32_t s = sc + fj;
-                // t[pprev[j]] = i  (lchain.rs:86), targets below lo are never read
-                if (ok && ppj >= lo) atomicOr(&ring[(ppj >> 5) & (RING_WORDS - 1)], 1u << (ppj & 31));
-                wave_lds_sync();
-                const bool marked = ok && ((ring[(j >> 5) & (RING_WORDS - 1)] >> (j & 31)) & 1u);
-                // strict new maximum in processing order
-                const int32_t v = ok ? s : INT_MIN;
-                const int32_t incl = wave_incl_scan(v, [](int32_t x, int32_t y) { return x > y ? x : y; });
-                int32_t excl = __shfl_up(incl, 1, 64);
-                if (lane == 0) excl = INT_MIN;
-                const int32_t pb = max_f > excl ? max_f : excl;
-                const bool nm = ok && s > pb;
-                // n_skip: compose x -> max(x + a, b)
-                int32_t sa = nm ? -1 : ((ok && marked) ? 1 : 0), sb = 0;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const int32_t oa = __shfl_up(sa, d, 64), ob = __shfl_up(sb, d, 64);
-                    if (lane >= d) { const int32_t t = ob + sa; sb = t > sb ? t : sb; sa = oa + sa; }
-                }
-                const int32_t na = (n_skip + sa) > sb ? (n_skip + sa) : sb;
-                const uint64_t brk = ballot(ok && !nm && marked && na > P.max_skip);
-                const uint64_t eff = brk ? (lanemask_lt_of(ctz64(brk))) : ~0ULL;
-                const uint64_t nmm = ballot(nm) & eff;
-                if (nmm) { const int L = 63 - clz64(nmm); max_f = rdl(s, L); max_j = jtop - L; }
-                {
-                    const uint64_t inr_m = ballot(inr);
-                    const uint64_t seen = brk ? (inr_m & (eff | (1ULL << ctz64(brk)))) : inr_m;
-                    pairs += (uint64_t)__popcll(seen);
-                }
-                ++nsteps;
-                if (brk) break;
-                n_skip = rdl(na, 63);
-                jtop -= 64;
-            }
-            TRACE(tr, 2, 5);
-            // clear this i's marks (all targets lie in [lo, i-1])
-            if (i - 1 >= lo) {
-                const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
-#pragma clang loop vectorize(disable) unroll(disable)
-                for (int32_t b0 = w0; b0 <= w1; b0 += 64) {
-                    const int32_t wd = b0 + lane;
-                    if (wd <= w1) ring[wd & (RING_WORDS - 1)] = 0;
-                }
+                if (lane == 0) rfp[i & (RK - 1)] = make_int2(max_f, max_j);
                 wave_lds_sync();
             }
-            // f[i], pprev[i]; fallback best_i = LAST index with max f
-            if (max_f >= best_f) { best_f = max_f; best_i = i; }
-            wp = shr1(wp, pi); wq = shr1(wq, qi); wf = shr1(wf, max_f); wpp = shr1(wpp, max_j);
-            if (((i + 1) & 63) == 0) { const int32_t j = i - lane; F[CK(j, A)] = wf; PP[CK(j, A)] = wpp; }
-        }
-        {
-            const int32_t rem = A & 63;
-            if (lane < rem) { const int32_t j = A - 1 - lane; F[CK(j, A)] = wf; PP[CK(j, A)] = wpp; }
+            if (isoM) { const int32_t li = i0 + 63 - clz64(isoM); st = st > li ? st : li; }
+            // ---- flush f/pprev of the block; fallback best_i = LAST index with max f
+            const int2 e = rfp[il & (RK - 1)];
+            if (valid) { F[CK(il, A)] = e.x; PP[CK(il, A)] = e.y; }
+            const int32_t fv = valid ? e.x : INT_MIN;
+            const int32_t bm = rdl(scan_max(fv), 63);
+            if (bm >= best_f) { best_f = bm; best_i = i0 + 63 - clz64(ballot(valid && fv == bm)); }
+            prev_lo = rdlu((uint32_t)ak, 63); prev_hi = rdlu((uint32_t)(ak >> 32), 63);
         }
         vm_drain();
         TRACE(tr, 2, 7);
@@ -808,6 +876,29 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
             O->dp_pairs = prev_pairs + pairs;
         }
         TRACE(tr, 2, 9);
+    }
+}
+
+// order[t] = reads by descending anchor count (largest-first hand-out to the
+// chain waves).  Counting sort on log2 buckets of the anchor count keeps it one
+// cheap pass: exact LPT is not needed, only "heavy reads first".
+__global__ __launch_bounds__(1024) void k_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order) {
+    __shared__ uint32_t hist[33], offs[33];
+    const int tid = threadIdx.x;
+    if (tid < 33) hist[tid] = 0;
+    __syncthreads();
+    for (uint32_t r = tid; r < n; r += 1024) {
+        const uint32_t c = a_cnt[r];
+        const int bk = c ? 32 - __builtin_clz(c) : 0;   // 0..32, heavier = larger
+        atomicAdd(&hist[32 - bk], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) { uint32_t run = 0; for (int b = 0; b < 33; ++b) { offs[b] = run; run += hist[b]; } }
+    __syncthreads();
+    for (uint32_t r = tid; r < n; r += 1024) {
+        const uint32_t c = a_cnt[r];
+        const int bk = c ? 32 - __builtin_clz(c) : 0;
+        order[atomicAdd(&offs[32 - bk], 1u)] = r;
     }
 }
 
@@ -940,8 +1031,24 @@ int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp
     LAUNCH_CHECK();
     return 0;
 }
+static size_t chain_lds(int lut_n) {
+    return (size_t)(((lut_n * 2) + 15) & ~15) + (size_t)DP_NW * (RING_WORDS * 4 + RK * 8 + RK * 8);
+}
+int chain_max_blocks(int lut_n) {
+    int dev = 0, ncu = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_dp, DP_NW * 64, chain_lds(lut_n)) != hipSuccess) return 0;
+    return ncu * (per > 0 ? per : 1);
+}
+int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStream_t st) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_read_order, dim3(1), dim3(1024), 0, st, n, a_cnt, order);
+    LAUNCH_CHECK();
+    return 0;
+}
 int launch_chain(const ChainArgs& a, int n_blocks, hipStream_t st) {
-    const size_t lds = (size_t)(((a.P.lut_n * 2) + 15) & ~15) + (size_t)DP_NW * RING_WORDS * 4;
+    const size_t lds = chain_lds(a.P.lut_n);
     hipLaunchKernelGGL(k_chain_dp, dim3(n_blocks), dim3(DP_NW * 64), lds, st, a);
     LAUNCH_CHECK();
     return 0;

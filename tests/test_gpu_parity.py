@@ -92,6 +92,16 @@ def small_world(tmp_path_factory):
     return ref, reads, rnames, rseqs
 
 
+def _dp_diff(gf, gpp, f, pp, want_a):
+    bad = np.nonzero((gf != f) | (gpp.astype(np.int64) != pp))[0]
+    if len(bad) == 0:
+        return ""
+    i = int(bad[0])
+    lo, hi = max(0, i - 3), min(len(f), i + 3)
+    return (f"A={len(f)} first diff at i={i} ({len(bad)} diffs): got f={gf[lo:hi].tolist()} pp={gpp[lo:hi].tolist()} "
+            f"want f={f[lo:hi].tolist()} pp={pp[lo:hi].tolist()} key_i={[hex(int(x)) for x in want_a[i]]}")
+
+
 def test_pipeline_parity(dev, small_world, tmp_path):
     ref, reads, rnames, rseqs = small_world
     oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
@@ -113,8 +123,8 @@ def test_pipeline_parity(dev, small_world, tmp_path):
         rescued = bool(res[r].flags & 2)
         f, pp, chain, score, _ = O.chain_dp(want_a, 15, bw=(20000 if rescued else 500))
         gf, gpp = dev.debug_dp(r)
-        assert np.array_equal(gf, f), f"f differs for read {r}"
-        assert np.array_equal(gpp.astype(np.int64), pp), f"pprev differs for read {r}"
+        assert np.array_equal(gf, f) and np.array_equal(gpp.astype(np.int64), pp), \
+            f"DP differs for read {r}: " + _dp_diff(gf, gpp, f, pp, want_a)
         n_checked += 1
     assert n_checked > 100
     want_paf = str(tmp_path / "want.paf")
@@ -129,3 +139,81 @@ def test_pipeline_determinism(dev, small_world):
     p1 = M.align(idx, rnames, rseqs, dev=dev)
     p2 = M.align(idx, rnames, rseqs, dev=dev)
     assert p1 == p2 and p1.count("\n") > 50
+
+
+def _mutate(rng, s: bytes, p: float) -> bytes:
+    b = bytearray(s)
+    for i in range(len(b)):
+        if rng.random() < p:
+            b[i] = ord(rng.choice("ACGT"))
+    return bytes(b)
+
+
+@pytest.fixture(scope="module")
+def dense_world(tmp_path_factory):
+    """Satellite arrays + segmental duplications: windows of thousands of
+    anchors once mid_occ is lifted (deep j-steps beyond the LDS ring, n_skip
+    breaks, max_iter clipping, rescue)."""
+    td = tmp_path_factory.mktemp("dense")
+    rng = random.Random(77)
+    mono = _rand_seq(rng, 171, p_low=0.0)
+    sat = b"".join(_mutate(rng, mono, 0.03) for _ in range(120))                 # ~20 kb alpha-like array
+    unit = _rand_seq(rng, 2000, p_low=0.0)
+    sd = b"".join(_mutate(rng, unit, 0.01) for _ in range(12))                   # 24 kb tandem segmental dup
+    c0 = _rand_seq(rng, 30000, p_low=0.0) + sat + _rand_seq(rng, 30000, p_low=0.0)
+    c1 = _rand_seq(rng, 10000, p_low=0.0) + sd + _rand_seq(rng, 10000, p_low=0.0)
+    sd2 = b"".join(_mutate(rng, unit[:1500], 0.02) for _ in range(10))          # 15 kb on an even rid
+    c2 = _rand_seq(rng, 40000, p_low=0.0) + sd2 + _rand_seq(rng, 8000, p_low=0.0)
+    ref = str(td / "dense.fa")
+    simdata.write_fasta(ref, ["c0", "c1", "c2"], [c0, c1, c2])
+    rnames, rseqs = [], []
+    for t in range(8):                       # inside the satellite
+        st = 30000 + rng.randrange(0, len(sat) - 4000)
+        rseqs.append(_mutate(rng, c0[st:st + 3500], 0.04))
+    for t in range(8):                       # inside / across the segmental dup
+        st = 10000 + rng.randrange(-3000, len(sd) - 3000)
+        rseqs.append(_mutate(rng, c1[st:st + 6000], 0.03))
+    for t in range(6):                       # unique sequence, one crossing into the array
+        st = rng.randrange(0, len(c2) - 5000)
+        rseqs.append(_mutate(rng, c2[st:st + 5000], 0.05))
+    rseqs.append(c0[27000:27000 + 6000])
+    for t in range(4):                       # chimeras: half unique, half elsewhere -> rescue DP
+        a0 = rng.randrange(0, 20000)
+        b0 = rng.randrange(0, 30000)
+        rseqs.append(_mutate(rng, c2[a0:a0 + 4000] + c0[b0:b0 + 4000], 0.03))
+    for t in range(4):                       # inside the even-rid duplication
+        st = 40000 + rng.randrange(0, len(sd2) - 5000)
+        rseqs.append(_mutate(rng, c2[st:st + 5000], 0.03))
+    rnames = [f"d{i}" for i in range(len(rseqs))]
+    reads = str(td / "dense_reads.fa")
+    simdata.write_fasta(reads, rnames, rseqs)
+    return ref, reads, rnames, rseqs
+
+
+@pytest.mark.parametrize("mid_occ", [20, 5000])
+def test_pipeline_parity_dense(dev, dense_world, tmp_path, mid_occ):
+    ref, reads, rnames, rseqs = dense_world
+    oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+    idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+    dev.upload_index(idx, mid_occ)
+    dev.set_debug(True)
+    dev.set_reads(rseqs)
+    res = dev.map(M.map_opts())
+    deep = 0
+    for r, q in enumerate(rseqs):
+        want_a, _ = oi.anchors(q, 10, 15, mid_occ)
+        got_a = dev.debug_anchors(r)
+        assert np.array_equal(got_a, want_a), f"anchors differ for read {r}"
+        if len(want_a) == 0:
+            continue
+        rescued = bool(res[r].flags & 2)
+        f, pp, chain, score, _ = O.chain_dp(want_a, 15, bw=(20000 if rescued else 500))
+        gf, gpp = dev.debug_dp(r)
+        assert np.array_equal(gf, f) and np.array_equal(gpp.astype(np.int64), pp), \
+            f"DP differs for read {r} (rescued={rescued}): " + _dp_diff(gf, gpp, f, pp, want_a)
+        deep += int(len(want_a) > 2000)
+    if mid_occ == 5000:
+        assert deep >= 4
+    want_paf = str(tmp_path / "want.paf")
+    oi.align_fasta(reads, want_paf, mid_occ=mid_occ)
+    assert dev.paf(rnames, res) == open(want_paf).read()
