@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--threads", type=int, default=0, help="host threads for index build (0 = auto)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    p.add_argument("--stats", default="", help="write per-read chain statistics (npz) to this path")
     return p.parse_args()
 
 
@@ -147,6 +148,11 @@ def main():
     prof = dev.prof()
     dev.prof_enable(False)
     cnt = dev.counters()                          # per batch (identical every step)
+    if args.stats:
+        cs = dev.chain_stats()
+        na = np.array([res[i].n_anchors for i in range(args.reads)], dtype=np.int64)
+        fl = np.array([res[i].flags for i in range(args.reads)], dtype=np.int64)
+        np.savez(args.stats, chain=cs, n_anchors=na, flags=fl)
 
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")

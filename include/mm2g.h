@@ -141,6 +141,12 @@ int64_t mm2g_debug_anchors(mm2g_ctx* ctx, uint32_t r, uint64_t* xy, int64_t cap)
 int64_t mm2g_debug_dp(mm2g_ctx* ctx, uint32_t r, int32_t* f, int32_t* pprev, int64_t cap);
 int64_t mm2g_debug_keep(mm2g_ctx* ctx, uint32_t r, uint8_t* keep, int64_t cap);
 
+/* After mm2g_batch_results: per read [pass-0 ticks, pass-1 ticks (100 MHz
+ * wall clock), anchors in long segments, DP j-steps, j-steps reading HBM,
+ * longest segment | #long segments << 16 (pass 0)] of the chain kernel
+ * (6 values per read).  Returns the batch size. */
+int64_t mm2g_debug_chain_stats(mm2g_ctx* ctx, uint32_t* out6, uint32_t n);
+
 /* Per-kernel device time (HIP events on the context stream) accumulated over
  * mm2g_batch_map calls since the last reset: names[i], ms[i], calls[i]. */
 int mm2g_prof_enable(mm2g_ctx* ctx, int on);

@@ -261,6 +261,14 @@ class Device:
             i += 1
         return out
 
+    def chain_stats(self) -> np.ndarray:
+        """(n, 6) uint32: pass-0/1 ticks (10 ns), anchors in long segments, j-steps, HBM j-steps,
+        longest segment | #long segments << 16, per read."""
+        n = self.n_reads
+        out = np.zeros(6 * max(n, 1), dtype=np.uint32)
+        check(load().mm2g_debug_chain_stats(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n), "chain_stats")
+        return out[: 6 * n].reshape(n, 6)
+
     def counters(self) -> dict:
         buf = (C.c_uint64 * 6)()
         check(load().mm2g_batch_counters(self._h, buf), "counters")

@@ -74,7 +74,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order, tmark;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, dv_separate = false;
@@ -471,6 +471,8 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     // heaviest reads first; grid = what is co-resident (one wave per read, static hand-out)
     uint32_t* order;
     ENSURE(c->order, uint32_t, n, order);
+    int32_t* tmark;
+    ENSURE(c->tmark, int32_t, A, tmark);
     LCHK(launch_read_order(n, a_cnt, order, c->stream));
     int max_blocks = chain_max_blocks(P.lut_n);
     if (max_blocks <= 0) max_blocks = 2048;
@@ -484,7 +486,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         HIPCHK(hipHostGetDevicePointer((void**)&trace_d, trace_h, 0));
     }
 #endif
-    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work, std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, trace_d, order};
+    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work, std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, trace_d, order, A, std::min<int32_t>((int32_t)n, 4 * 256), tmark};
     auto dump_trace = [&](const char* what) {
         if (!trace_h) return;
         std::vector<uint64_t> ho(n + 1);
@@ -736,6 +738,17 @@ int mm2g_prof_reset(mm2g_ctx* c) {
     c->prof_collect();
     for (auto& s : c->slots) { s.ms = 0; s.calls = 0; }
     return 0;
+}
+int64_t mm2g_debug_chain_stats(mm2g_ctx* c, uint32_t* out6, uint32_t n) {
+    if (!c) return set_err(MM2G_E_ARG, "null context");
+    if (!c->mapped || !c->h_out) return set_err(MM2G_E_STATE, "call mm2g_batch_results first");
+    if (out6)
+        for (uint32_t i = 0; i < n && i < c->n_reads; ++i) {
+            const ReadOut& o = c->h_out[i];
+            out6[6 * i + 0] = o.t_pass[0]; out6[6 * i + 1] = o.t_pass[1];
+            out6[6 * i + 2] = o.n_noniso; out6[6 * i + 3] = o.n_steps; out6[6 * i + 4] = o.n_deep; out6[6 * i + 5] = o.pad2;
+        }
+    return (int64_t)c->n_reads;
 }
 int mm2g_batch_counters(mm2g_ctx* c, uint64_t* out6) {
     if (!c || !out6) return set_err(MM2G_E_ARG, "null argument");

@@ -35,8 +35,13 @@ struct ReadOut {
     int32_t qlen;
     int32_t m_kept;        // minimizers kept by the query filter
     uint64_t dp_pairs;     // inner-loop j evaluations (all passes)
+    // chain-kernel statistics (mm2g_debug_chain_stats): wall-clock ticks
+    // (100 MHz) of pass 0 / pass 1, non-isolated anchors, j-steps, HBM j-steps
+    uint32_t t_pass[2];
+    uint32_t n_noniso, n_steps, n_deep;
+    uint32_t pad2;
 };
-static_assert(sizeof(ReadOut) == 72, "ReadOut layout");
+static_assert(sizeof(ReadOut) == 96, "ReadOut layout");
 
 enum : int32_t {
     RF_MAPPED = 1, RF_RESCUED = 2, RF_DV_FOUND = 4, RF_PANIC = 8, RF_EMPTY = 16,
@@ -110,6 +115,9 @@ struct ChainArgs {
     uint64_t cap_keys;
     uint32_t* trace;    // MM2G_CHECKED: host-mapped per-wave progress {read, i, phase, aux}
     const uint32_t* order;   // reads in hand-out order (heaviest first); null = identity
+    uint64_t a_total;        // anchors in the batch; chain[a_total + a_off[r] ...] = segment scratch
+    int32_t n_prio;          // order[0 .. n_prio) run at raised wave priority
+    int32_t* tmark;          // per-anchor scratch: the reference's t[] for one-lane segments
 };
 struct DvArgs {
     uint32_t n;

@@ -77,6 +77,14 @@ DEVI uint32_t wave_excl_sum(uint32_t v, uint32_t& total) {
     total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);   // SGPR: wave-uniform
     return inc - v;
 }
+DEVI uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, d, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
 DEVI uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -644,6 +652,13 @@ DEVI int32_t scan_max(int32_t v) {
     v = max(v, dpp<0x142, 0xa>(INT_MIN, v)); v = max(v, dpp<0x143, 0xc>(INT_MIN, v));
     return v;
 }
+// OR over the wave (row_shr 1/2/4/8 + row_bcast 15/31 leave the total in lane 63)
+DEVI uint32_t wave_or32(uint32_t v) {
+    int32_t x = (int32_t)v;
+    x |= dpp<0x111>(0, x); x |= dpp<0x112>(0, x); x |= dpp<0x114>(0, x); x |= dpp<0x118>(0, x);
+    x |= dpp<0x142, 0xa>(0, x); x |= dpp<0x143, 0xc>(0, x);
+    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
 // lane l <- lane l-1, lane 0 <- old0 (wave_shr:1)
 DEVI int32_t shr1_dpp(int32_t v, int32_t old0) { return dpp<0x138>(old0, v); }
 // composition scan of x -> max(x + a, b) in lane order (earlier applied first)
@@ -657,6 +672,70 @@ DEVI void scan_nskip(int32_t& a, int32_t& b) {
     NS_STEP(0x111, 0xf) NS_STEP(0x112, 0xf) NS_STEP(0x114, 0xf) NS_STEP(0x118, 0xf)
     NS_STEP(0x142, 0xa) NS_STEP(0x143, 0xc)
 #undef NS_STEP
+}
+
+constexpr int TINY = 8;           // segments up to this many anchors: one lane, registers
+constexpr int MED = 128;          // up to this many: one lane, state machine over HBM; longer: whole wave
+
+// "last argmax" merge: larger f wins, ties go to the larger index (lchain.rs:162-167)
+DEVI void best_merge(int32_t& bf, int32_t& bi, int32_t f, int32_t i) {
+    if (f > bf || (f == bf && i > bi)) { bf = f; bi = i; }
+}
+
+// Scalar chain_dp_all (lchain.rs:73-90) of one segment of <= TINY anchors held
+// in registers; `act` lanes only.  Local indices; marks t[pprev[j]] = i are a
+// per-i bitmask (t is only ever compared with the current i).
+DEVI void tiny_segment_dp(bool act, int32_t len, const uint64_t* K, int32_t s, int32_t* F, int32_t* PP, const int16_t* lut,
+                          const ChainKParams& P, uint32_t qb, uint64_t qmask, uint64_t rmask, int32_t& bf, int32_t& bi,
+                          uint64_t& pairs) {
+    int32_t pp_[TINY], qq_[TINY], f_[TINY], pv_[TINY];
+#pragma unroll
+    for (int m = 0; m < TINY; ++m) {
+        const uint64_t k = (act && m < len) ? K[s + m] : 0;
+        pp_[m] = (int32_t)((k >> qb) & rmask); qq_[m] = (int32_t)(k & qmask);
+        f_[m] = P.span; pv_[m] = -1;
+    }
+    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    int32_t st = 0;
+    uint32_t npairs = 0;
+#pragma unroll
+    for (int i = 1; i < TINY; ++i) {
+        const bool ai = act && i < len;
+        // st (lchain.rs:75); every anchor of the segment is in i's group
+#pragma unroll
+        for (int m = 0; m < i; ++m)
+            if (st == m && pp_[i] > (int32_t)((uint32_t)pp_[m] + (uint32_t)maxdx)) st = m + 1;
+        const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
+        int32_t max_f = span, max_j = -1, n_skip = 0;
+        uint32_t marks = 0;
+        bool brk = !ai;
+#pragma unroll
+        for (int j = i - 1; j >= 0; --j) {
+            if (!brk && j >= lo) {
+                ++npairs;
+                const int32_t dq = qq_[i] - qq_[j], dr = pp_[i] - pp_[j];
+                bool ok = dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
+                const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                ok = ok && dd <= bw;
+                if (ok) {
+                    const int32_t dg = dr < dq ? dr : dq;
+                    const int32_t sv = (span < dg ? span : dg) - (int32_t)lut[dd] + f_[j];
+                    if (sv > max_f) { max_f = sv; max_j = j; if (n_skip > 0) --n_skip; }
+                    else if ((marks >> j) & 1u) { ++n_skip; if (n_skip > P.max_skip) brk = true; }
+                    if (!brk && pv_[j] >= 0) marks |= 1u << pv_[j];
+                }
+            }
+        }
+        if (ai) { f_[i] = max_f; pv_[i] = max_j; }
+    }
+#pragma unroll
+    for (int m = 0; m < TINY; ++m)
+        if (act && m < len) {
+            F[s + m] = f_[m];
+            PP[s + m] = pv_[m] >= 0 ? s + pv_[m] : -1;
+            best_merge(bf, bi, f_[m], s + m);
+        }
+    pairs += npairs;
 }
 
 __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
@@ -687,6 +766,13 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
         TRACE(tr, 0, r); TRACE(tr, 2, 1);
         const int32_t flags0 = uni(a.out[r].flags);
         if (P.pass == 1 && !(flags0 & RF_RESCUED)) continue;
+        const uint64_t t_start = wall_clock64();
+        uint32_t n_noniso = 0, n_steps = 0, n_deep = 0, n_big = 0;
+        int32_t max_seg = 0;
+        // the heaviest reads (first in `order`) set the kernel's critical path:
+        // let their waves win issue arbitration on the SIMD
+        if (t < (uint32_t)a.n_prio) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
         const uint64_t base = uni64(a.a_off[r]);
         const int32_t A = (int32_t)(uni64(a.a_off[r + 1]) - base);
         const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
@@ -703,141 +789,282 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
 #endif
         const uint64_t* K = a.keys + base;
         int32_t* F = a.f + base; int32_t* PP = a.pp + base;
-        int32_t st = 0, stb = INT_MIN / 2, skv = INT_MIN / 2;   // st window [stb, stb+63], keys valid up to skv
-        uint64_t sk = 0;
-        int32_t best_f = INT_MIN, best_i = -1;
-        uint64_t pairs = 0;
-        uint32_t prev_lo = 0, prev_hi = 0;        // key of anchor i0-1 (uniform)
-        uint64_t nk = lane < A ? K[lane] : 0;     // block prefetch
-        for (int32_t i0 = 0; i0 < A; i0 += 64) {
-            const uint64_t ak = nk;
-            const int32_t il = i0 + lane;
-            const bool valid = il < A;
-            nk = (il + 64 < A) ? K[il + 64] : 0;
-            const int32_t ring_lo = i0 + 64 - RK;   // ring holds anchors [ring_lo, i0+63]
-            TRACE(tr, 1, i0); TRACE(tr, 2, 2);
-            // ---- isolated anchors (st(i) == i)
-            const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)prev_hi) << 32) |
-                                (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)prev_lo);
-            const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
-            const int32_t p = (int32_t)((ak >> qb) & rmask), pprv = (int32_t)((pk >> qb) & rmask);
-            const bool iso = valid && (il == 0 || g != gp || p > (int32_t)((uint32_t)pprv + (uint32_t)maxdx));
-            const uint64_t isoM = ballot(iso), validM = ballot(valid);
-            rkey[il & (RK - 1)] = ak;
-            if (iso) rfp[il & (RK - 1)] = make_int2(span, -1);
-            wave_lds_sync();
-            bool drained = false;
-            uint64_t todo = validM & ~isoM;
-            while (todo) {
-                const int b = ctz64(todo);
-                todo &= todo - 1;
-                const int32_t i = i0 + b;
-                {   // st never falls below an isolated anchor at or before i
-                    const uint64_t below = isoM & lanemask_lt_of(b);
-                    if (below) { const int32_t li = i0 + 63 - clz64(below); st = st > li ? st : li; }
-                }
-                const uint64_t ki = rdl64(ak, b);
-                const uint32_t gi = (uint32_t)(ki >> gsh);
-                const int32_t pi = (int32_t)((ki >> qb) & rmask);
-                const int32_t qi = (int32_t)(ki & qmask);
-                // ---- st (lchain.rs:75): first j in i's group with rpos_i <= rpos_j + max_dist_x
-                for (;;) {
-                    // (re)load the window; ring slots above this block are not yet written
-                    if (st < stb || st >= stb + 64 || (i > skv && skv < stb + 63)) {
-                        stb = st;
-                        skv = i0 + 63;
-                        const int32_t j = stb + lane;
-                        sk = 0;
-                        if (j < A) sk = j >= ring_lo ? rkey[j & (RK - 1)] : K[j];
-                    }
-                    const int32_t j = stb + lane;
-                    const uint32_t gj = (uint32_t)(sk >> gsh);
-                    const int32_t pj = (int32_t)((sk >> qb) & rmask);
-                    const bool cand = j >= st && j <= i;
-                    const bool stop = cand && (j == i || (gj == gi && !(pi > (int32_t)((uint32_t)pj + (uint32_t)maxdx))));
-                    const uint64_t m = ballot(stop);
-                    if (m) { st = stb + ctz64(m); break; }
-                    st = stb + 64;
-                }
-                TRACE(tr, 2, 3); TRACE(tr, 3, st);
-                const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
-                int32_t max_f = span, max_j = -1, n_skip = 0;
-                bool marks = false;
-                for (int32_t jtop = i - 1; jtop >= lo; jtop -= 64) {
-                    const int32_t j = jtop - lane;
-                    const bool inr = j >= lo;
-                    const bool deep = inr && j < ring_lo;
-                    if (any(deep) && !drained) { vm_drain(); drained = true; }   // f/pprev flushes
-                    uint64_t kj = 0;
-                    int2 fpj = make_int2(0, -1);
-                    if (inr) {
-                        if (!deep) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
-                        else { kj = K[CK(j, A)]; fpj = make_int2(F[CK(j, A)], PP[CK(j, A)]); }
-                    }
-                    const int32_t pj = (int32_t)((kj >> qb) & rmask), qj = (int32_t)(kj & qmask);
-                    const int32_t fj = fpj.x, ppj = fpj.y;
-                    // comput_sc (lchain.rs:17-34); rid/rev equal for every j >= st
-                    const int32_t dq = qi - qj, dr = pi - pj;
-                    bool ok = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
-                    const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-                    ok = ok && dd <= bw;
-                    const int32_t dg = dr < dq ? dr : dq;
-                    const int32_t sc = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
-                    const int32_t sv = sc + fj;
-                    // t[pprev[j]] = i  (lchain.rs:86); targets below lo are never read
-                    const bool mk = ok && ppj >= lo;
-                    if (any(mk)) {
-                        if (mk) atomicOr(&ring[(ppj >> 5) & (RING_WORDS - 1)], 1u << (ppj & 31));
-                        marks = true;
-                        wave_lds_sync();
-                    }
-                    bool marked = false;
-                    if (marks) marked = ok && ((ring[(j >> 5) & (RING_WORDS - 1)] >> (j & 31)) & 1u);
-                    // strict new maximum in processing order
-                    const int32_t v = ok ? sv : INT_MIN;
-                    const int32_t excl = shr1_dpp(scan_max(v), INT_MIN);
-                    const int32_t pb = max_f > excl ? max_f : excl;
-                    const bool nm = ok && sv > pb;
-                    const bool plus = ok && !nm && marked;
-                    const uint64_t nmM = ballot(nm), plusM = ballot(plus), inrM = ballot(inr);
-                    uint64_t eff = ~0ULL, brkM = 0;
-                    if (plusM) {
-                        int32_t sa = nm ? -1 : (plus ? 1 : 0), sb = 0;
-                        scan_nskip(sa, sb);
-                        const int32_t na = (n_skip + sa) > sb ? (n_skip + sa) : sb;
-                        brkM = ballot(plus && na > P.max_skip);
-                        if (brkM) eff = lanemask_lt_of(ctz64(brkM));
-                        else n_skip = rdl(na, 63);
-                    } else {
-                        n_skip -= __popcll(nmM);
-                        n_skip = n_skip > 0 ? n_skip : 0;
-                    }
-                    const uint64_t nmm = nmM & eff;
-                    if (nmm) { const int L = 63 - clz64(nmm); max_f = rdl(sv, L); max_j = jtop - L; }
-                    pairs += (uint64_t)__popcll(brkM ? (inrM & (eff | (1ULL << ctz64(brkM)))) : inrM);
-                    if (brkM) break;
-                }
-                TRACE(tr, 2, 5);
-                // clear this i's marks (all targets lie in [lo, i-1])
-                if (marks) {
-                    const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
-#pragma clang loop vectorize(disable) unroll(disable)
-                    for (int32_t b0 = w0; b0 <= w1; b0 += 64) {
-                        const int32_t wd = b0 + lane;
-                        if (wd <= w1) ring[wd & (RING_WORDS - 1)] = 0;
-                    }
-                }
-                if (lane == 0) rfp[i & (RK - 1)] = make_int2(max_f, max_j);
-                wave_lds_sync();
+        uint32_t* SEG = a.chain + a.a_total + base;   // segment starts (scratch; second half of the chain buffer)
+        uint64_t pairs = 0, cpairs = 0;   // per-lane (tiny segments) / uniform (cooperative)
+        // ---- 1. segments: an isolated anchor (st(i) == i: i == 0, another
+        // (rid, strand) group than i-1, or rpos_i > rpos_{i-1} + max_dist_x)
+        // starts a segment; the DP of a segment never reads outside it.
+        int32_t nseg = 0;
+        {
+            uint32_t prev_lo = 0, prev_hi = 0;
+            uint64_t nk = lane < A ? K[lane] : 0;
+            for (int32_t i0 = 0; i0 < A; i0 += 64) {
+                const uint64_t ak = nk;
+                const int32_t il = i0 + lane;
+                const bool valid = il < A;
+                nk = (il + 64 < A) ? K[il + 64] : 0;
+                const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)prev_hi) << 32) |
+                                    (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)prev_lo);
+                const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
+                const int32_t p = (int32_t)((ak >> qb) & rmask), pprv = (int32_t)((pk >> qb) & rmask);
+                const bool iso = valid && (il == 0 || g != gp || p > (int32_t)((uint32_t)pprv + (uint32_t)maxdx));
+                const uint64_t isoM = ballot(iso);
+                if (iso) SEG[CK(nseg + __popcll(isoM & lanemask_lt()), A)] = (uint32_t)il;
+                nseg += __popcll(isoM);
+                prev_lo = rdlu((uint32_t)ak, 63); prev_hi = rdlu((uint32_t)(ak >> 32), 63);
             }
-            if (isoM) { const int32_t li = i0 + 63 - clz64(isoM); st = st > li ? st : li; }
-            // ---- flush f/pprev of the block; fallback best_i = LAST index with max f
-            const int2 e = rfp[il & (RK - 1)];
-            if (valid) { F[CK(il, A)] = e.x; PP[CK(il, A)] = e.y; }
-            const int32_t fv = valid ? e.x : INT_MIN;
-            const int32_t bm = rdl(scan_max(fv), 63);
-            if (bm >= best_f) { best_f = bm; best_i = i0 + 63 - clz64(ballot(valid && fv == bm)); }
-            prev_lo = rdlu((uint32_t)ak, 63); prev_hi = rdlu((uint32_t)(ak >> 32), 63);
+        }
+        vm_drain();
+        TRACE(tr, 2, 2);
+        // ---- 2. per batch of 64 segments: tiny ones one-per-lane in registers,
+        // longer ones cooperatively (below)
+        int32_t bf = INT_MIN, bi = -1;      // per-lane best (tiny and medium segments)
+        int32_t best_f = INT_MIN, best_i = -1;   // uniform best (long segments)
+        uint32_t* MEDL = a.chain + base;    // medium segments (s, e) (scratch: the chain slots, written last)
+        int32_t nmed = 0;
+        for (int32_t b0 = 0; b0 < nseg; b0 += 64) {
+            const int32_t k = b0 + lane;
+            const bool vs = k < nseg;
+            const int32_t s0 = vs ? (int32_t)SEG[CK(k, A)] : 0;
+            const int32_t e0 = vs ? (k + 1 < nseg ? (int32_t)SEG[CK(k + 1, A)] : A) : 0;
+            const int32_t len = e0 - s0;
+            const bool tiny = vs && len <= TINY;
+            if (any(tiny && len > 1))
+                tiny_segment_dp(tiny && len > 1, len, K, s0, F, PP, lut, P, qb, qmask, rmask, bf, bi, pairs);
+            if (tiny && len == 1) { F[s0] = span; PP[s0] = -1; best_merge(bf, bi, span, s0); }
+            // medium segments: queued for the one-lane-per-segment pass (3.)
+            const bool med = vs && len > TINY && len <= MED;
+            const uint64_t medM = ballot(med);
+            if (med) {
+                const int32_t q = nmed + __popcll(medM & lanemask_lt());
+                MEDL[CK(2 * q, A)] = (uint32_t)s0; MEDL[CK(2 * q + 1, A)] = (uint32_t)e0;
+            }
+            nmed += __popcll(medM);
+            uint64_t bigM = ballot(vs && len > MED);
+            while (bigM) {
+                const int b = ctz64(bigM);
+                bigM &= bigM - 1;
+                const int32_t s = rdl(s0, b), e = rdl(e0, b);
+                n_noniso += (uint32_t)(e - s - 1);
+                ++n_big; max_seg = max_seg > e - s ? max_seg : e - s;
+                // ---- cooperative DP of segment [s, e): anchor s is isolated, every
+                // later anchor has a candidate predecessor.  The 64 newest
+                // predecessors (rpos, qpos, f, pprev; lane l <-> j = i-1-l) live in
+                // registers and shift one lane per anchor (DPP wave_shr); the newest
+                // RK keys and f/pprev also go to the wave's LDS ring for the st
+                // window and deep steps; older ones come from HBM (flushed per block).
+                int32_t st = s, stb = INT_MIN / 2, skv = INT_MIN / 2;   // st window [stb, stb+63], valid up to skv
+                uint64_t sk = 0;
+                int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
+                uint64_t nk = (s + lane < e) ? K[s + lane] : 0;
+                for (int32_t i0 = s; i0 < e; i0 += 64) {
+                    const uint64_t ak = nk;
+                    const int32_t il = i0 + lane;
+                    const bool valid = il < e;
+                    nk = (il + 64 < e) ? K[il + 64] : 0;
+                    const int32_t ring_lo = i0 + 64 - RK;   // ring holds anchors [max(s, ring_lo), i0+63]
+                    rkey[il & (RK - 1)] = ak;
+                    if (il == s) rfp[il & (RK - 1)] = make_int2(span, -1);
+                    wave_lds_sync();
+                    bool drained = false;
+                    const int32_t ib = i0 == s ? s + 1 : i0;
+                    const int32_t ie = e < i0 + 64 ? e : i0 + 64;
+                    if (i0 == s) {   // anchor s enters the register window
+                        const uint64_t k0 = rdl64(ak, 0);
+                        wp = shr1_dpp(wp, (int32_t)((k0 >> qb) & rmask)); wq = shr1_dpp(wq, (int32_t)(k0 & qmask));
+                        wf = shr1_dpp(wf, span); wpp = shr1_dpp(wpp, -1);
+                    }
+                    for (int32_t i = ib; i < ie; ++i) {
+                        const uint64_t ki = rdl64(ak, i - i0);
+                        const int32_t pi = (int32_t)((ki >> qb) & rmask);
+                        const int32_t qi = (int32_t)(ki & qmask);
+                        // st (lchain.rs:75): first j >= st with rpos_i <= rpos_j + max_dist_x
+                        for (;;) {
+                            if (st < stb || st >= stb + 64 || (i > skv && skv < stb + 63)) {
+                                stb = st;
+                                skv = i0 + 63;
+                                const int32_t j = stb + lane;
+                                sk = 0;
+                                if (j < e) sk = j >= ring_lo ? rkey[j & (RK - 1)] : K[j];
+                            }
+                            const int32_t j = stb + lane;
+                            const int32_t pj = (int32_t)((sk >> qb) & rmask);
+                            const bool cand = j >= st && j <= i;
+                            const bool stop = cand && (j == i || !(pi > (int32_t)((uint32_t)pj + (uint32_t)maxdx)));
+                            const uint64_t m = ballot(stop);
+                            if (m) { st = stb + ctz64(m); break; }
+                            st = stb + 64;
+                        }
+                        const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
+                        int32_t max_f = span, max_j = -1, n_skip = 0;
+                        bool marks = false;
+                        for (int32_t jtop = i - 1; jtop >= lo; jtop -= 64) {
+                            const int32_t j = jtop - lane;
+                            const bool inr = j >= lo;
+                            int32_t pj, qj, fj, ppj;
+                            if (jtop == i - 1) { pj = wp; qj = wq; fj = wf; ppj = wpp; }
+                            else {
+                                const bool deep = inr && j < ring_lo;
+                                const bool any_deep = any(deep);
+                                n_deep += any_deep ? 1u : 0u;
+                                if (any_deep && !drained) { vm_drain(); drained = true; }   // f/pprev flushes
+                                uint64_t kj = 0;
+                                int2 fpj = make_int2(0, -1);
+                                if (inr) {
+                                    if (!deep) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
+                                    else { kj = K[CK(j, A)]; fpj = make_int2(F[CK(j, A)], PP[CK(j, A)]); }
+                                }
+                                pj = (int32_t)((kj >> qb) & rmask); qj = (int32_t)(kj & qmask); fj = fpj.x; ppj = fpj.y;
+                            }
+                            ++n_steps;
+                            // comput_sc (lchain.rs:17-34)
+                            const int32_t dq = qi - qj, dr = pi - pj;
+                            bool ok = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
+                            const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                            ok = ok && dd <= bw;
+                            const int32_t dg = dr < dq ? dr : dq;
+                            const int32_t sc = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
+                            const int32_t sv = sc + fj;
+                            // t[pprev[j]] = i  (lchain.rs:86); targets below lo are never read.
+                            // Targets inside this step's window (j' in [jtop-63, jtop]) are a
+                            // 64-bit mask built by a DPP OR-reduction; only targets below it
+                            // (read by a later, deeper step) and marks of earlier steps use
+                            // the LDS ring.
+                            const bool mk = ok && ppj >= lo;
+                            const int32_t tb = jtop - ppj;                 // target lane
+                            const bool mk_in = mk && tb < 64;
+                            const uint64_t tbit = mk_in ? (1ULL << (tb & 63)) : 0ULL;
+                            const uint64_t M = ((uint64_t)wave_or32((uint32_t)(tbit >> 32)) << 32) | wave_or32((uint32_t)tbit);
+                            // strict new maximum in processing order
+                            const int32_t v = ok ? sv : INT_MIN;
+                            const int32_t excl = shr1_dpp(scan_max(v), INT_MIN);
+                            const int32_t pb = max_f > excl ? max_f : excl;
+                            const bool nm = ok && sv > pb;
+                            bool marked = ok && ((M >> lane) & 1ULL);
+                            if (marks) marked = marked || (ok && ((ring[(j >> 5) & (RING_WORDS - 1)] >> (j & 31)) & 1u));
+                            const bool plus = ok && !nm && marked;
+                            const uint64_t nmM = ballot(nm), plusM = ballot(plus), inrM = ballot(inr);
+                            uint64_t eff = ~0ULL, brkM = 0;
+                            if (plusM) {
+                                int32_t sa = nm ? -1 : (plus ? 1 : 0), sb = 0;
+                                scan_nskip(sa, sb);
+                                const int32_t na = (n_skip + sa) > sb ? (n_skip + sa) : sb;
+                                brkM = ballot(plus && na > P.max_skip);
+                                if (brkM) eff = lanemask_lt_of(ctz64(brkM));
+                                else n_skip = rdl(na, 63);
+                            } else {
+                                n_skip -= __popcll(nmM);
+                                n_skip = n_skip > 0 ? n_skip : 0;
+                            }
+                            const uint64_t nmm = nmM & eff;
+                            if (nmm) { const int L = 63 - clz64(nmm); max_f = rdl(sv, L); max_j = jtop - L; }
+                            cpairs += (uint64_t)__popcll(brkM ? (inrM & (eff | (1ULL << ctz64(brkM)))) : inrM);
+                            if (brkM) break;
+                            // a deeper step follows: record this step's marks below its window
+                            if (jtop - 64 >= lo) {
+                                const bool mk_out = mk && !mk_in;
+                                if (any(mk_out)) {
+                                    if (mk_out) atomicOr(&ring[(ppj >> 5) & (RING_WORDS - 1)], 1u << (ppj & 31));
+                                    marks = true;
+                                }
+                                wave_lds_sync();
+                            }
+                        }
+                        // clear this i's marks (all targets lie in [lo, i-1])
+                        if (marks) {
+                            const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
+#pragma clang loop vectorize(disable) unroll(disable)
+                            for (int32_t c0 = w0; c0 <= w1; c0 += 64) {
+                                const int32_t wd = c0 + lane;
+                                if (wd <= w1) ring[wd & (RING_WORDS - 1)] = 0;
+                            }
+                        }
+                        if (lane == 0) rfp[i & (RK - 1)] = make_int2(max_f, max_j);
+                        wp = shr1_dpp(wp, pi); wq = shr1_dpp(wq, qi); wf = shr1_dpp(wf, max_f); wpp = shr1_dpp(wpp, max_j);
+                    }
+                    wave_lds_sync();
+                    // flush f/pprev of the block; segment best (last index with max f)
+                    const int2 ev = rfp[il & (RK - 1)];
+                    if (valid) { F[CK(il, A)] = ev.x; PP[CK(il, A)] = ev.y; }
+                    const int32_t fv = valid ? ev.x : INT_MIN;
+                    const int32_t bm = rdl(scan_max(fv), 63);
+                    best_merge(best_f, best_i, bm, i0 + 63 - clz64(ballot(valid && fv == bm)));
+                }
+            }
+        }
+        // ---- 3. medium segments, one lane each: chain_dp_all (lchain.rs:73-90)
+        // as a flattened per-lane state machine (advance st | evaluate one j |
+        // finish i) inside a wave-uniform loop; idle lanes take the next queued
+        // segment.  t[] is the reference's own mark array (t[j] == i), kept in
+        // HBM scratch and reset to -1 when anchor j is finished.
+        vm_drain();
+        if (nmed > 0) {
+            int32_t* T = a.tmark + base;
+            int32_t ms = 0, me = 0, i = 0, j = 0, lo = 0, sx = 0, max_f = 0, max_j = -1, n_skip = 0, pi = 0, qi = 0, psx = 0;
+            int32_t state = 0;                  // 0 idle, 1 advance st, 2 j-loop
+            int32_t next = 0;                   // uniform: next queued segment
+            for (;;) {
+                const bool idle = state == 0;
+                const uint64_t idleM = ballot(idle);
+                if (idleM && next < nmed) {
+                    const int32_t kq = next + __popcll(idleM & lanemask_lt());
+                    if (idle && kq < nmed) {
+                        ms = (int32_t)MEDL[CK(2 * kq, A)]; me = (int32_t)MEDL[CK(2 * kq + 1, A)];
+                        F[ms] = span; PP[ms] = -1; T[ms] = -1; best_merge(bf, bi, span, ms);
+                        const uint64_t k0 = K[ms], k1 = K[ms + 1];
+                        psx = (int32_t)((k0 >> qb) & rmask);
+                        pi = (int32_t)((k1 >> qb) & rmask); qi = (int32_t)(k1 & qmask);
+                        sx = ms; i = ms + 1; state = 1;
+                    }
+                    next += __popcll(idleM);
+                }
+                if (!any(state != 0)) break;
+                if (state == 1) {
+                    if (sx < i && pi > (int32_t)((uint32_t)psx + (uint32_t)maxdx)) {
+                        ++sx;
+                        psx = (int32_t)((K[sx] >> qb) & rmask);
+                    } else {
+                        lo = sx > i - P.max_iter ? sx : i - P.max_iter;
+                        j = i - 1; max_f = span; max_j = -1; n_skip = 0; state = 2;
+                    }
+                } else if (state == 2) {
+                    if (j >= lo) {
+                        const uint64_t kj = K[j];
+                        const int32_t fj = F[j], ppj = PP[j], tj = T[j];
+                        const int32_t pj = (int32_t)((kj >> qb) & rmask), qj = (int32_t)(kj & qmask);
+                        const int32_t dq = qi - qj, dr = pi - pj;
+                        bool ok = dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
+                        const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                        ok = ok && dd <= bw;
+                        bool brk = false;
+                        ++pairs;
+                        if (ok) {
+                            const int32_t dg = dr < dq ? dr : dq;
+                            const int32_t sv = (span < dg ? span : dg) - (int32_t)lut[dd] + fj;
+                            if (sv > max_f) { max_f = sv; max_j = j; if (n_skip > 0) --n_skip; }
+                            else if (tj == i) { ++n_skip; if (n_skip > P.max_skip) brk = true; }
+                            if (!brk && ppj >= 0) T[ppj] = i;
+                        }
+                        j = brk ? lo - 1 : j - 1;
+                    } else {
+                        F[i] = max_f; PP[i] = max_j; T[i] = -1; best_merge(bf, bi, max_f, i);
+                        ++i;
+                        if (i >= me) state = 0;
+                        else {
+                            const uint64_t ki = K[i];
+                            pi = (int32_t)((ki >> qb) & rmask); qi = (int32_t)(ki & qmask);
+                            state = 1;
+                        }
+                    }
+                }
+            }
+            vm_drain();
+        }
+        // merge lane bests (tiny segments) with the cooperative best
+        {
+            const int32_t m = rdl(scan_max(bf), 63);
+            const int32_t mi = rdl(scan_max(bf == m ? bi : -1), 63);
+            best_merge(best_f, best_i, m, mi);
         }
         vm_drain();
         TRACE(tr, 2, 7);
@@ -868,12 +1095,18 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
             if (unc > P.rescue_size || (float)cov < (float)qlen * P.rescue_ratio_f) fl |= RF_RESCUED;
         }
         const uint64_t prev_pairs = P.pass == 0 ? 0ULL : uni64(a.out[r].dp_pairs);
+        const uint64_t wpairs = uni64(wave_sum64(pairs)) + cpairs;
         if (lane == 0) {
             ReadOut* O = a.out + r;
             O->flags = fl; O->n_anchors = A; O->qlen = qlen;
             O->score = best_f; O->cm = cm; O->qs = qs; O->qe = qe; O->ts = ts; O->te = te;
             O->group = (int32_t)g; O->best_i = best_i;
-            O->dp_pairs = prev_pairs + pairs;
+            O->dp_pairs = prev_pairs + wpairs;
+            O->t_pass[P.pass] = (uint32_t)(wall_clock64() - t_start);
+            O->pad2 = P.pass == 0 ? ((uint32_t)(max_seg > 65535 ? 65535 : max_seg) | ((n_big > 65535 ? 65535u : n_big) << 16))
+                                  : O->pad2;
+            if (P.pass == 0) { O->n_noniso = n_noniso; O->n_steps = n_steps; O->n_deep = n_deep; }
+            else { O->n_noniso += n_noniso; O->n_steps += n_steps; O->n_deep += n_deep; }
         }
         TRACE(tr, 2, 9);
     }

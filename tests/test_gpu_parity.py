@@ -215,5 +215,7 @@ def test_pipeline_parity_dense(dev, dense_world, tmp_path, mid_occ):
     if mid_occ == 5000:
         assert deep >= 4
     want_paf = str(tmp_path / "want.paf")
-    oi.align_fasta(reads, want_paf, mid_occ=mid_occ)
+    _, counts, _ = oi.align_fasta(reads, want_paf, mid_occ=mid_occ)
     assert dev.paf(rnames, res) == open(want_paf).read()
+    # the DP pair counter behind bench.py's pairs/s equals the reference's inner-loop iterations
+    assert dev.counters()["dp_pairs"] == counts["inner_iters"]
