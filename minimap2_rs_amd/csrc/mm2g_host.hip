@@ -74,7 +74,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order, tmark;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, dv_separate = false;
@@ -473,48 +473,29 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->order, uint32_t, n, order);
     int32_t* tmark;
     ENSURE(c->tmark, int32_t, A, tmark);
+    const uint32_t lcap = (uint32_t)std::min<uint64_t>(A / (CHAIN_MED + 1) + 64, 0xffffffffu);
+    uint4* lseg; uint32_t *lseg_n, *lseg_order; unsigned long long* rbest;
+    ENSURE(c->lseg, uint4, lcap, lseg);
+    ENSURE(c->lseg_order, uint32_t, lcap, lseg_order);
+    ENSURE(c->lseg_n, uint32_t, 4, lseg_n);
+    ENSURE(c->rbest, unsigned long long, n, rbest);
     LCHK(launch_read_order(n, a_cnt, order, c->stream));
-    int max_blocks = chain_max_blocks(P.lut_n);
-    if (max_blocks <= 0) max_blocks = 2048;
-    const int chain_blocks = std::max(1, std::min((int)((n + 3) / 4), max_blocks));
-    uint32_t* trace_h = nullptr; uint32_t* trace_d = nullptr;
-#ifdef MM2G_CHECKED
-    if (g_sync_each) {
-        const size_t tb = (size_t)chain_blocks * 4 * 4 * sizeof(uint32_t);
-        HIPCHK(hipHostMalloc((void**)&trace_h, tb, hipHostMallocMapped));
-        memset(trace_h, 0xff, tb);
-        HIPCHK(hipHostGetDevicePointer((void**)&trace_d, trace_h, 0));
-    }
-#endif
-    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work, std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, trace_d, order, A, std::min<int32_t>((int32_t)n, 4 * 256), tmark};
-    auto dump_trace = [&](const char* what) {
-        if (!trace_h) return;
-        std::vector<uint64_t> ho(n + 1);
-        fprintf(stderr, "[mm2g] trace after %s (waves not at phase 9/1-done):\n", what);
-        for (int wv = 0; wv < chain_blocks * 4; ++wv) {
-            const uint32_t* t = trace_h + 4 * wv;
-            if (t[2] != 9 && !(t[2] == 1 && t[0] >= n) && t[2] != 0xffffffffu)
-                fprintf(stderr, "  wave %d: read %u i %u phase %u aux %u\n", wv, t[0], t[1], t[2], t[3]);
+    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work,
+                 std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, nullptr, order, A, std::min<int32_t>((int32_t)n, 4 * 256), tmark,
+                 lseg, lseg_n, lcap, lseg_order, rbest};
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1) {
+            ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
+            ca.P.lut_n = o->bw_long + 1; ca.lseg_n = lseg_n + 1;
         }
-        fflush(stderr);
-    };
-    {
-        ProfScope ps(c, "chain_dp");
-        LCHK(launch_chain(ca, chain_blocks, c->stream));
-    }
-    if (trace_h) {
-        hipError_t e = hipStreamSynchronize(c->stream);
-        if (e != hipSuccess) {
-            dump_trace("chain_dp");
-            // anchor counts of the in-flight reads (host copy of a_off is not available after a fault)
-            return set_err(MM2G_E_HIP, "chain_dp failed: %s", hipGetErrorString(e));
-        }
-    }
-    ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
-    ca.P.lut_n = o->bw_long + 1; ca.work = work + 1;
-    {
-        ProfScope ps(c, "chain_dp_rescue");
-        LCHK(launch_chain(ca, chain_blocks, c->stream));
+        int sb = chain_max_blocks(ca.P.lut_n, 0), lb = chain_max_blocks(ca.P.lut_n, 1);
+        if (sb <= 0) sb = 1024;
+        if (lb <= 0) lb = 1024;
+        sb = std::max(1, std::min((int)((n + 3) / 4), sb));
+        HIPCHK(hipMemsetAsync(rbest, 0, (size_t)n * 8, c->stream));
+        HIPCHK(hipMemsetAsync(ca.lseg_n, 0, 4, c->stream));
+        ProfScope ps(c, pass == 0 ? "chain_dp" : "chain_dp_rescue");
+        LCHK(launch_chain(ca, sb, lb, c->stream));
     }
     // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
     const bool sep = (H.w != o->w || H.k != o->k);

@@ -6,6 +6,10 @@ namespace mm2g {
 
 constexpr uint64_t U64MAX = ~0ULL;
 constexpr int WAVE = 64;
+// chain DP segment classes (DESIGN.md "Chain DP"): <= CHAIN_TINY anchors one
+// lane in registers, <= CHAIN_MED one lane (state machine), longer one wave
+constexpr int CHAIN_TINY = 8;
+constexpr int CHAIN_MED = 128;
 
 // Anchor key packing (DESIGN.md "Anchor key").  The reference anchor is
 // (x, y) = (rev<<63 | rid<<32 | rpos, span<<32 | qpos) sorted by (x, y)
@@ -118,6 +122,11 @@ struct ChainArgs {
     uint64_t a_total;        // anchors in the batch; chain[a_total + a_off[r] ...] = segment scratch
     int32_t n_prio;          // order[0 .. n_prio) run at raised wave priority
     int32_t* tmark;          // per-anchor scratch: the reference's t[] for one-lane segments
+    uint4* lseg;             // long-segment queue: (read, s, e, -)
+    uint32_t* lseg_n;        // its length (atomic counter)
+    uint32_t lseg_cap;
+    uint32_t* lseg_order;    // long segments, longest first
+    unsigned long long* rbest;   // per read: packed (f, index) of the last argmax f
 };
 struct DvArgs {
     uint32_t n;
@@ -139,8 +148,9 @@ int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st);
 // MM2G_CHECKED builds: first recorded bounds violation {line, index, cap}; 0 = none
 int mm2g_checked_read(unsigned long long out[4], hipStream_t st);
-int launch_chain(const mm2g::ChainArgs& a, int n_blocks, hipStream_t st);
-int chain_max_blocks(int lut_n);   // co-resident workgroups of k_chain_dp on the current device
+// chain DP of one pass: k_chain_seg, k_lseg_order, k_chain_long, k_chain_fin
+int launch_chain(const mm2g::ChainArgs& a, int seg_blocks, int long_blocks, hipStream_t st);
+int chain_max_blocks(int lut_n, int which);   // co-resident workgroups (0 = k_chain_seg, 1 = k_chain_long)
 int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStream_t st);
 int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st);

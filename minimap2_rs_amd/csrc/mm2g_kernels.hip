@@ -674,8 +674,8 @@ DEVI void scan_nskip(int32_t& a, int32_t& b) {
 #undef NS_STEP
 }
 
-constexpr int TINY = 8;           // segments up to this many anchors: one lane, registers
-constexpr int MED = 128;          // up to this many: one lane, state machine over HBM; longer: whole wave
+constexpr int TINY = CHAIN_TINY;  // segments up to this many anchors: one lane, registers
+constexpr int MED = CHAIN_MED;    // up to this many: one lane, state machine over HBM; longer: whole wave
 
 // "last argmax" merge: larger f wins, ties go to the larger index (lchain.rs:162-167)
 DEVI void best_merge(int32_t& bf, int32_t& bi, int32_t f, int32_t i) {
@@ -738,59 +738,48 @@ DEVI void tiny_segment_dp(bool act, int32_t len, const uint64_t* K, int32_t s, i
     pairs += npairs;
 }
 
-__global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
+// packed "last argmax" key: larger f first, then larger index (lchain.rs:162-167)
+DEVI unsigned long long best_key(int32_t f, int32_t i) {
+    return ((unsigned long long)((uint32_t)f ^ 0x80000000u) << 32) | (uint32_t)i;
+}
+
+// ---- 5a. per read: segments, tiny + medium segments one-per-lane, long
+// segments queued for k_chain_long.  Dynamic-programming state of every
+// segment stays inside it (DESIGN.md "Chain DP"), so the three parts write
+// disjoint f/pprev ranges; the read's best (last argmax f) is merged with a
+// packed 64-bit atomicMax.
+__global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
-    const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
-    uint32_t* rings = (uint32_t*)(smem + lut_bytes);
-    uint64_t* rkeys = (uint64_t*)(rings + DP_NW * RING_WORDS);
-    int2* rfps = (int2*)(rkeys + DP_NW * RK);
     for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
-    for (int i = threadIdx.x; i < DP_NW * RING_WORDS; i += blockDim.x) rings[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wv = wave_id();
-    uint32_t* ring = rings + wv * RING_WORDS;
-    uint64_t* rkey = rkeys + wv * RK;
-    int2* rfp = rfps + wv * RK;
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const uint32_t gsh = rb + qb;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
-    uint32_t* tr = (a.trace && lane == 0) ? a.trace + 4 * (blockIdx.x * DP_NW + wv) : nullptr;
-    (void)tr;
     // Static, wave-uniform assignment of reads in `order` (heaviest first).
     const uint32_t nwaves = gridDim.x * DP_NW;
     for (uint32_t t = blockIdx.x * DP_NW + wv; t < a.n; t += nwaves) {
         const uint32_t r = a.order ? (uint32_t)uni((int32_t)a.order[t]) : t;
-        TRACE(tr, 0, r); TRACE(tr, 2, 1);
         const int32_t flags0 = uni(a.out[r].flags);
         if (P.pass == 1 && !(flags0 & RF_RESCUED)) continue;
         const uint64_t t_start = wall_clock64();
-        uint32_t n_noniso = 0, n_steps = 0, n_deep = 0, n_big = 0;
-        int32_t max_seg = 0;
-        // the heaviest reads (first in `order`) set the kernel's critical path:
-        // let their waves win issue arbitration on the SIMD
         if (t < (uint32_t)a.n_prio) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
         const uint64_t base = uni64(a.a_off[r]);
         const int32_t A = (int32_t)(uni64(a.a_off[r + 1]) - base);
-        const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
-        if (A == 0) {
-            if (lane == 0) {
-                ReadOut* O = a.out + r;
-                O->flags = flags0 & RF_EMPTY; O->n_anchors = 0; O->score = 0; O->cm = 0;
-                O->qs = O->qe = O->ts = O->te = 0; O->group = 0; O->best_i = -1; O->qlen = qlen;
-            }
-            continue;
-        }
+        if (A == 0) continue;
 #ifdef MM2G_CHECKED
         if (base + (uint64_t)A > a.cap_keys) { if (lane == 0) CK(base + A, a.cap_keys); continue; }
 #endif
         const uint64_t* K = a.keys + base;
         int32_t* F = a.f + base; int32_t* PP = a.pp + base;
         uint32_t* SEG = a.chain + a.a_total + base;   // segment starts (scratch; second half of the chain buffer)
-        uint64_t pairs = 0, cpairs = 0;   // per-lane (tiny segments) / uniform (cooperative)
+        uint64_t pairs = 0;
+        uint32_t n_big = 0;
+        int32_t max_seg = 0;
         // ---- 1. segments: an isolated anchor (st(i) == i: i == 0, another
         // (rid, strand) group than i-1, or rpos_i > rpos_{i-1} + max_dist_x)
         // starts a segment; the DP of a segment never reads outside it.
@@ -815,11 +804,9 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
             }
         }
         vm_drain();
-        TRACE(tr, 2, 2);
         // ---- 2. per batch of 64 segments: tiny ones one-per-lane in registers,
-        // longer ones cooperatively (below)
+        // medium ones queued per read, long ones queued globally
         int32_t bf = INT_MIN, bi = -1;      // per-lane best (tiny and medium segments)
-        int32_t best_f = INT_MIN, best_i = -1;   // uniform best (long segments)
         uint32_t* MEDL = a.chain + base;    // medium segments (s, e) (scratch: the chain slots, written last)
         int32_t nmed = 0;
         for (int32_t b0 = 0; b0 < nseg; b0 += 64) {
@@ -832,7 +819,6 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
             if (any(tiny && len > 1))
                 tiny_segment_dp(tiny && len > 1, len, K, s0, F, PP, lut, P, qb, qmask, rmask, bf, bi, pairs);
             if (tiny && len == 1) { F[s0] = span; PP[s0] = -1; best_merge(bf, bi, span, s0); }
-            // medium segments: queued for the one-lane-per-segment pass (3.)
             const bool med = vs && len > TINY && len <= MED;
             const uint64_t medM = ballot(med);
             if (med) {
@@ -840,157 +826,20 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
                 MEDL[CK(2 * q, A)] = (uint32_t)s0; MEDL[CK(2 * q + 1, A)] = (uint32_t)e0;
             }
             nmed += __popcll(medM);
-            uint64_t bigM = ballot(vs && len > MED);
-            while (bigM) {
-                const int b = ctz64(bigM);
-                bigM &= bigM - 1;
-                const int32_t s = rdl(s0, b), e = rdl(e0, b);
-                n_noniso += (uint32_t)(e - s - 1);
-                ++n_big; max_seg = max_seg > e - s ? max_seg : e - s;
-                // ---- cooperative DP of segment [s, e): anchor s is isolated, every
-                // later anchor has a candidate predecessor.  The 64 newest
-                // predecessors (rpos, qpos, f, pprev; lane l <-> j = i-1-l) live in
-                // registers and shift one lane per anchor (DPP wave_shr); the newest
-                // RK keys and f/pprev also go to the wave's LDS ring for the st
-                // window and deep steps; older ones come from HBM (flushed per block).
-                int32_t st = s, stb = INT_MIN / 2, skv = INT_MIN / 2;   // st window [stb, stb+63], valid up to skv
-                uint64_t sk = 0;
-                int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
-                uint64_t nk = (s + lane < e) ? K[s + lane] : 0;
-                for (int32_t i0 = s; i0 < e; i0 += 64) {
-                    const uint64_t ak = nk;
-                    const int32_t il = i0 + lane;
-                    const bool valid = il < e;
-                    nk = (il + 64 < e) ? K[il + 64] : 0;
-                    const int32_t ring_lo = i0 + 64 - RK;   // ring holds anchors [max(s, ring_lo), i0+63]
-                    rkey[il & (RK - 1)] = ak;
-                    if (il == s) rfp[il & (RK - 1)] = make_int2(span, -1);
-                    wave_lds_sync();
-                    bool drained = false;
-                    const int32_t ib = i0 == s ? s + 1 : i0;
-                    const int32_t ie = e < i0 + 64 ? e : i0 + 64;
-                    if (i0 == s) {   // anchor s enters the register window
-                        const uint64_t k0 = rdl64(ak, 0);
-                        wp = shr1_dpp(wp, (int32_t)((k0 >> qb) & rmask)); wq = shr1_dpp(wq, (int32_t)(k0 & qmask));
-                        wf = shr1_dpp(wf, span); wpp = shr1_dpp(wpp, -1);
-                    }
-                    for (int32_t i = ib; i < ie; ++i) {
-                        const uint64_t ki = rdl64(ak, i - i0);
-                        const int32_t pi = (int32_t)((ki >> qb) & rmask);
-                        const int32_t qi = (int32_t)(ki & qmask);
-                        // st (lchain.rs:75): first j >= st with rpos_i <= rpos_j + max_dist_x
-                        for (;;) {
-                            if (st < stb || st >= stb + 64 || (i > skv && skv < stb + 63)) {
-                                stb = st;
-                                skv = i0 + 63;
-                                const int32_t j = stb + lane;
-                                sk = 0;
-                                if (j < e) sk = j >= ring_lo ? rkey[j & (RK - 1)] : K[j];
-                            }
-                            const int32_t j = stb + lane;
-                            const int32_t pj = (int32_t)((sk >> qb) & rmask);
-                            const bool cand = j >= st && j <= i;
-                            const bool stop = cand && (j == i || !(pi > (int32_t)((uint32_t)pj + (uint32_t)maxdx)));
-                            const uint64_t m = ballot(stop);
-                            if (m) { st = stb + ctz64(m); break; }
-                            st = stb + 64;
-                        }
-                        const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
-                        int32_t max_f = span, max_j = -1, n_skip = 0;
-                        bool marks = false;
-                        for (int32_t jtop = i - 1; jtop >= lo; jtop -= 64) {
-                            const int32_t j = jtop - lane;
-                            const bool inr = j >= lo;
-                            int32_t pj, qj, fj, ppj;
-                            if (jtop == i - 1) { pj = wp; qj = wq; fj = wf; ppj = wpp; }
-                            else {
-                                const bool deep = inr && j < ring_lo;
-                                const bool any_deep = any(deep);
-                                n_deep += any_deep ? 1u : 0u;
-                                if (any_deep && !drained) { vm_drain(); drained = true; }   // f/pprev flushes
-                                uint64_t kj = 0;
-                                int2 fpj = make_int2(0, -1);
-                                if (inr) {
-                                    if (!deep) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
-                                    else { kj = K[CK(j, A)]; fpj = make_int2(F[CK(j, A)], PP[CK(j, A)]); }
-                                }
-                                pj = (int32_t)((kj >> qb) & rmask); qj = (int32_t)(kj & qmask); fj = fpj.x; ppj = fpj.y;
-                            }
-                            ++n_steps;
-                            // comput_sc (lchain.rs:17-34)
-                            const int32_t dq = qi - qj, dr = pi - pj;
-                            bool ok = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
-                            const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-                            ok = ok && dd <= bw;
-                            const int32_t dg = dr < dq ? dr : dq;
-                            const int32_t sc = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
-                            const int32_t sv = sc + fj;
-                            // t[pprev[j]] = i  (lchain.rs:86); targets below lo are never read.
-                            // Targets inside this step's window (j' in [jtop-63, jtop]) are a
-                            // 64-bit mask built by a DPP OR-reduction; only targets below it
-                            // (read by a later, deeper step) and marks of earlier steps use
-                            // the LDS ring.
-                            const bool mk = ok && ppj >= lo;
-                            const int32_t tb = jtop - ppj;                 // target lane
-                            const bool mk_in = mk && tb < 64;
-                            const uint64_t tbit = mk_in ? (1ULL << (tb & 63)) : 0ULL;
-                            const uint64_t M = ((uint64_t)wave_or32((uint32_t)(tbit >> 32)) << 32) | wave_or32((uint32_t)tbit);
-                            // strict new maximum in processing order
-                            const int32_t v = ok ? sv : INT_MIN;
-                            const int32_t excl = shr1_dpp(scan_max(v), INT_MIN);
-                            const int32_t pb = max_f > excl ? max_f : excl;
-                            const bool nm = ok && sv > pb;
-                            bool marked = ok && ((M >> lane) & 1ULL);
-                            if (marks) marked = marked || (ok && ((ring[(j >> 5) & (RING_WORDS - 1)] >> (j & 31)) & 1u));
-                            const bool plus = ok && !nm && marked;
-                            const uint64_t nmM = ballot(nm), plusM = ballot(plus), inrM = ballot(inr);
-                            uint64_t eff = ~0ULL, brkM = 0;
-                            if (plusM) {
-                                int32_t sa = nm ? -1 : (plus ? 1 : 0), sb = 0;
-                                scan_nskip(sa, sb);
-                                const int32_t na = (n_skip + sa) > sb ? (n_skip + sa) : sb;
-                                brkM = ballot(plus && na > P.max_skip);
-                                if (brkM) eff = lanemask_lt_of(ctz64(brkM));
-                                else n_skip = rdl(na, 63);
-                            } else {
-                                n_skip -= __popcll(nmM);
-                                n_skip = n_skip > 0 ? n_skip : 0;
-                            }
-                            const uint64_t nmm = nmM & eff;
-                            if (nmm) { const int L = 63 - clz64(nmm); max_f = rdl(sv, L); max_j = jtop - L; }
-                            cpairs += (uint64_t)__popcll(brkM ? (inrM & (eff | (1ULL << ctz64(brkM)))) : inrM);
-                            if (brkM) break;
-                            // a deeper step follows: record this step's marks below its window
-                            if (jtop - 64 >= lo) {
-                                const bool mk_out = mk && !mk_in;
-                                if (any(mk_out)) {
-                                    if (mk_out) atomicOr(&ring[(ppj >> 5) & (RING_WORDS - 1)], 1u << (ppj & 31));
-                                    marks = true;
-                                }
-                                wave_lds_sync();
-                            }
-                        }
-                        // clear this i's marks (all targets lie in [lo, i-1])
-                        if (marks) {
-                            const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
-#pragma clang loop vectorize(disable) unroll(disable)
-                            for (int32_t c0 = w0; c0 <= w1; c0 += 64) {
-                                const int32_t wd = c0 + lane;
-                                if (wd <= w1) ring[wd & (RING_WORDS - 1)] = 0;
-                            }
-                        }
-                        if (lane == 0) rfp[i & (RK - 1)] = make_int2(max_f, max_j);
-                        wp = shr1_dpp(wp, pi); wq = shr1_dpp(wq, qi); wf = shr1_dpp(wf, max_f); wpp = shr1_dpp(wpp, max_j);
-                    }
-                    wave_lds_sync();
-                    // flush f/pprev of the block; segment best (last index with max f)
-                    const int2 ev = rfp[il & (RK - 1)];
-                    if (valid) { F[CK(il, A)] = ev.x; PP[CK(il, A)] = ev.y; }
-                    const int32_t fv = valid ? ev.x : INT_MIN;
-                    const int32_t bm = rdl(scan_max(fv), 63);
-                    best_merge(best_f, best_i, bm, i0 + 63 - clz64(ballot(valid && fv == bm)));
+            const bool big = vs && len > MED;
+            const uint64_t bigM = ballot(big);
+            if (bigM) {
+                uint32_t q0 = 0;
+                if (lane == 0) q0 = atomicAdd(a.lseg_n, (uint32_t)__popcll(bigM));
+                q0 = (uint32_t)uni((int32_t)q0);
+                if (big) {
+                    const uint32_t q = q0 + (uint32_t)__popcll(bigM & lanemask_lt());
+                    if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)s0, (uint32_t)e0, 0u);
                 }
-            }
+                n_big += (uint32_t)__popcll(bigM);
+                const int32_t ml = rdl(scan_max(big ? len : 0), 63);
+                max_seg = max_seg > ml ? max_seg : ml;
+                            }
         }
         // ---- 3. medium segments, one lane each: chain_dp_all (lchain.rs:73-90)
         // as a flattened per-lane state machine (advance st | evaluate one j |
@@ -1060,56 +909,283 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_dp(ChainArgs a) {
             }
             vm_drain();
         }
-        // merge lane bests (tiny segments) with the cooperative best
+        // the read's best over tiny + medium segments
         {
             const int32_t m = rdl(scan_max(bf), 63);
             const int32_t mi = rdl(scan_max(bf == m ? bi : -1), 63);
-            best_merge(best_f, best_i, m, mi);
+            const uint64_t wpairs = uni64(wave_sum64(pairs));
+            if (lane == 0) {
+                if (mi >= 0) atomicMax(a.rbest + r, best_key(m, mi));
+                atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)wpairs);
+                ReadOut* O = a.out + r;
+                O->t_pass[P.pass] = (uint32_t)(wall_clock64() - t_start);
+                const uint32_t st6 = (uint32_t)(max_seg > 65535 ? 65535 : max_seg) | ((n_big > 65535 ? 65535u : n_big) << 16);
+                if (P.pass == 0) O->pad2 = st6; else O->n_deep = st6;
+            }
         }
-        vm_drain();
-        TRACE(tr, 2, 7);
-        // ---- fallback chain walk (lchain.rs:162-171), chain ranges, rescue test.
-        // All lanes walk together (same address each step, uniform loop).
-        uint32_t* CB = a.chain + base;
-        int32_t idx = best_i, root = best_i, cm = 0;
-        while (idx >= 0 && cm < A) {
-            if (lane == 0) CB[cm] = (uint32_t)idx;
-            ++cm; root = idx;
-            idx = uni(PP[CK(idx, A)]);
-        }
-        const uint64_t kb = uni64(K[CK(best_i, A)]), kr = uni64(K[CK(root, A)]);
-        const uint32_t g = (uint32_t)(kb >> gsh);
-        const int32_t qe = (int32_t)(kb & qmask) + 1;
-        int32_t qs = (int32_t)(kr & qmask) - (span - 1); if (qs < 0) qs = 0;
-        int32_t ts, te;
-        if (g == 2u * a.kl.n_seq) { ts = 0; te = -1; }    // Q19: rpos = p - 2^31 < 0
-        else {
-            te = (int32_t)((kb >> qb) & rmask) + 1;
-            ts = (int32_t)((kr >> qb) & rmask) - (span - 1); if (ts < 0) ts = 0;
-        }
-        int32_t fl = RF_MAPPED | (flags0 & RF_RESCUED);
-        if (g == 2u * a.kl.n_seq) fl |= RF_PANIC;
-        if (P.pass == 0) {
-            int32_t cov = qe - qs; if (cov < 0) cov = 0;
-            int32_t unc = qlen - cov; if (unc < 0) unc = 0;
-            if (unc > P.rescue_size || (float)cov < (float)qlen * P.rescue_ratio_f) fl |= RF_RESCUED;
-        }
-        const uint64_t prev_pairs = P.pass == 0 ? 0ULL : uni64(a.out[r].dp_pairs);
-        const uint64_t wpairs = uni64(wave_sum64(pairs)) + cpairs;
-        if (lane == 0) {
-            ReadOut* O = a.out + r;
-            O->flags = fl; O->n_anchors = A; O->qlen = qlen;
-            O->score = best_f; O->cm = cm; O->qs = qs; O->qe = qe; O->ts = ts; O->te = te;
-            O->group = (int32_t)g; O->best_i = best_i;
-            O->dp_pairs = prev_pairs + wpairs;
-            O->t_pass[P.pass] = (uint32_t)(wall_clock64() - t_start);
-            O->pad2 = P.pass == 0 ? ((uint32_t)(max_seg > 65535 ? 65535 : max_seg) | ((n_big > 65535 ? 65535u : n_big) << 16))
-                                  : O->pad2;
-            if (P.pass == 0) { O->n_noniso = n_noniso; O->n_steps = n_steps; O->n_deep = n_deep; }
-            else { O->n_noniso += n_noniso; O->n_steps += n_steps; O->n_deep += n_deep; }
-        }
-        TRACE(tr, 2, 9);
     }
+}
+
+// long segments by descending length (largest-first hand-out to k_chain_long)
+__global__ __launch_bounds__(1024) void k_lseg_order(const uint32_t* lseg_n, uint32_t cap, const uint4* lseg, uint32_t* order) {
+    __shared__ uint32_t hist[33], offs[33];
+    const int tid = threadIdx.x;
+    const uint32_t n = min(*lseg_n, cap);
+    if (tid < 33) hist[tid] = 0;
+    __syncthreads();
+    for (uint32_t q = tid; q < n; q += 1024) {
+        const uint32_t c = lseg[q].z - lseg[q].y;
+        atomicAdd(&hist[32 - (32 - __builtin_clz(c | 1))], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) { uint32_t run = 0; for (int b = 0; b < 33; ++b) { offs[b] = run; run += hist[b]; } }
+    __syncthreads();
+    for (uint32_t q = tid; q < n; q += 1024) {
+        const uint32_t c = lseg[q].z - lseg[q].y;
+        order[atomicAdd(&offs[32 - (32 - __builtin_clz(c | 1))], 1u)] = q;
+    }
+}
+
+// ---- 5b. one long segment per wave, wave-cooperative (heaviest first)
+__global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const ChainKParams P = a.P;
+    int16_t* lut = (int16_t*)smem;
+    const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
+    uint32_t* rings = (uint32_t*)(smem + lut_bytes);
+    uint64_t* rkeys = (uint64_t*)(rings + DP_NW * RING_WORDS);
+    int2* rfps = (int2*)(rkeys + DP_NW * RK);
+    for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
+    for (int i = threadIdx.x; i < DP_NW * RING_WORDS; i += blockDim.x) rings[i] = 0;
+    __syncthreads();
+    const int lane = lane_id(), wv = wave_id();
+    uint32_t* ring = rings + wv * RING_WORDS;
+    uint64_t* rkey = rkeys + wv * RK;
+    int2* rfp = rfps + wv * RK;
+    const uint32_t qb = a.kl.qb, rb = a.kl.rb;
+    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
+    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    const uint32_t nl = min((uint32_t)uni((int32_t)*a.lseg_n), a.lseg_cap);
+    const uint32_t nwaves = gridDim.x * DP_NW;
+    for (uint32_t t = blockIdx.x * DP_NW + wv; t < nl; t += nwaves) {
+        const uint32_t q = (uint32_t)uni((int32_t)a.lseg_order[t]);
+        const uint4 L = a.lseg[q];
+        const uint32_t r = (uint32_t)uni((int32_t)L.x);
+        const int32_t s = uni((int32_t)L.y), e = uni((int32_t)L.z);
+        if (t < 256) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
+        const uint64_t base = uni64(a.a_off[r]);
+        const int32_t A = (int32_t)(uni64(a.a_off[r + 1]) - base);
+        const uint64_t* K = a.keys + base;
+        int32_t* F = a.f + base; int32_t* PP = a.pp + base;
+        uint64_t cpairs = 0;
+        uint32_t n_steps = 0, n_deep = 0;
+        int32_t best_f = INT_MIN, best_i = -1;
+        (void)A; (void)n_deep;
+        // ---- cooperative DP of segment [s, e): anchor s is isolated, every
+        // later anchor has a candidate predecessor.  The 64 newest
+        // predecessors (rpos, qpos, f, pprev; lane l <-> j = i-1-l) live in
+        // registers and shift one lane per anchor (DPP wave_shr); the newest
+        // RK keys and f/pprev also go to the wave's LDS ring for the st
+        // window and deep steps; older ones come from HBM (flushed per block).
+        int32_t st = s, stb = INT_MIN / 2, skv = INT_MIN / 2;   // st window [stb, stb+63], valid up to skv
+        uint64_t sk = 0;
+        int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
+        uint64_t nk = (s + lane < e) ? K[s + lane] : 0;
+        for (int32_t i0 = s; i0 < e; i0 += 64) {
+            const uint64_t ak = nk;
+            const int32_t il = i0 + lane;
+            const bool valid = il < e;
+            nk = (il + 64 < e) ? K[il + 64] : 0;
+            const int32_t ring_lo = i0 + 64 - RK;   // ring holds anchors [max(s, ring_lo), i0+63]
+            rkey[il & (RK - 1)] = ak;
+            if (il == s) rfp[il & (RK - 1)] = make_int2(span, -1);
+            wave_lds_sync();
+            bool drained = false;
+            const int32_t ib = i0 == s ? s + 1 : i0;
+            const int32_t ie = e < i0 + 64 ? e : i0 + 64;
+            if (i0 == s) {   // anchor s enters the register window
+                const uint64_t k0 = rdl64(ak, 0);
+                wp = shr1_dpp(wp, (int32_t)((k0 >> qb) & rmask)); wq = shr1_dpp(wq, (int32_t)(k0 & qmask));
+                wf = shr1_dpp(wf, span); wpp = shr1_dpp(wpp, -1);
+            }
+            for (int32_t i = ib; i < ie; ++i) {
+                const uint64_t ki = rdl64(ak, i - i0);
+                const int32_t pi = (int32_t)((ki >> qb) & rmask);
+                const int32_t qi = (int32_t)(ki & qmask);
+                // st (lchain.rs:75): first j >= st with rpos_i <= rpos_j + max_dist_x
+                for (;;) {
+                    if (st < stb || st >= stb + 64 || (i > skv && skv < stb + 63)) {
+                        stb = st;
+                        skv = i0 + 63;
+                        const int32_t j = stb + lane;
+                        sk = 0;
+                        if (j < e) sk = j >= ring_lo ? rkey[j & (RK - 1)] : K[j];
+                    }
+                    const int32_t j = stb + lane;
+                    const int32_t pj = (int32_t)((sk >> qb) & rmask);
+                    const bool cand = j >= st && j <= i;
+                    const bool stop = cand && (j == i || !(pi > (int32_t)((uint32_t)pj + (uint32_t)maxdx)));
+                    const uint64_t m = ballot(stop);
+                    if (m) { st = stb + ctz64(m); break; }
+                    st = stb + 64;
+                }
+                const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
+                int32_t max_f = span, max_j = -1, n_skip = 0;
+                bool marks = false;
+                for (int32_t jtop = i - 1; jtop >= lo; jtop -= 64) {
+                    const int32_t j = jtop - lane;
+                    const bool inr = j >= lo;
+                    int32_t pj, qj, fj, ppj;
+                    if (jtop == i - 1) { pj = wp; qj = wq; fj = wf; ppj = wpp; }
+                    else {
+                        const bool deep = inr && j < ring_lo;
+                        const bool any_deep = any(deep);
+                        n_deep += any_deep ? 1u : 0u;
+                        if (any_deep && !drained) { vm_drain(); drained = true; }   // f/pprev flushes
+                        uint64_t kj = 0;
+                        int2 fpj = make_int2(0, -1);
+                        if (inr) {
+                            if (!deep) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
+                            else { kj = K[CK(j, A)]; fpj = make_int2(F[CK(j, A)], PP[CK(j, A)]); }
+                        }
+                        pj = (int32_t)((kj >> qb) & rmask); qj = (int32_t)(kj & qmask); fj = fpj.x; ppj = fpj.y;
+                    }
+                    ++n_steps;
+                    // comput_sc (lchain.rs:17-34)
+                    const int32_t dq = qi - qj, dr = pi - pj;
+                    bool ok = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
+                    const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                    ok = ok && dd <= bw;
+                    const int32_t dg = dr < dq ? dr : dq;
+                    const int32_t sc = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
+                    const int32_t sv = sc + fj;
+                    // t[pprev[j]] = i  (lchain.rs:86); targets below lo are never read.
+                    // Targets inside this step's window (j' in [jtop-63, jtop]) are a
+                    // 64-bit mask built by a DPP OR-reduction; only targets below it
+                    // (read by a later, deeper step) and marks of earlier steps use
+                    // the LDS ring.
+                    const bool mk = ok && ppj >= lo;
+                    const int32_t tb = jtop - ppj;                 // target lane
+                    const bool mk_in = mk && tb < 64;
+                    const uint64_t tbit = mk_in ? (1ULL << (tb & 63)) : 0ULL;
+                    const uint64_t M = ((uint64_t)wave_or32((uint32_t)(tbit >> 32)) << 32) | wave_or32((uint32_t)tbit);
+                    // strict new maximum in processing order
+                    const int32_t v = ok ? sv : INT_MIN;
+                    const int32_t excl = shr1_dpp(scan_max(v), INT_MIN);
+                    const int32_t pb = max_f > excl ? max_f : excl;
+                    const bool nm = ok && sv > pb;
+                    bool marked = ok && ((M >> lane) & 1ULL);
+                    if (marks) marked = marked || (ok && ((ring[(j >> 5) & (RING_WORDS - 1)] >> (j & 31)) & 1u));
+                    const bool plus = ok && !nm && marked;
+                    const uint64_t nmM = ballot(nm), plusM = ballot(plus), inrM = ballot(inr);
+                    uint64_t eff = ~0ULL, brkM = 0;
+                    if (plusM) {
+                        int32_t sa = nm ? -1 : (plus ? 1 : 0), sb = 0;
+                        scan_nskip(sa, sb);
+                        const int32_t na = (n_skip + sa) > sb ? (n_skip + sa) : sb;
+                        brkM = ballot(plus && na > P.max_skip);
+                        if (brkM) eff = lanemask_lt_of(ctz64(brkM));
+                        else n_skip = rdl(na, 63);
+                    } else {
+                        n_skip -= __popcll(nmM);
+                        n_skip = n_skip > 0 ? n_skip : 0;
+                    }
+                    const uint64_t nmm = nmM & eff;
+                    if (nmm) { const int L = 63 - clz64(nmm); max_f = rdl(sv, L); max_j = jtop - L; }
+                    cpairs += (uint64_t)__popcll(brkM ? (inrM & (eff | (1ULL << ctz64(brkM)))) : inrM);
+                    if (brkM) break;
+                    // a deeper step follows: record this step's marks below its window
+                    if (jtop - 64 >= lo) {
+                        const bool mk_out = mk && !mk_in;
+                        if (any(mk_out)) {
+                            if (mk_out) atomicOr(&ring[(ppj >> 5) & (RING_WORDS - 1)], 1u << (ppj & 31));
+                            marks = true;
+                        }
+                        wave_lds_sync();
+                    }
+                }
+                // clear this i's marks (all targets lie in [lo, i-1])
+                if (marks) {
+                    const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
+#pragma clang loop vectorize(disable) unroll(disable)
+                    for (int32_t c0 = w0; c0 <= w1; c0 += 64) {
+                        const int32_t wd = c0 + lane;
+                        if (wd <= w1) ring[wd & (RING_WORDS - 1)] = 0;
+                    }
+                }
+                if (lane == 0) rfp[i & (RK - 1)] = make_int2(max_f, max_j);
+                wp = shr1_dpp(wp, pi); wq = shr1_dpp(wq, qi); wf = shr1_dpp(wf, max_f); wpp = shr1_dpp(wpp, max_j);
+            }
+            wave_lds_sync();
+            // flush f/pprev of the block; segment best (last index with max f)
+            const int2 ev = rfp[il & (RK - 1)];
+            if (valid) { F[CK(il, A)] = ev.x; PP[CK(il, A)] = ev.y; }
+            const int32_t fv = valid ? ev.x : INT_MIN;
+            const int32_t bm = rdl(scan_max(fv), 63);
+            best_merge(best_f, best_i, bm, i0 + 63 - clz64(ballot(valid && fv == bm)));
+        }
+        if (lane == 0) {
+            atomicMax(a.rbest + r, best_key(best_f, best_i));
+            atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)cpairs);
+            atomicAdd(&a.out[r].n_noniso, (uint32_t)(e - s - 1));
+            atomicAdd(&a.out[r].n_steps, n_steps);
+        }
+    }
+}
+
+// ---- 5c. per read: fallback chain walk (lchain.rs:162-171), chain_qrange /
+// chain_trange (178-200) and the rescue test of rescue_long_join (316-330).
+__global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.n) return;
+    const ChainKParams P = a.P;
+    ReadOut* O = a.out + r;
+    const int32_t flags0 = O->flags;
+    if (P.pass == 1 && !(flags0 & RF_RESCUED)) return;
+    const uint64_t base = a.a_off[r];
+    const int32_t A = (int32_t)(a.a_off[r + 1] - base);
+    const int32_t qlen = (int32_t)(a.rd_off[r + 1] - a.rd_off[r]);
+    if (A == 0) {
+        O->flags = flags0 & RF_EMPTY; O->n_anchors = 0; O->score = 0; O->cm = 0;
+        O->qs = O->qe = O->ts = O->te = 0; O->group = 0; O->best_i = -1; O->qlen = qlen;
+        return;
+    }
+    const uint32_t qb = a.kl.qb, rb = a.kl.rb;
+    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
+    const uint32_t gsh = rb + qb;
+    const int32_t span = P.span;
+    const unsigned long long bk = a.rbest[r];
+    const int32_t best_f = (int32_t)((uint32_t)(bk >> 32) ^ 0x80000000u), best_i = (int32_t)(uint32_t)bk;
+    const uint64_t* K = a.keys + base;
+    const int32_t* PP = a.pp + base;
+    uint32_t* CB = a.chain + base;
+    int32_t idx = best_i, root = best_i, cm = 0;
+    while (idx >= 0 && cm < A) {
+        CB[cm] = (uint32_t)idx;
+        ++cm; root = idx;
+        idx = PP[CK(idx, A)];
+    }
+    const uint64_t kb = K[CK(best_i, A)], kr = K[CK(root, A)];
+    const uint32_t g = (uint32_t)(kb >> gsh);
+    const int32_t qe = (int32_t)(kb & qmask) + 1;
+    int32_t qs = (int32_t)(kr & qmask) - (span - 1); if (qs < 0) qs = 0;
+    int32_t ts, te;
+    if (g == 2u * a.kl.n_seq) { ts = 0; te = -1; }    // Q19: rpos = p - 2^31 < 0
+    else {
+        te = (int32_t)((kb >> qb) & rmask) + 1;
+        ts = (int32_t)((kr >> qb) & rmask) - (span - 1); if (ts < 0) ts = 0;
+    }
+    int32_t fl = RF_MAPPED | (flags0 & RF_RESCUED);
+    if (g == 2u * a.kl.n_seq) fl |= RF_PANIC;
+    if (P.pass == 0) {
+        int32_t cov = qe - qs; if (cov < 0) cov = 0;
+        int32_t unc = qlen - cov; if (unc < 0) unc = 0;
+        if (unc > P.rescue_size || (float)cov < (float)qlen * P.rescue_ratio_f) fl |= RF_RESCUED;
+    }
+    O->flags = fl; O->n_anchors = A; O->qlen = qlen;
+    O->score = best_f; O->cm = cm; O->qs = qs; O->qe = qe; O->ts = ts; O->te = te;
+    O->group = (int32_t)g; O->best_i = best_i;
 }
 
 // order[t] = reads by descending anchor count (largest-first hand-out to the
@@ -1267,11 +1343,14 @@ int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp
 static size_t chain_lds(int lut_n) {
     return (size_t)(((lut_n * 2) + 15) & ~15) + (size_t)DP_NW * (RING_WORDS * 4 + RK * 8 + RK * 8);
 }
-int chain_max_blocks(int lut_n) {
+static size_t seg_lds(int lut_n) { return (size_t)(((lut_n * 2) + 15) & ~15); }
+int chain_max_blocks(int lut_n, int which) {
     int dev = 0, ncu = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_dp, DP_NW * 64, chain_lds(lut_n)) != hipSuccess) return 0;
+    hipError_t e = which == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_seg, DP_NW * 64, seg_lds(lut_n))
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_long, DP_NW * 64, chain_lds(lut_n));
+    if (e != hipSuccess) return 0;
     return ncu * (per > 0 ? per : 1);
 }
 int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStream_t st) {
@@ -1280,9 +1359,15 @@ int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStr
     LAUNCH_CHECK();
     return 0;
 }
-int launch_chain(const ChainArgs& a, int n_blocks, hipStream_t st) {
-    const size_t lds = chain_lds(a.P.lut_n);
-    hipLaunchKernelGGL(k_chain_dp, dim3(n_blocks), dim3(DP_NW * 64), lds, st, a);
+int launch_chain(const ChainArgs& a, int seg_blocks, int long_blocks, hipStream_t st) {
+    if (a.n == 0) return 0;
+    hipLaunchKernelGGL(k_chain_seg, dim3(seg_blocks), dim3(DP_NW * 64), seg_lds(a.P.lut_n), st, a);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, (const uint32_t*)a.lseg_n, a.lseg_cap, (const uint4*)a.lseg, a.lseg_order);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_chain_long, dim3(long_blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
     LAUNCH_CHECK();
     return 0;
 }
