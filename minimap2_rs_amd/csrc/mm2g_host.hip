@@ -74,7 +74,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, dv_separate = false;
@@ -479,23 +479,27 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->lseg_order, uint32_t, lcap, lseg_order);
     ENSURE(c->lseg_n, uint32_t, 4, lseg_n);
     ENSURE(c->rbest, unsigned long long, n, rbest);
+    const uint32_t mcap2 = (uint32_t)std::min<uint64_t>(A / (CHAIN_TINY + 1) + 64, 0xffffffffu);
+    uint4* mseg;
+    ENSURE(c->mseg, uint4, mcap2, mseg);
     LCHK(launch_read_order(n, a_cnt, order, c->stream));
     ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work,
                  std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, nullptr, order, A, std::min<int32_t>((int32_t)n, 4 * 256), tmark,
-                 lseg, lseg_n, lcap, lseg_order, rbest};
+                 lseg, lseg_n, lcap, lseg_order, rbest, mseg, lseg_n + 2, lseg_n + 3, mcap2};
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) {
             ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
             ca.P.lut_n = o->bw_long + 1; ca.lseg_n = lseg_n + 1;
         }
-        int sb = chain_max_blocks(ca.P.lut_n, 0), lb = chain_max_blocks(ca.P.lut_n, 1);
+        int sb = chain_max_blocks(ca.P.lut_n, 0), lb = chain_max_blocks(ca.P.lut_n, 1), mb = chain_max_blocks(ca.P.lut_n, 2);
         if (sb <= 0) sb = 1024;
         if (lb <= 0) lb = 1024;
+        if (mb <= 0) mb = 1024;
         sb = std::max(1, std::min((int)((n + 3) / 4), sb));
         HIPCHK(hipMemsetAsync(rbest, 0, (size_t)n * 8, c->stream));
-        HIPCHK(hipMemsetAsync(ca.lseg_n, 0, 4, c->stream));
+        HIPCHK(hipMemsetAsync(lseg_n, 0, 16, c->stream));   // long count (pass 0/1 slot), medium count, medium taken
         ProfScope ps(c, pass == 0 ? "chain_dp" : "chain_dp_rescue");
-        LCHK(launch_chain(ca, sb, lb, c->stream));
+        LCHK(launch_chain(ca, sb, mb, lb, c->stream));
     }
     // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
     const bool sep = (H.w != o->w || H.k != o->k);

@@ -127,6 +127,10 @@ struct ChainArgs {
     uint32_t lseg_cap;
     uint32_t* lseg_order;    // long segments, longest first
     unsigned long long* rbest;   // per read: packed (f, index) of the last argmax f
+    uint4* mseg;             // medium-segment queue: (read, s, e, -)
+    uint32_t* mseg_n;        // its length (atomic counter)
+    uint32_t* mseg_take;     // next entry to hand out (atomic counter)
+    uint32_t mseg_cap;
 };
 struct DvArgs {
     uint32_t n;
@@ -148,9 +152,9 @@ int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st);
 // MM2G_CHECKED builds: first recorded bounds violation {line, index, cap}; 0 = none
 int mm2g_checked_read(unsigned long long out[4], hipStream_t st);
-// chain DP of one pass: k_chain_seg, k_lseg_order, k_chain_long, k_chain_fin
-int launch_chain(const mm2g::ChainArgs& a, int seg_blocks, int long_blocks, hipStream_t st);
-int chain_max_blocks(int lut_n, int which);   // co-resident workgroups (0 = k_chain_seg, 1 = k_chain_long)
+// chain DP of one pass: k_chain_seg, k_chain_med, k_lseg_order, k_chain_long, k_chain_fin
+int launch_chain(const mm2g::ChainArgs& a, int seg_blocks, int med_blocks, int long_blocks, hipStream_t st);
+int chain_max_blocks(int lut_n, int which);   // co-resident workgroups (0 = k_chain_seg, 1 = k_chain_long, 2 = k_chain_med)
 int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStream_t st);
 int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st);

@@ -682,16 +682,22 @@ DEVI void best_merge(int32_t& bf, int32_t& bi, int32_t f, int32_t i) {
     if (f > bf || (f == bf && i > bi)) { bf = f; bi = i; }
 }
 
+constexpr int KRING = 512;        // per-wave LDS ring of the newest anchor keys (k_chain_seg)
+constexpr int TQ = 128;           // per-wave LDS queue per tiny length class (2 | 3-4 | 5-8 anchors)
+constexpr int MEDB = 128;         // per-wave LDS buffer of medium segments before the global append
+constexpr int64_t EST_LANE = 2048;   // estimated DP pairs above which a segment goes to a whole wave
+
 // Scalar chain_dp_all (lchain.rs:73-90) of one segment of <= TINY anchors held
-// in registers; `act` lanes only.  Local indices; marks t[pprev[j]] = i are a
+// in registers (keys from the wave's LDS key ring); `act` lanes only.  Local indices; marks t[pprev[j]] = i are a
 // per-i bitmask (t is only ever compared with the current i).
-DEVI void tiny_segment_dp(bool act, int32_t len, const uint64_t* K, int32_t s, int32_t* F, int32_t* PP, const int16_t* lut,
+template <int N>
+DEVI void tiny_segment_dp(bool act, int32_t len, const uint64_t* kring, int32_t s, int32_t* F, int32_t* PP, const int16_t* lut,
                           const ChainKParams& P, uint32_t qb, uint64_t qmask, uint64_t rmask, int32_t& bf, int32_t& bi,
                           uint64_t& pairs) {
-    int32_t pp_[TINY], qq_[TINY], f_[TINY], pv_[TINY];
+    int32_t pp_[N], qq_[N], f_[N], pv_[N];
 #pragma unroll
-    for (int m = 0; m < TINY; ++m) {
-        const uint64_t k = (act && m < len) ? K[s + m] : 0;
+    for (int m = 0; m < N; ++m) {
+        const uint64_t k = (act && m < len) ? kring[(s + m) & (KRING - 1)] : 0;
         pp_[m] = (int32_t)((k >> qb) & rmask); qq_[m] = (int32_t)(k & qmask);
         f_[m] = P.span; pv_[m] = -1;
     }
@@ -699,7 +705,7 @@ DEVI void tiny_segment_dp(bool act, int32_t len, const uint64_t* K, int32_t s, i
     int32_t st = 0;
     uint32_t npairs = 0;
 #pragma unroll
-    for (int i = 1; i < TINY; ++i) {
+    for (int i = 1; i < N; ++i) {
         const bool ai = act && i < len;
         // st (lchain.rs:75); every anchor of the segment is in i's group
 #pragma unroll
@@ -729,7 +735,7 @@ DEVI void tiny_segment_dp(bool act, int32_t len, const uint64_t* K, int32_t s, i
         if (ai) { f_[i] = max_f; pv_[i] = max_j; }
     }
 #pragma unroll
-    for (int m = 0; m < TINY; ++m)
+    for (int m = 0; m < N; ++m)
         if (act && m < len) {
             F[s + m] = f_[m];
             PP[s + m] = pv_[m] >= 0 ? s + pv_[m] : -1;
@@ -743,22 +749,35 @@ DEVI unsigned long long best_key(int32_t f, int32_t i) {
     return ((unsigned long long)((uint32_t)f ^ 0x80000000u) << 32) | (uint32_t)i;
 }
 
-// ---- 5a. per read: segments, tiny + medium segments one-per-lane, long
-// segments queued for k_chain_long.  Dynamic-programming state of every
-// segment stays inside it (DESIGN.md "Chain DP"), so the three parts write
-// disjoint f/pprev ranges; the read's best (last argmax f) is merged with a
-// packed 64-bit atomicMax.
+// ---- 5a. per read, one streaming pass over the sorted anchors: isolated
+// anchors (st(i) == i: i == 0, another (rid, strand) group than i-1, or
+// rpos_i > rpos_{i-1} + max_dist_x) delimit independent segments — the DP of
+// a segment never reads outside it (DESIGN.md "Chain DP").  Completed
+// segments queue in LDS; per batch of 64, tiny ones run one-per-lane in
+// registers (keys from the LDS key ring), the others are routed by their
+// estimated pair count to k_chain_med (one lane each) or k_chain_long (one
+// wave each).  The read's best (last argmax f) is merged with a packed
+// 64-bit atomicMax.
 __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
+    const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
+    uint64_t* krings = (uint64_t*)(smem + lut_bytes);
+    int32_t* tqs = (int32_t*)(krings + DP_NW * KRING);          // 3 classes x TQ segment starts
+    uint8_t* tls = (uint8_t*)(tqs + DP_NW * 3 * TQ);            // their lengths
+    int2* medbs = (int2*)(tls + DP_NW * 3 * TQ);
     for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
     __syncthreads();
     const int lane = lane_id(), wv = wave_id();
+    uint64_t* kring = krings + wv * KRING;
+    int32_t* tq = tqs + wv * 3 * TQ;
+    uint8_t* tl = tls + wv * 3 * TQ;
+    int2* medb = medbs + wv * MEDB;
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const uint32_t gsh = rb + qb;
-    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    const int32_t maxdx = P.max_dist_x, span = P.span;
     // Static, wave-uniform assignment of reads in `order` (heaviest first).
     const uint32_t nwaves = gridDim.x * DP_NW;
     for (uint32_t t = blockIdx.x * DP_NW + wv; t < a.n; t += nwaves) {
@@ -776,140 +795,132 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
 #endif
         const uint64_t* K = a.keys + base;
         int32_t* F = a.f + base; int32_t* PP = a.pp + base;
-        uint32_t* SEG = a.chain + a.a_total + base;   // segment starts (scratch; second half of the chain buffer)
         uint64_t pairs = 0;
         uint32_t n_big = 0;
         int32_t max_seg = 0;
-        // ---- 1. segments: an isolated anchor (st(i) == i: i == 0, another
-        // (rid, strand) group than i-1, or rpos_i > rpos_{i-1} + max_dist_x)
-        // starts a segment; the DP of a segment never reads outside it.
-        int32_t nseg = 0;
-        {
-            uint32_t prev_lo = 0, prev_hi = 0;
-            uint64_t nk = lane < A ? K[lane] : 0;
-            for (int32_t i0 = 0; i0 < A; i0 += 64) {
-                const uint64_t ak = nk;
-                const int32_t il = i0 + lane;
-                const bool valid = il < A;
-                nk = (il + 64 < A) ? K[il + 64] : 0;
-                const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)prev_hi) << 32) |
-                                    (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)prev_lo);
-                const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
-                const int32_t p = (int32_t)((ak >> qb) & rmask), pprv = (int32_t)((pk >> qb) & rmask);
-                const bool iso = valid && (il == 0 || g != gp || p > (int32_t)((uint32_t)pprv + (uint32_t)maxdx));
-                const uint64_t isoM = ballot(iso);
-                if (iso) SEG[CK(nseg + __popcll(isoM & lanemask_lt()), A)] = (uint32_t)il;
-                nseg += __popcll(isoM);
-                prev_lo = rdlu((uint32_t)ak, 63); prev_hi = rdlu((uint32_t)(ak >> 32), 63);
+        int32_t bf = INT_MIN, bi = -1;      // per-lane best (singletons and tiny segments)
+        int32_t pend = -1;                  // start of the open segment
+        int32_t th0 = 0, th1 = 0, th2 = 0, tt0 = 0, tt1 = 0, tt2 = 0;   // tiny class queue heads / tails
+        int32_t nmb = 0;                    // medium buffer fill (uniform)
+        // one batch of a tiny class queue (cls 0: 2 anchors, 1: 3-4, 2: 5-8)
+        auto tiny_batch = [&](int cls, int32_t& h, int32_t cnt) {
+            const bool vs = lane < cnt;
+            const int slot = cls * TQ + ((h + lane) & (TQ - 1));
+            const int32_t s0 = vs ? tq[slot] : 0;
+            const int32_t len = vs ? (int32_t)tl[slot] : 0;
+            if (cls == 0) tiny_segment_dp<2>(vs, len, kring, s0, F, PP, lut, P, qb, qmask, rmask, bf, bi, pairs);
+            else if (cls == 1) tiny_segment_dp<4>(vs, len, kring, s0, F, PP, lut, P, qb, qmask, rmask, bf, bi, pairs);
+            else tiny_segment_dp<8>(vs, len, kring, s0, F, PP, lut, P, qb, qmask, rmask, bf, bi, pairs);
+            h += cnt;
+            wave_lds_sync();
+        };
+        // medium buffer -> global queue for k_chain_med (one atomic per 64)
+        auto flush_med = [&](int32_t cnt) {
+            uint32_t q0 = 0;
+            if (lane == 0) q0 = atomicAdd(a.mseg_n, (uint32_t)cnt);
+            q0 = (uint32_t)uni((int32_t)q0);
+            if (lane < cnt) {
+                const int2 m = medb[lane];
+                const uint32_t q = q0 + (uint32_t)lane;
+                if (q < a.mseg_cap) a.mseg[q] = make_uint4(r, (uint32_t)m.x, (uint32_t)m.y, 0u);
             }
-        }
-        vm_drain();
-        // ---- 2. per batch of 64 segments: tiny ones one-per-lane in registers,
-        // medium ones queued per read, long ones queued globally
-        int32_t bf = INT_MIN, bi = -1;      // per-lane best (tiny and medium segments)
-        uint32_t* MEDL = a.chain + base;    // medium segments (s, e) (scratch: the chain slots, written last)
-        int32_t nmed = 0;
-        for (int32_t b0 = 0; b0 < nseg; b0 += 64) {
-            const int32_t k = b0 + lane;
-            const bool vs = k < nseg;
-            const int32_t s0 = vs ? (int32_t)SEG[CK(k, A)] : 0;
-            const int32_t e0 = vs ? (k + 1 < nseg ? (int32_t)SEG[CK(k + 1, A)] : A) : 0;
-            const int32_t len = e0 - s0;
-            const bool tiny = vs && len <= TINY;
-            if (any(tiny && len > 1))
-                tiny_segment_dp(tiny && len > 1, len, K, s0, F, PP, lut, P, qb, qmask, rmask, bf, bi, pairs);
-            if (tiny && len == 1) { F[s0] = span; PP[s0] = -1; best_merge(bf, bi, span, s0); }
-            const bool med = vs && len > TINY && len <= MED;
+            wave_lds_sync();
+            const int2 rest = (lane + 64 < MEDB) ? medb[lane + 64] : make_int2(0, 0);
+            wave_lds_sync();
+            if (lane + 64 < MEDB) medb[lane] = rest;
+            nmb -= cnt;
+            wave_lds_sync();
+        };
+        // route completed segments [sl, el) of the emitting lanes
+        auto route = [&](bool emit, int32_t sl, int32_t el) {
+            const int32_t len = el - sl;
+            if (emit && len == 1) { F[sl] = span; PP[sl] = -1; best_merge(bf, bi, span, sl); }
+            const bool c0 = emit && len == 2, c1 = emit && len >= 3 && len <= 4, c2 = emit && len >= 5 && len <= TINY;
+            const uint64_t m0 = ballot(c0), m1 = ballot(c1), m2 = ballot(c2);
+            const uint64_t lt = lanemask_lt();
+            if (c0) { const int sl0 = 0 * TQ + ((tt0 + __popcll(m0 & lt)) & (TQ - 1)); tq[sl0] = sl; tl[sl0] = (uint8_t)len; }
+            if (c1) { const int sl1 = 1 * TQ + ((tt1 + __popcll(m1 & lt)) & (TQ - 1)); tq[sl1] = sl; tl[sl1] = (uint8_t)len; }
+            if (c2) { const int sl2 = 2 * TQ + ((tt2 + __popcll(m2 & lt)) & (TQ - 1)); tq[sl2] = sl; tl[sl2] = (uint8_t)len; }
+            tt0 += __popcll(m0); tt1 += __popcll(m1); tt2 += __popcll(m2);
+            // longer: by estimated pairs (len x expected window) to one lane or one wave
+            bool med = false;
+            if (emit && len > TINY && len <= MED) {
+                const int32_t p0 = (int32_t)((kring[sl & (KRING - 1)] >> qb) & rmask);
+                const int32_t p1 = (int32_t)((kring[(el - 1) & (KRING - 1)] >> qb) & rmask);
+                const int64_t bp = p1 - p0 > 0 ? (int64_t)(p1 - p0) : 1;
+                int64_t win = ((int64_t)len * maxdx + bp - 1) / bp;
+                win = win < len ? win : len;
+                med = (int64_t)len * win / 2 <= EST_LANE;
+            }
+            const bool big = emit && len > TINY && !med;
             const uint64_t medM = ballot(med);
-            if (med) {
-                const int32_t q = nmed + __popcll(medM & lanemask_lt());
-                MEDL[CK(2 * q, A)] = (uint32_t)s0; MEDL[CK(2 * q + 1, A)] = (uint32_t)e0;
-            }
-            nmed += __popcll(medM);
-            const bool big = vs && len > MED;
+            if (med) medb[nmb + __popcll(medM & lt)] = make_int2(sl, el);
+            nmb += __popcll(medM);
             const uint64_t bigM = ballot(big);
-            if (bigM) {
+            if (bigM) {   // long segments: global queue for k_chain_long (rare)
                 uint32_t q0 = 0;
                 if (lane == 0) q0 = atomicAdd(a.lseg_n, (uint32_t)__popcll(bigM));
                 q0 = (uint32_t)uni((int32_t)q0);
                 if (big) {
-                    const uint32_t q = q0 + (uint32_t)__popcll(bigM & lanemask_lt());
-                    if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)s0, (uint32_t)e0, 0u);
+                    const uint32_t q = q0 + (uint32_t)__popcll(bigM & lt);
+                    if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
                 }
                 n_big += (uint32_t)__popcll(bigM);
                 const int32_t ml = rdl(scan_max(big ? len : 0), 63);
                 max_seg = max_seg > ml ? max_seg : ml;
-                            }
-        }
-        // ---- 3. medium segments, one lane each: chain_dp_all (lchain.rs:73-90)
-        // as a flattened per-lane state machine (advance st | evaluate one j |
-        // finish i) inside a wave-uniform loop; idle lanes take the next queued
-        // segment.  t[] is the reference's own mark array (t[j] == i), kept in
-        // HBM scratch and reset to -1 when anchor j is finished.
-        vm_drain();
-        if (nmed > 0) {
-            int32_t* T = a.tmark + base;
-            int32_t ms = 0, me = 0, i = 0, j = 0, lo = 0, sx = 0, max_f = 0, max_j = -1, n_skip = 0, pi = 0, qi = 0, psx = 0;
-            int32_t state = 0;                  // 0 idle, 1 advance st, 2 j-loop
-            int32_t next = 0;                   // uniform: next queued segment
-            for (;;) {
-                const bool idle = state == 0;
-                const uint64_t idleM = ballot(idle);
-                if (idleM && next < nmed) {
-                    const int32_t kq = next + __popcll(idleM & lanemask_lt());
-                    if (idle && kq < nmed) {
-                        ms = (int32_t)MEDL[CK(2 * kq, A)]; me = (int32_t)MEDL[CK(2 * kq + 1, A)];
-                        F[ms] = span; PP[ms] = -1; T[ms] = -1; best_merge(bf, bi, span, ms);
-                        const uint64_t k0 = K[ms], k1 = K[ms + 1];
-                        psx = (int32_t)((k0 >> qb) & rmask);
-                        pi = (int32_t)((k1 >> qb) & rmask); qi = (int32_t)(k1 & qmask);
-                        sx = ms; i = ms + 1; state = 1;
-                    }
-                    next += __popcll(idleM);
-                }
-                if (!any(state != 0)) break;
-                if (state == 1) {
-                    if (sx < i && pi > (int32_t)((uint32_t)psx + (uint32_t)maxdx)) {
-                        ++sx;
-                        psx = (int32_t)((K[sx] >> qb) & rmask);
-                    } else {
-                        lo = sx > i - P.max_iter ? sx : i - P.max_iter;
-                        j = i - 1; max_f = span; max_j = -1; n_skip = 0; state = 2;
-                    }
-                } else if (state == 2) {
-                    if (j >= lo) {
-                        const uint64_t kj = K[j];
-                        const int32_t fj = F[j], ppj = PP[j], tj = T[j];
-                        const int32_t pj = (int32_t)((kj >> qb) & rmask), qj = (int32_t)(kj & qmask);
-                        const int32_t dq = qi - qj, dr = pi - pj;
-                        bool ok = dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
-                        const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-                        ok = ok && dd <= bw;
-                        bool brk = false;
-                        ++pairs;
-                        if (ok) {
-                            const int32_t dg = dr < dq ? dr : dq;
-                            const int32_t sv = (span < dg ? span : dg) - (int32_t)lut[dd] + fj;
-                            if (sv > max_f) { max_f = sv; max_j = j; if (n_skip > 0) --n_skip; }
-                            else if (tj == i) { ++n_skip; if (n_skip > P.max_skip) brk = true; }
-                            if (!brk && ppj >= 0) T[ppj] = i;
-                        }
-                        j = brk ? lo - 1 : j - 1;
-                    } else {
-                        F[i] = max_f; PP[i] = max_j; T[i] = -1; best_merge(bf, bi, max_f, i);
-                        ++i;
-                        if (i >= me) state = 0;
-                        else {
-                            const uint64_t ki = K[i];
-                            pi = (int32_t)((ki >> qb) & rmask); qi = (int32_t)(ki & qmask);
-                            state = 1;
-                        }
-                    }
-                }
             }
-            vm_drain();
+            wave_lds_sync();
+            if (nmb >= 64) flush_med(64);
+        };
+        // drain tiny queues: full batches, and before the oldest start leaves the key ring
+        auto drain = [&](int32_t horizon, bool all) {
+            for (;;) {
+                const int32_t n0 = tt0 - th0;
+                if (n0 <= 0) break;
+                if (n0 < 64 && !all && uni(tq[0 * TQ + (th0 & (TQ - 1))]) >= horizon) break;
+                tiny_batch(0, th0, n0 < 64 ? n0 : 64);
+            }
+            for (;;) {
+                const int32_t n1 = tt1 - th1;
+                if (n1 <= 0) break;
+                if (n1 < 64 && !all && uni(tq[1 * TQ + (th1 & (TQ - 1))]) >= horizon) break;
+                tiny_batch(1, th1, n1 < 64 ? n1 : 64);
+            }
+            for (;;) {
+                const int32_t n2 = tt2 - th2;
+                if (n2 <= 0) break;
+                if (n2 < 64 && !all && uni(tq[2 * TQ + (th2 & (TQ - 1))]) >= horizon) break;
+                tiny_batch(2, th2, n2 < 64 ? n2 : 64);
+            }
+        };
+        uint32_t prev_lo = 0, prev_hi = 0;
+        uint64_t nk = lane < A ? K[lane] : 0;
+        for (int32_t i0 = 0; i0 < A; i0 += 64) {
+            const uint64_t ak = nk;
+            const int32_t il = i0 + lane;
+            const bool valid = il < A;
+            nk = (il + 64 < A) ? K[il + 64] : 0;
+            kring[il & (KRING - 1)] = ak;
+            const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)prev_hi) << 32) |
+                                (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)prev_lo);
+            const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
+            const int32_t p = (int32_t)((ak >> qb) & rmask), pprv = (int32_t)((pk >> qb) & rmask);
+            const bool iso = valid && (il == 0 || g != gp || p > (int32_t)((uint32_t)pprv + (uint32_t)maxdx));
+            const uint64_t isoM = ballot(iso);
+            // an isolated anchor closes the segment opened by the previous one
+            const uint64_t lower = isoM & lanemask_lt();
+            const int32_t sl = lower ? i0 + 63 - clz64(lower) : pend;
+            wave_lds_sync();
+            route(iso && sl >= 0, sl, il);
+            if (isoM) pend = i0 + 63 - clz64(isoM);
+            prev_lo = rdlu((uint32_t)ak, 63); prev_hi = rdlu((uint32_t)(ak >> 32), 63);
+            // the next block overwrites ring slots of anchors < i0 + 128 - KRING
+            drain(i0 + 192 - KRING, false);
         }
-        // the read's best over tiny + medium segments
+        route(lane == 0, pend, A);          // the last segment
+        drain(0, true);
+        if (nmb > 0) flush_med(nmb);
+        // the read's best over its singletons and tiny segments
         {
             const int32_t m = rdl(scan_max(bf), 63);
             const int32_t mi = rdl(scan_max(bf == m ? bi : -1), 63);
@@ -921,6 +932,124 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
                 O->t_pass[P.pass] = (uint32_t)(wall_clock64() - t_start);
                 const uint32_t st6 = (uint32_t)(max_seg > 65535 ? 65535 : max_seg) | ((n_big > 65535 ? 65535u : n_big) << 16);
                 if (P.pass == 0) O->pad2 = st6; else O->n_deep = st6;
+            }
+        }
+    }
+}
+
+// ---- 5b. medium segments, one lane each, from a global queue: chain_dp_all
+// (lchain.rs:73-90) as a flattened per-lane state machine (advance st |
+// evaluate up to MJ predecessors | finish i) inside a wave-uniform loop.
+// Lane g takes queue entries g, g + stride, ... (interleaved, no atomics).
+// The MJ predecessors of one iteration are loaded together; a mark
+// t[pprev[j]] = i landing on a later j of the same group is forwarded.  t[]
+// is the reference's own mark array (t[j] == i) in HBM scratch, reset to -1
+// when anchor j is finished.
+constexpr int MJ = 4;
+__global__ __launch_bounds__(256) void k_chain_med(ChainArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const ChainKParams P = a.P;
+    int16_t* lut = (int16_t*)smem;
+    for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
+    __syncthreads();
+    const uint32_t qb = a.kl.qb;
+    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << a.kl.rb) - 1;
+    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    const uint32_t nm = min((uint32_t)uni((int32_t)*a.mseg_n), a.mseg_cap);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t kq = blockIdx.x * blockDim.x + threadIdx.x;   // this lane's next queue entry
+    const uint64_t* K = nullptr;
+    int32_t *F = nullptr, *PP = nullptr, *T = nullptr;
+    uint32_t r = 0;
+    int32_t me = 0, i = 0, j = 0, lo = 0, sx = 0, max_f = 0, max_j = -1, n_skip = 0, pi = 0, qi = 0, psx = 0;
+    int32_t bf = INT_MIN, bi = -1;      // segment best
+    int32_t pf = 0, ppf = -1;           // f/pprev of anchor i-1 (forwarded to the first j of i)
+    uint32_t pairs = 0;
+    int32_t state = 0;                  // 0 idle, 1 advance st, 2 j-loop
+    for (;;) {
+        const bool idle = state == 0;
+        if (any(idle && kq < nm)) {
+            if (idle && kq < nm) {
+                const uint4 L = a.mseg[kq];
+                r = L.x;
+                const uint64_t base = a.a_off[r];
+                K = a.keys + base; F = a.f + base; PP = a.pp + base; T = a.tmark + base;
+                const int32_t ms = (int32_t)L.y;
+                me = (int32_t)L.z;
+                F[ms] = span; PP[ms] = -1; T[ms] = -1;
+                bf = span; bi = ms; pairs = 0;
+                const uint64_t k0 = K[ms], k1 = K[ms + 1];
+                psx = (int32_t)((k0 >> qb) & rmask);
+                pi = (int32_t)((k1 >> qb) & rmask); qi = (int32_t)(k1 & qmask);
+                pf = span; ppf = -1;
+                sx = ms; i = ms + 1; state = 1;
+                kq += stride;
+            }
+        }
+        if (!any(state != 0)) break;
+        if (state == 1) {
+            if (sx < i && pi > (int32_t)((uint32_t)psx + (uint32_t)maxdx)) {
+                ++sx;
+                psx = (int32_t)((K[sx] >> qb) & rmask);
+            } else {
+                lo = sx > i - P.max_iter ? sx : i - P.max_iter;
+                j = i - 1; max_f = span; max_j = -1; n_skip = 0; state = 2;
+            }
+        } else if (state == 2) {
+            if (j >= lo) {
+                uint64_t kk[MJ];
+                int32_t ff[MJ], pv[MJ], tt[MJ];
+#pragma unroll
+                for (int u = 0; u < MJ; ++u) {
+                    const int32_t jj = j - u;
+                    kk[u] = 0; ff[u] = 0; pv[u] = -1; tt[u] = -1;
+                    if (jj >= lo) {
+                        kk[u] = K[jj];
+                        if (jj == i - 1) { ff[u] = pf; pv[u] = ppf; }   // just finished: from registers
+                        else { ff[u] = F[jj]; pv[u] = PP[jj]; tt[u] = T[jj]; }
+                    }
+                }
+                bool brk = false;
+                int32_t done = 0;
+#pragma unroll
+                for (int u = 0; u < MJ; ++u) {
+                    const int32_t jj = j - u;
+                    if (!brk && jj >= lo) {
+                        ++done; ++pairs;
+                        const int32_t pj = (int32_t)((kk[u] >> qb) & rmask), qj = (int32_t)(kk[u] & qmask);
+                        const int32_t dq = qi - qj, dr = pi - pj;
+                        bool ok = dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
+                        const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                        ok = ok && dd <= bw;
+                        if (ok) {
+                            const int32_t dg = dr < dq ? dr : dq;
+                            const int32_t sv = (span < dg ? span : dg) - (int32_t)lut[dd] + ff[u];
+                            if (sv > max_f) { max_f = sv; max_j = jj; if (n_skip > 0) --n_skip; }
+                            else if (tt[u] == i) { ++n_skip; if (n_skip > P.max_skip) brk = true; }
+                            if (!brk && pv[u] >= 0) {
+                                T[pv[u]] = i;
+#pragma unroll
+                                for (int w = u + 1; w < MJ; ++w)
+                                    if (pv[u] == j - w) tt[w] = i;
+                            }
+                        }
+                    }
+                }
+                j = brk ? lo - 1 : j - done;
+            } else {
+                F[i] = max_f; PP[i] = max_j; T[i] = -1;
+                best_merge(bf, bi, max_f, i);
+                pf = max_f; ppf = max_j;
+                ++i;
+                if (i >= me) {
+                    atomicMax(a.rbest + r, best_key(bf, bi));
+                    atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)pairs);
+                    state = 0;
+                } else {
+                    const uint64_t ki = K[i];
+                    pi = (int32_t)((ki >> qb) & rmask); qi = (int32_t)(ki & qmask);
+                    state = 1;
+                }
             }
         }
     }
@@ -1343,13 +1472,15 @@ int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp
 static size_t chain_lds(int lut_n) {
     return (size_t)(((lut_n * 2) + 15) & ~15) + (size_t)DP_NW * (RING_WORDS * 4 + RK * 8 + RK * 8);
 }
-static size_t seg_lds(int lut_n) { return (size_t)(((lut_n * 2) + 15) & ~15); }
+static size_t lut_lds(int lut_n) { return (size_t)(((lut_n * 2) + 15) & ~15); }
+static size_t seg_lds(int lut_n) { return lut_lds(lut_n) + (size_t)DP_NW * (KRING * 8 + 3 * TQ * 5 + MEDB * 8); }
 int chain_max_blocks(int lut_n, int which) {
     int dev = 0, ncu = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    hipError_t e = which == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_seg, DP_NW * 64, seg_lds(lut_n))
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_long, DP_NW * 64, chain_lds(lut_n));
+    hipError_t e = which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_seg, DP_NW * 64, seg_lds(lut_n))
+                   : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_long, DP_NW * 64, chain_lds(lut_n))
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_med, 256, lut_lds(lut_n));
     if (e != hipSuccess) return 0;
     return ncu * (per > 0 ? per : 1);
 }
@@ -1359,9 +1490,11 @@ int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStr
     LAUNCH_CHECK();
     return 0;
 }
-int launch_chain(const ChainArgs& a, int seg_blocks, int long_blocks, hipStream_t st) {
+int launch_chain(const ChainArgs& a, int seg_blocks, int med_blocks, int long_blocks, hipStream_t st) {
     if (a.n == 0) return 0;
     hipLaunchKernelGGL(k_chain_seg, dim3(seg_blocks), dim3(DP_NW * 64), seg_lds(a.P.lut_n), st, a);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_chain_med, dim3(med_blocks), dim3(256), lut_lds(a.P.lut_n), st, a);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, (const uint32_t*)a.lseg_n, a.lseg_cap, (const uint4*)a.lseg, a.lseg_order);
     LAUNCH_CHECK();
