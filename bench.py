@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     p.add_argument("--stats", default="", help="write per-read chain statistics (npz) to this path")
+    p.add_argument("--streams", type=int, default=2,
+                   help="contexts (HIP streams) per GPU, each mapping a contiguous share of the step's reads "
+                        "from its own host thread against one shared device index")
     return p.parse_args()
 
 
@@ -106,27 +109,52 @@ def main():
     rnames = [f"r{i}" for i in range(args.reads)]
     n_bases = int(roffs[-1])
 
-    dev = M.Device(local)
+    S = max(1, args.streams)
+    devs = [M.Device(local) for _ in range(S)]
     t0 = time.time()
-    dev.upload_index(idx, mid)
+    devs[0].upload_index(idx, mid)
+    for d in devs[1:]:
+        d.share_index(devs[0], mid)
     t_up = time.time() - t0
+    # contiguous shares of the batch, one per context; reads resident in HBM before timing
+    cuts = [round(k * args.reads / S) for k in range(S + 1)]
+    shards = []
     t0 = time.time()
-    dev.set_reads_packed(rbuf, roffs)            # reads resident in HBM before the timed region
+    for k, d in enumerate(devs):
+        lo_r, hi_r = cuts[k], cuts[k + 1]
+        sub_offs = (roffs[lo_r:hi_r + 1] - roffs[lo_r]).astype(np.uint64)
+        d.set_reads_packed(rbuf[int(roffs[lo_r]):int(roffs[hi_r])], sub_offs)
+        nr = hi_r - lo_r
+        shards.append({
+            "dev": d, "n": nr,
+            "res": (L.ReadResult * max(nr, 1))(),
+            "names": (C.c_char_p * max(nr, 1))(*[x.encode() for x in rnames[lo_r:hi_r]]),
+            "cap": 256 * nr + (1 << 20),
+        })
+        shards[-1]["buf"] = C.create_string_buffer(shards[-1]["cap"])
+        shards[-1]["len"] = 0
     t_h2d = time.time() - t0
-    log(f"rank {rank}: index upload {t_up:.1f}s, reads H2D {t_h2d * 1e3:.1f} ms ({n_bases / 1e9:.3f} Gb)")
+    log(f"rank {rank}: index upload {t_up:.1f}s ({S} contexts share it), reads H2D {t_h2d * 1e3:.1f} ms ({n_bases / 1e9:.3f} Gb)")
 
     opts = M.map_opts()
-    res = (L.ReadResult * args.reads)()
-    nm_arr = (C.c_char_p * args.reads)(*[x.encode() for x in rnames])
-    paf_cap = 256 * args.reads + (1 << 20)
-    paf_buf = C.create_string_buffer(paf_cap)
-    h = dev._h
     ih = idx._h
 
-    def step() -> int:
+    def run_shard(sh):
+        h = sh["dev"]._h
         L.check(lib.mm2g_batch_map(h, C.byref(opts)), "batch_map")
-        L.check(lib.mm2g_batch_results(h, res, args.reads), "batch_results")
-        return L.check(lib.mm2g_format_paf(ih, res, nm_arr, args.reads, paf_buf, paf_cap), "format_paf")
+        L.check(lib.mm2g_batch_results(h, sh["res"], sh["n"]), "batch_results")
+        sh["len"] = L.check(lib.mm2g_format_paf(ih, sh["res"], sh["names"], sh["n"], sh["buf"], sh["cap"]), "format_paf")
+
+    import concurrent.futures as cf
+    pool = cf.ThreadPoolExecutor(max_workers=S) if S > 1 else None
+
+    def step() -> int:
+        if pool is None:
+            run_shard(shards[0])
+        else:
+            for f in [pool.submit(run_shard, sh) for sh in shards]:
+                f.result()
+        return sum(sh["len"] for sh in shards)
 
     for _ in range(args.warmup):
         step()
@@ -137,21 +165,29 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    dev.prof_enable(True)
-    dev.prof_reset()
+    for d in devs:
+        d.prof_enable(True)
+        d.prof_reset()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         paf_len = step()
     barrier()
     elapsed = time.perf_counter() - t0
-    prof = dev.prof()
-    dev.prof_enable(False)
-    cnt = dev.counters()                          # per batch (identical every step)
+    prof = {}
+    cnt = {}
+    for d in devs:
+        for k, (ms, calls) in d.prof().items():
+            a0, c0 = prof.get(k, (0.0, 0))
+            prof[k] = (a0 + ms, c0 + calls)
+        d.prof_enable(False)
+        for k, v in d.counters().items():        # per batch (identical every step)
+            cnt[k] = cnt.get(k, 0) + v
+    paf_all = b"".join(sh["buf"].raw[:sh["len"]] for sh in shards)
     if args.stats:
-        cs = dev.chain_stats()
-        na = np.array([res[i].n_anchors for i in range(args.reads)], dtype=np.int64)
-        fl = np.array([res[i].flags for i in range(args.reads)], dtype=np.int64)
+        cs = np.concatenate([d.chain_stats() for d in devs])
+        na = np.array([sh["res"][i].n_anchors for sh in shards for i in range(sh["n"])], dtype=np.int64)
+        fl = np.array([sh["res"][i].flags for sh in shards for i in range(sh["n"])], dtype=np.int64)
         np.savez(args.stats, chain=cs, n_anchors=na, flags=fl)
 
     if world > 1:
@@ -166,7 +202,7 @@ def main():
 
     value = total_bases / elapsed / 1e9
     ms_per_step = elapsed / max(args.steps, 1) * 1e3
-    n_lines = paf_buf.raw[:paf_len].count(b"\n") if paf_len else 0
+    n_lines = paf_all.count(b"\n")
 
     # ---- roofline of the dominant kernel (HIP events on the library stream) --
     # Algorithmic bytes per unit (DESIGN.md "Roofline accounting").
@@ -212,7 +248,7 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = cpu_baseline(args, names, lens, gbuf, rbuf, roffs, rnames, mid, thr, paf_buf.raw[:paf_len])
+        cpu, parity = cpu_baseline(args, names, lens, gbuf, rbuf, roffs, rnames, mid, thr, paf_all)
 
     if rank == 0:
         line = {
@@ -232,7 +268,7 @@ def main():
                 "workload": f"hg38-shaped {lens.sum() / 1e9:.2f} Gb reference index in HBM + "
                             f"{args.reads}x{args.read_len // 1000} kb ONT reads per GPU per step",
                 "reads_per_gpu_step": args.reads, "read_len": args.read_len, "ref_bases": int(lens.sum()),
-                "mid_occ": mid, "parallelism": f"reads sharded x{world} (index replicated)",
+                "mid_occ": mid, "parallelism": f"reads sharded x{world} (index replicated), {S} streams per GPU",
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -73,6 +73,10 @@ void mm2g_ctx_destroy(mm2g_ctx* ctx);
  * array (DESIGN.md "Index layout").  mid_occ as computed by the caller
  * (main.rs:196-197: max(calc_mid_occ(-f), 10)). */
 int mm2g_ctx_upload_index(mm2g_ctx* ctx, const mm2g_index* idx, int32_t mid_occ);
+/* Use the device index of `src` (same device) in `dst` without another copy:
+ * several contexts — one per host thread, each with its own stream and batch
+ * buffers — map concurrently against one index in HBM. */
+int mm2g_ctx_share_index(mm2g_ctx* dst, const mm2g_ctx* src, int32_t mid_occ);
 
 /* Mapping options: `mm2rs align` flags (src/main.rs:55-89) and the chain
  * parameters they drive (default_chain_params, src/main.rs:105-123). */

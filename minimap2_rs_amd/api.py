@@ -170,6 +170,11 @@ class Device:
         check(load().mm2g_ctx_upload_index(self._h, index._h, mid_occ), "upload_index")
         self.index = index
 
+    def share_index(self, other: "Device", mid_occ: int) -> None:
+        """Map against `other`'s device index (same GPU) without another copy."""
+        check(load().mm2g_ctx_share_index(self._h, other._h, mid_occ), "share_index")
+        self.index = other.index
+
     def set_reads(self, seqs: Sequence[bytes]) -> None:
         offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
         if seqs:

@@ -59,9 +59,10 @@ struct ProfSlot { std::string name; double ms = 0; int64_t calls = 0; };
 struct mm2g_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // index
+    // index (device copy shared by every context it was shared with, same device)
     const HostIndex* hidx = nullptr;
-    DevBuf tab, ix_pos;
+    struct DevIndex { DevBuf tab, ix_pos; };
+    std::shared_ptr<DevIndex> dix;
     uint32_t log2cap = 0;
     int32_t mid_occ = 10;
     bool have_index = false;
@@ -265,8 +266,9 @@ int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
     while ((1ULL << l2) < 2 * std::max<uint64_t>(nk, 1)) ++l2;     // load factor <= 0.5
     if (l2 > 31) return set_err(MM2G_E_UNSUP, "index too large for the device table");
     IxEntry* tab; uint64_t* dpos;
-    ENSURE(c->tab, IxEntry, (size_t)1 << l2, tab);
-    ENSURE(c->ix_pos, uint64_t, pos.size(), dpos);
+    c->dix = std::make_shared<mm2g_ctx::DevIndex>();    // a fresh copy (contexts sharing the old one keep it)
+    ENSURE(c->dix->tab, IxEntry, (size_t)1 << l2, tab);
+    ENSURE(c->dix->ix_pos, uint64_t, pos.size(), dpos);
     HIPCHK(hipMemsetAsync(tab, 0xff, sizeof(IxEntry) << l2, c->stream));
     if (!pos.empty()) HIPCHK(hipMemcpyAsync(dpos, pos.data(), pos.size() * 8, hipMemcpyHostToDevice, c->stream));
     DevBuf dk, doff, dn;
@@ -283,6 +285,18 @@ int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
     c->hidx = &H;
     c->mid_occ = mid_occ;
     c->have_index = true;
+    return 0;
+}
+
+int mm2g_ctx_share_index(mm2g_ctx* dst, const mm2g_ctx* src, int32_t mid_occ) {
+    if (!dst || !src) return set_err(MM2G_E_ARG, "null argument");
+    if (!src->have_index) return set_err(MM2G_E_STATE, "source context has no index");
+    if (dst->device != src->device) return set_err(MM2G_E_ARG, "contexts are on different devices");
+    dst->dix = src->dix;
+    dst->log2cap = src->log2cap;
+    dst->hidx = src->hidx;
+    dst->mid_occ = mid_occ;
+    dst->have_index = true;
     return 0;
 }
 
@@ -431,8 +445,8 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->mz_n, uint32_t, mcap, mz_n); ENSURE(c->mz_poff, uint32_t, mcap, mz_poff);
     ENSURE(c->a_cnt, uint32_t, n + 1, a_cnt); ENSURE(c->a_off, uint64_t, n + 1, a_off);
     SeedArgs sa{n, (const uint64_t*)c->rd_off.p, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, (const uint32_t*)c->mz_y.p, keep,
-                (const IxEntry*)c->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k,
-                0, c->ix_pos.cap / 8, mcap, out};
+                (const IxEntry*)c->dix->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->dix->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k,
+                0, c->dix->ix_pos.cap / 8, mcap, out};
     {
         ProfScope ps(c, "seed_count");
         LCHK(launch_seed_count(sa, grid_for(n), c->stream));
@@ -456,7 +470,8 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     // 4. anchor sort (seeds.rs:58)
     {
         ProfScope ps(c, "sort");
-        LCHK(launch_sort(n, a_off, keys, ktmp, c->keys.cap / 8, c->stream));
+        if (getenv("MM2G_OLD_SORT")) LCHK(launch_sort(n, a_off, keys, ktmp, c->keys.cap / 8, c->stream));
+        else LCHK(launch_sort_read(n, a_off, keys, ktmp, kl.qb, c->keys.cap / 8, c->stream));
     }
     // 5. chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
     build_lut(c, o->k, lut_need);

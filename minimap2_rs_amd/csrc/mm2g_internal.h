@@ -150,6 +150,8 @@ int launch_filter(const mm2g::FilterArgs& a, int n_blocks, hipStream_t st);
 int launch_seed_count(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st);
+// per-read MSD bucket sort on (group, rpos) + per-bucket full-key sort (qb = query bits of the key)
+int launch_sort_read(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb, uint64_t cap_keys, hipStream_t st);
 // MM2G_CHECKED builds: first recorded bounds violation {line, index, cap}; 0 = none
 int mm2g_checked_read(unsigned long long out[4], hipStream_t st);
 // chain DP of one pass: k_chain_seg, k_chain_med, k_lseg_order, k_chain_long, k_chain_fin

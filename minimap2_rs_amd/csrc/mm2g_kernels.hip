@@ -613,6 +613,124 @@ __global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t*
     }
 }
 
+// ---- per-read LSD radix sort on (group, rpos), then qpos for ties.
+// The query bits are left out of the radix passes (two fewer passes for
+// 10 kb reads); runs of equal (group, rpos) — rare — are ordered by qpos
+// afterwards, which gives exactly the (x, y) order of src/seeds.rs:58.
+// All digit histograms come from one read pass; a pass processes chunks of
+// RS_CH keys: per-wave digit counts -> per-(wave, digit) offsets -> stable
+// scatter (items in order, lanes ranked by ballot matching).
+constexpr int RS_ITEMS = 8;
+constexpr int RS_CH = 1024 * RS_ITEMS;
+constexpr int RS_MAXP = 8;   // digit passes (64 bits)
+
+__global__ __launch_bounds__(1024) void k_sort_read(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb,
+                                                    uint64_t cap_keys) {
+    __shared__ uint32_t hist[RS_MAXP][256];
+    __shared__ uint32_t wh[16][256];
+    __shared__ uint64_t red[32];
+    const uint32_t r = blockIdx.x;
+    if (r >= n) return;
+    const uint64_t base = a_off[r];
+    const uint32_t A = (uint32_t)(a_off[r + 1] - base);
+    if (A <= SORT_SMALL) return;     // k_sort_small
+#ifdef MM2G_CHECKED
+    if (base + A > cap_keys) { if (threadIdx.x == 0) CK(base + A, cap_keys); return; }
+#endif
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    uint64_t* src = keys + base;
+    uint64_t* dst = tmp + base;
+    // bits of (group, rpos) that vary, and all digit histograms in one pass
+    uint64_t vo = 0, va = U64MAX;
+    for (uint32_t i = tid; i < A; i += 1024) { const uint64_t h = src[i] >> qb; vo |= h; va &= h; }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { vo |= __shfl_xor(vo, d, 64); va &= __shfl_xor(va, d, 64); }
+    if (lane == 0) { red[wv] = vo; red[16 + wv] = va; }
+    for (int t = tid; t < RS_MAXP * 256; t += 1024) (&hist[0][0])[t] = 0;
+    __syncthreads();
+    vo = 0; va = U64MAX;
+    for (int t = 0; t < 16; ++t) { vo |= red[t]; va &= red[16 + t]; }
+    const uint64_t vary = vo ^ va;
+    const int top = vary ? 64 - clz64(vary) : 0;
+    const int npass = (top + 7) >> 3;
+    for (uint32_t i = tid; i < A; i += 1024) {
+        const uint64_t h = src[i] >> qb;
+        for (int k = 0; k < npass; ++k)
+            if ((vary >> (8 * k)) & 0xffULL) atomicAdd(&hist[k][(uint32_t)(h >> (8 * k)) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < npass) {
+        uint32_t run = 0;
+        for (int d = 0; d < 256; ++d) { const uint32_t c = hist[tid][d]; hist[tid][d] = run; run += c; }
+    }
+    __syncthreads();
+    bool in_tmp = false;
+    for (int k = 0; k < npass; ++k) {
+        if (((vary >> (8 * k)) & 0xffULL) == 0) continue;       // constant digit: order unchanged
+        const int sh = (int)qb + 8 * k;
+        for (uint32_t c0 = 0; c0 < A; c0 += RS_CH) {
+            const uint32_t w0 = c0 + (uint32_t)wv * 64 * RS_ITEMS;
+#pragma unroll
+            for (int t0 = 0; t0 < 256; t0 += 64) wh[wv][t0 + lane] = 0;
+            wave_lds_sync();
+            uint64_t x[RS_ITEMS];
+#pragma unroll
+            for (int it = 0; it < RS_ITEMS; ++it) {
+                const uint32_t i = w0 + (uint32_t)it * 64 + (uint32_t)lane;
+                x[it] = i < A ? src[i] : 0;
+                if (i < A) atomicAdd(&wh[wv][(uint32_t)(x[it] >> sh) & 255u], 1u);
+            }
+            __syncthreads();
+            if (tid < 256) {
+                uint32_t run = hist[k][tid];
+                for (int w = 0; w < 16; ++w) { const uint32_t c = wh[w][tid]; wh[w][tid] = run; run += c; }
+                hist[k][tid] = run;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < RS_ITEMS; ++it) {
+                const uint32_t i = w0 + (uint32_t)it * 64 + (uint32_t)lane;
+                const bool valid = i < A;
+                const uint32_t d = (uint32_t)(x[it] >> sh) & 255u;
+                uint64_t peers = ballot(valid);
+#pragma unroll
+                for (int bb = 0; bb < 8; ++bb) {
+                    const bool bit = (d >> bb) & 1u;
+                    const uint64_t mb = ballot(bit);
+                    peers &= bit ? mb : ~mb;
+                }
+                const uint64_t lt = peers & lanemask_lt();
+                const uint32_t pos = wh[wv][d] + (uint32_t)__popcll(lt);
+                if (valid) dst[CK(pos, A)] = x[it];
+                wave_lds_sync();
+                if (valid && lt == 0) wh[wv][d] += (uint32_t)__popcll(peers);
+                wave_lds_sync();
+            }
+            __syncthreads();
+        }
+        uint64_t* t = src; src = dst; dst = t;
+        in_tmp = !in_tmp;
+    }
+    // sorted by (group, rpos) in src; order runs of equal (group, rpos) by the full key
+    uint64_t* out = keys + base;
+    for (uint32_t i = tid; i < A; i += 1024) {
+        const uint64_t h = src[i] >> qb;
+        const bool start = (i == 0 || (src[i - 1] >> qb) != h) && (i + 1 < A && (src[i + 1] >> qb) == h);
+        if (start) {
+            uint32_t e = i + 1;
+            while (e < A && (src[e] >> qb) == h) ++e;
+            for (uint32_t u = i + 1; u < e; ++u) {      // insertion sort (runs are short)
+                const uint64_t v = src[u];
+                uint32_t w = u;
+                while (w > i && src[w - 1] > v) { src[w] = src[w - 1]; --w; }
+                src[w] = v;
+            }
+        }
+    }
+    __syncthreads();
+    if (in_tmp) for (uint32_t i = tid; i < A; i += 1024) out[i] = src[i];
+}
+
 // ============================================================================
 // 5. CHAIN DP — chain_dp_all (src/lchain.rs:59-91) + the fallback chain
 // (lchain.rs:162-173) + chain_qrange/trange (178-200) + the rescue test of
@@ -1458,6 +1576,14 @@ int launch_seed_count(const SeedArgs& a, int n_blocks, hipStream_t st) {
 }
 int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
     hipLaunchKernelGGL(k_seed_write, dim3(n_blocks), dim3(256), 0, st, a);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_sort_read(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb, uint64_t cap_keys, hipStream_t st) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_sort_small, dim3(n), dim3(256), 0, st, n, a_off, keys, cap_keys);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sort_read, dim3(n), dim3(1024), 0, st, n, a_off, keys, tmp, qb, cap_keys);
     LAUNCH_CHECK();
     return 0;
 }

@@ -219,3 +219,21 @@ def test_pipeline_parity_dense(dev, dense_world, tmp_path, mid_occ):
     assert dev.paf(rnames, res) == open(want_paf).read()
     # the DP pair counter behind bench.py's pairs/s equals the reference's inner-loop iterations
     assert dev.counters()["dp_pairs"] == counts["inner_iters"]
+
+
+def test_anchor_sort_many_shapes(dev, dense_world):
+    """Sorted anchors equal the oracle's for reads whose buckets take every
+    path of the per-read sort (single keys, <= 8, <= 64, <= 512, block radix)."""
+    ref, reads, rnames, rseqs = dense_world
+    oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+    idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+    rng = random.Random(9)
+    qs = list(rseqs) + [rseqs[0] * 3, rseqs[8] + rseqs[16], _rand_seq(rng, 20000)]
+    for mid_occ in (10, 100000):
+        dev.upload_index(idx, mid_occ)
+        dev.set_debug(True)
+        dev.set_reads(qs)
+        dev.map(M.map_opts())
+        for r, q in enumerate(qs):
+            want_a, _ = oi.anchors(q, 10, 15, mid_occ)
+            assert np.array_equal(dev.debug_anchors(r), want_a), (mid_occ, r, len(want_a))
