@@ -61,6 +61,30 @@ def parse():
     return p.parse_args()
 
 
+def share_cuts(n: int, s: int):
+    """Contiguous shares of n reads for s contexts: [cuts[k], cuts[k+1])."""
+    s = max(1, s)
+    return [round(k * n / s) for k in range(s + 1)]
+
+
+def rank_read_seed(read_seed: int, rank: int) -> int:
+    """Weak scaling: every rank maps its own reads (no data-path collective)."""
+    return read_seed + rank
+
+
+def reduce_step_time(dist, elapsed: float, n_bases: int, world: int, device):
+    """Max-over-ranks wall time and all ranks' bases (one all-reduce each,
+    outside the timed region)."""
+    if world <= 1:
+        return elapsed, float(n_bases)
+    import torch
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    bt = torch.tensor([float(n_bases)], dtype=torch.float64, device=device)
+    dist.all_reduce(bt, op=dist.ReduceOp.SUM)
+    return float(tt.item()), float(bt.item())
+
+
 def host_threads(world: int) -> int:
     n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     if n <= 0:
@@ -105,7 +129,7 @@ def main():
     log(f"rank {rank}: index built in {time.time() - t0:.1f}s, stats {idx.stats()}, mid_occ {mid}")
 
     # ---- reads (per rank: distinct seed) -----------------------------------
-    rbuf, roffs, _ = simdata.reads(gbuf, lens, args.reads, args.read_len, args.read_seed + rank)
+    rbuf, roffs, _ = simdata.reads(gbuf, lens, args.reads, args.read_len, rank_read_seed(args.read_seed, rank))
     rnames = [f"r{i}" for i in range(args.reads)]
     n_bases = int(roffs[-1])
 
@@ -117,7 +141,7 @@ def main():
         d.share_index(devs[0], mid)
     t_up = time.time() - t0
     # contiguous shares of the batch, one per context; reads resident in HBM before timing
-    cuts = [round(k * args.reads / S) for k in range(S + 1)]
+    cuts = share_cuts(args.reads, S)
     shards = []
     t0 = time.time()
     for k, d in enumerate(devs):
@@ -190,15 +214,8 @@ def main():
         fl = np.array([sh["res"][i].flags for sh in shards for i in range(sh["n"])], dtype=np.int64)
         np.savez(args.stats, chain=cs, n_anchors=na, flags=fl)
 
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        bt = torch.tensor([n_bases], dtype=torch.float64, device="cuda")
-        dist.all_reduce(bt, op=dist.ReduceOp.SUM)
-        total_bases = float(bt.item()) * args.steps
-    else:
-        total_bases = float(n_bases) * args.steps
+    elapsed, all_bases = reduce_step_time(dist, elapsed, n_bases, world, "cuda")
+    total_bases = all_bases * args.steps
 
     value = total_bases / elapsed / 1e9
     ms_per_step = elapsed / max(args.steps, 1) * 1e3

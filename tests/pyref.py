@@ -319,3 +319,104 @@ def fallback_chain(f, pprev, v):
         ch.append(i)
         i = pprev[i]
     return ch[::-1], v[best_i]
+
+
+# ---------------------------------------------------------------- align flow
+I32MAX = 2 ** 31 - 1
+
+
+def chain_qrange(anchors, chain):  # lchain.rs:178-188
+    qs, qe = I32MAX, -1
+    for i in chain:
+        s = qpos(anchors[i]) - (qspan(anchors[i]) - 1)
+        e = qpos(anchors[i]) + 1
+        qs = min(qs, s)
+        qe = max(qe, e)
+    return max(qs, 0), qe
+
+
+def rust_binary_search(xs, target):
+    """slice::binary_search as implemented in Rust >= 1.82 (base/size halving);
+    returns the index found or None (paf.rs:178)."""
+    size = len(xs)
+    if size == 0:
+        return None
+    base = 0
+    while size > 1:
+        half = size // 2
+        mid = base + half
+        base = base if xs[mid] > target else mid
+        size -= half
+    return base if xs[base] == target else None
+
+
+def paf_line(index, anchors, chain, qname, q, s1):  # paf.rs:130-236
+    a0 = anchors[chain[0]]
+    strand = "-" if rev(a0) else "+"
+    qs, qe, ts, te = I32MAX, -1, I32MAX, -1
+    for i in chain:
+        a = anchors[i]
+        qs = min(qs, qpos(a) - (qspan(a) - 1)); qe = max(qe, qpos(a) + 1)
+        ts = min(ts, rpos(a) - (qspan(a) - 1)); te = max(te, rpos(a) + 1)
+    qs, ts = max(qs, 0), max(ts, 0)
+    rid0 = (a0[0] >> 32) & 0x7FFFFFFF
+    if rid0 >= len(index.seq):
+        return None, True                     # idx.seq[rid] out of bounds: the reference panics
+    tname, tlen = index.seq[rid0]
+    mv = sketch_sequence(q, index.w, index.k, 0, False)
+    mini_pos = [i32((m[1] >> 1) & 0xFFFFFFFF) for m in mv]
+    sum_k = sum(m[0] & 0xFF for m in mv)
+    avg_k = f32(f32(sum_k) / f32(len(mv))) if mv else f32(index.k)
+    qlen = len(q)
+
+    def qfwd(a):
+        return (qlen - 1 - (qpos(a) + 1 - qspan(a))) if rev(a) else qpos(a)
+
+    cq = [qfwd(anchors[i]) for i in (reversed(chain) if strand == "-" else chain)]
+    dv = f32(0.0)
+    if mini_pos and cq:
+        st = rust_binary_search(mini_pos, cq[0])
+        if st is not None:
+            while st > 0 and mini_pos[st - 1] == cq[0]:
+                st -= 1
+            j, k, en, n_match = st, 1, st, 1
+            while j + 1 < len(mini_pos) and k < len(cq):
+                j += 1
+                if mini_pos[j] == cq[k]:
+                    n_match += 1; en = j; k += 1
+            n_tot = en - st + 1
+            rqs = qlen - qe if strand == "-" else qs
+            rqe = qlen - qs if strand == "-" else qe
+            ak = int(avg_k)                   # `avg_k as i32` (truncation)
+            if rqs > ak and ts > ak:
+                n_tot += 1
+            if qlen - rqe > ak and tlen - te > ak:
+                n_tot += 1
+            frac = f32(f32(n_match) / f32(n_tot))
+            dv = f32(0.0) if frac >= f32(1.0) else f32(f32(1.0) - np.power(frac, f32(f32(1.0) / max(avg_k, f32(1.0)))))
+    pqs, pqe = (qlen - qe, qlen - qs) if strand == "-" else (qs, qe)
+    line = (f"{qname}\t{qlen}\t{pqs}\t{pqe}\t{strand}\t{tname or '*'}\t{tlen}\t{ts}\t{te}\t{max(qe - qs, 0)}\t{max(te - ts, 0)}"
+            f"\t60\ttp:A:P\tcm:i:{len(chain)}\ts1:i:{max(s1, 0)}\ts2:i:0\tdv:f:{float(dv):.4f}\trl:i:0")
+    return line, False
+
+
+def align_one(index, qname, q, mid_occ, w=10, k=15):
+    """The Align flow of src/main.rs:189-230 for one read with default chain
+    parameters (main.rs:105-123): -> (PAF line or None, panics?, rescued?)."""
+    if len(q) == 0:
+        return None, False, False
+    mv = filter_query_minimizers(sketch_sequence(q, w, k, 0, False))
+    anchors = build_anchors_filtered(index, mv, len(q), mid_occ)
+    if not anchors:
+        return None, False, False
+    gap = f32(f32(0.01) * f32(0.8)) * f32(k)
+    f, pprev, v = chain_dp_all_dp(anchors, 5000, 5000, 500, 5000, gap, k, 25)
+    chain, score = fallback_chain(f, pprev, v)
+    qs, qe = chain_qrange(anchors, chain)
+    cov = max(qe - qs, 0)
+    rescued = max(len(q) - cov, 0) > 1000 or f32(cov) < f32(len(q)) * (f32(1.0) - f32(0.1))
+    if rescued:   # rescue_long_join: bw = bw_long -> max_dist_x = max_dist_y = 20000 (lchain.rs:63-66)
+        f, pprev, v = chain_dp_all_dp(anchors, 5000, 5000, 20000, 5000, gap, k, 25)
+        chain, score = fallback_chain(f, pprev, v)
+    line, panic = paf_line(index, anchors, chain, qname, q, score)
+    return line, panic, rescued

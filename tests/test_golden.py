@@ -1,0 +1,133 @@
+"""CPU: the C++ oracle (and the product's host-side index) against the golden
+fixtures written by tests/golden/make_golden.py from the independent
+pure-Python restatement tests/pyref.py.
+
+The reference has no tests of its own and cannot be built here (SURVEY.md
+§8c), so these fixtures are the pin: two separately written readings of the
+Rust sources must agree bit for bit before the oracle is trusted as the GPU
+checker.  PAF lines of reads whose chain lies on an odd rid are absent: the
+reference panics there."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import minimap2_rs_amd as M
+from oracle import oracle as O
+
+import pyref as R
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def sf():
+    with open(os.path.join(GOLD, "sketch_filter.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="module")
+def world(tmp_path_factory):
+    with open(os.path.join(GOLD, "world.json")) as fh:
+        w = json.load(fh)
+    td = tmp_path_factory.mktemp("gold")
+    ref = str(td / "ref.fa")
+    with open(ref, "w") as fh:
+        for n, s in w["contigs"]:
+            fh.write(f">{n}\n{s}\n")
+    reads = str(td / "reads.fa")
+    with open(reads, "w") as fh:
+        for r in w["reads"]:
+            fh.write(f">{r['name']}\n{r['seq']}\n")
+    w["ref_path"], w["reads_path"] = ref, reads
+    return w
+
+
+def test_oracle_sketch(sf):
+    for c in sf["sketch"]:
+        got = O.sketch(c["seq"].encode(), c["w"], c["k"], c["rid"], c["hpc"])
+        want = np.array(c["out"], dtype=np.uint64).reshape(-1, 2)
+        assert np.array_equal(got.reshape(-1, 2), want), (c["w"], c["k"], c["hpc"], len(c["seq"]))
+
+
+def test_oracle_filter(sf):
+    for c in sf["filter"]:
+        got = O.filter_minimizers(np.array(c["mv"], dtype=np.uint64).reshape(-1, 2))
+        assert np.array_equal(got.reshape(-1, 2), np.array(c["out"], dtype=np.uint64).reshape(-1, 2))
+
+
+def test_pyref_reproduces_fixtures(sf):
+    """Guards the generator against drift (a subset: pure Python is slow)."""
+    for c in sf["sketch"][::7]:
+        assert [list(x) for x in R.sketch_sequence(c["seq"].encode(), c["w"], c["k"], c["rid"], c["hpc"])] == c["out"]
+
+
+def test_oracle_index(world):
+    oi = O.OIndex.build(world["ref_path"], world["w"], world["k"], world["b"], 0, 2)
+    for fr, want in world["calc_mid_occ"].items():
+        assert oi.mid_occ(float(fr)) == want, fr
+    assert oi.stats()[0] == world["n_keys"]
+    for g in world["gets"]:
+        got = oi.get(g["key"])
+        if g["kind"] == 0:
+            assert got is None
+        elif g["kind"] == 1:
+            assert got == ("Single", g["pos"][0])
+        else:
+            assert got == ("Multi", g["pos"])
+
+
+def test_oracle_anchors_dp_paf(world, tmp_path):
+    oi = O.OIndex.build(world["ref_path"], world["w"], world["k"], world["b"], 0, 2)
+    mid = world["mid_occ"]
+    for r in world["reads"]:
+        a, _ = oi.anchors(r["seq"].encode(), world["w"], world["k"], mid)
+        assert np.array_equal(a.reshape(-1, 2), np.array(r["anchors"], dtype=np.uint64).reshape(-1, 2)), r["name"]
+        if not r["anchors"]:
+            continue
+        f, pp, chain, score, _ = O.chain_dp(a, world["k"])
+        assert f.tolist() == r["f"] and pp.tolist() == r["pprev"], r["name"]
+        assert chain.tolist() == r["chain"] and score == r["score"], r["name"]
+    out = str(tmp_path / "o.paf")
+    _, counts, _ = oi.align_fasta(world["reads_path"], out, mid_occ=mid)
+    want = [r["paf"] for r in world["reads"] if r["paf"]]
+    assert open(out).read().splitlines() == want
+    assert counts["panics"] == sum(r["panic"] for r in world["reads"])
+    assert counts["rescued_anchors"] == sum(len(r["anchors"]) for r in world["reads"] if r["rescued"])
+
+
+def test_host_index_matches_oracle(world, tmp_path):
+    """The product's host index (libmm2g.so host code; no GPU needed) against
+    the oracle: stats, calc_mid_occ, Index::get and byte-identical .mmi."""
+    idx = M.Index.build_index_from_fasta(world["ref_path"], world["w"], world["k"], world["b"], 0, 2)
+    oi = O.OIndex.build(world["ref_path"], world["w"], world["k"], world["b"], 0, 2)
+    assert idx.stats()[0] == world["n_keys"]
+    assert tuple(idx.stats()) == tuple(oi.stats())
+    for fr, want in world["calc_mid_occ"].items():
+        assert idx.calc_mid_occ(float(fr)) == want
+    for g in world["gets"]:
+        got = idx.get(g["key"])
+        exp = None if g["kind"] == 0 else (("Single", g["pos"][0]) if g["kind"] == 1 else ("Multi", g["pos"]))
+        assert got == exp
+    p1, p2 = str(tmp_path / "p.mmi"), str(tmp_path / "o.mmi")
+    idx.save_to_mmi(p1)
+    oi.save_mmi(p2)
+    assert open(p1, "rb").read() == open(p2, "rb").read()
+    back = M.Index.load_from_mmi(p1)
+    assert tuple(back.stats()) == tuple(idx.stats())
+    assert back.params == idx.params
+    for g in world["gets"][:50]:
+        assert back.get(g["key"]) == idx.get(g["key"])
+
+
+@pytest.mark.parametrize("w,k,flag", [(10, 15, 0), (5, 11, 1), (19, 19, 0)])
+def test_host_index_params(world, tmp_path, w, k, flag):
+    """HPC and other (w, k): product host index == oracle, byte for byte."""
+    idx = M.Index.build_index_from_fasta(world["ref_path"], w, k, 12, flag, 3)
+    oi = O.OIndex.build(world["ref_path"], w, k, 12, flag, 3)
+    p1, p2 = str(tmp_path / "p.mmi"), str(tmp_path / "o.mmi")
+    idx.save_to_mmi(p1)
+    oi.save_mmi(p2)
+    assert open(p1, "rb").read() == open(p2, "rb").read()
+    assert idx.calc_mid_occ(2e-4) == oi.mid_occ(2e-4)

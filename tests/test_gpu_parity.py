@@ -237,3 +237,41 @@ def test_anchor_sort_many_shapes(dev, dense_world):
         for r, q in enumerate(qs):
             want_a, _ = oi.anchors(q, 10, 15, mid_occ)
             assert np.array_equal(dev.debug_anchors(r), want_a), (mid_occ, r, len(want_a))
+
+
+def test_golden_world_gpu(dev, tmp_path):
+    """The committed fixtures (pure-Python restatement, tests/golden) on the GPU:
+    anchors, DP arrays and PAF lines."""
+    import json
+    gold = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "world.json")))
+    ref = str(tmp_path / "ref.fa")
+    simdata.write_fasta(ref, [c[0] for c in gold["contigs"]], [c[1].encode() for c in gold["contigs"]])
+    idx = M.Index.build_index_from_fasta(ref, gold["w"], gold["k"], gold["b"], 0, 2)
+    dev.upload_index(idx, gold["mid_occ"])
+    dev.set_debug(True)
+    seqs = [r["seq"].encode() for r in gold["reads"]]
+    dev.set_reads(seqs)
+    res = dev.map(M.map_opts())
+    for i, r in enumerate(gold["reads"]):
+        assert dev.debug_anchors(i).reshape(-1).tolist() == [v for xy in r["anchors"] for v in xy], r["name"]
+        if r["anchors"] and not r["rescued"]:
+            f, pp = dev.debug_dp(i)
+            assert f.tolist() == r["f"] and pp.tolist() == r["pprev"], r["name"]
+        assert bool(res[i].flags & 8) == r["panic"], r["name"]
+        assert bool(res[i].flags & 2) == r["rescued"], r["name"]
+    got = dev.paf([r["name"] for r in gold["reads"]], res).splitlines()
+    assert got == [r["paf"] for r in gold["reads"] if r["paf"]]
+
+
+def test_cli_align_gpu(small_world, tmp_path):
+    """`mm2rs align` (GPU) prints the oracle CLI's lines for every read."""
+    import subprocess
+    ref, reads, rnames, rseqs = small_world
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mm2rs = os.path.join(root, "minimap2_rs_amd", "build", "mm2rs")
+    cpu = os.path.join(root, "oracle", "build", "mm2rs-cpu")
+    mmi = str(tmp_path / "ref.mmi")
+    subprocess.run([mm2rs, "index", ref, "-d", mmi], check=True, capture_output=True)
+    g = subprocess.run([mm2rs, "align", mmi, reads], check=True, capture_output=True, text=True).stdout
+    c = subprocess.run([cpu, "align", ref, reads], check=True, capture_output=True, text=True).stdout
+    assert g == c and g.count("\n") > 50
