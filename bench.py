@@ -85,6 +85,23 @@ def reduce_step_time(dist, elapsed: float, n_bases: int, world: int, device):
     return float(tt.item()), float(bt.item())
 
 
+SORT_SMALL = 4096   # reads up to this many anchors are sorted by k_sort_small (mm2g_kernels.hip)
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    passes (profiles/pmc_traffic.json, written by tools/pmc_traffic.py:
+    2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md §HBM), or None when no PMC profile of it exists."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+        return t["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def host_threads(world: int) -> int:
     n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     if n <= 0:
@@ -222,38 +239,37 @@ def main():
     n_lines = paf_all.count(b"\n")
 
     # ---- roofline of the dominant kernel (HIP events on the library stream) --
-    # Algorithmic bytes per unit (DESIGN.md "Roofline accounting").
+    # Algorithmic bytes per launch (DESIGN.md "Roofline accounting").
     A, Ar, m, mk = cnt["anchors"], cnt["rescued_anchors"], cnt["minimizers"], cnt["kept_minimizers"]
     L_tot = cnt["bases"]
-    kernel_bytes = {
-        "sketch": L_tot + 12 * m,                       # ASCII in; (x 8 B, y 4 B) per minimizer out
-        "filter": 9 * m,                                # x in, keep out
-        "seed_count": 9 * m + 16 * mk + 8 * m,          # keep+x in, 16 B table entry per kept, (n, poff) out
-        "seed_write": 12 * m + 16 * A,                  # (n, poff, y) in; 8 B position in + 8 B key out per anchor
-        "sort": 16 * A,                                 # each 8 B key read once and written once
-        "chain_dp": 24 * A,                             # 16 B anchor in + 8 B f/pprev out per anchor
-        "chain_dp_rescue": 24 * Ar,
+    na = np.array([sh["res"][i].n_anchors for sh in shards for i in range(sh["n"])], dtype=np.int64)
+    A_large = int(na[na > SORT_SMALL].sum())
+    A_small = int(na[(na > 1) & (na <= SORT_SMALL)].sum())
+    kernel_bytes = {   # slot -> (kernel symbol, algorithmic bytes per step)
+        "sketch": ("k_sketch", L_tot + 12 * m),              # ASCII in; (x 8 B, y 4 B) per minimizer out
+        "filter": ("k_filter", 9 * m),                       # x in, keep flag out
+        "seed_count": ("k_seed_count", 9 * m + 16 * mk + 8 * m),   # keep+x in, 16 B table entry per kept, (n, poff) out
+        "seed_write": ("k_seed_write", 12 * m + 16 * A),     # (n, poff, y) in; 8 B position in + 8 B key out per anchor
+        "sort_small": ("k_sort_small", 16 * A_small),        # each 8 B key read once and written once
+        "sort_large": ("k_sort_read", 16 * A_large),
+        "chain_seg": ("k_chain_seg", 8 * A),                 # every key read once (segmenting)
+        "dv": ("k_dv", 0),
     }
     per_kernel = {}
     for name, (ms, calls) in prof.items():
-        if calls <= 0:
-            continue
-        per_kernel[name] = {"ms_per_step": ms / args.steps, "launches_per_step": calls / args.steps}
-    # k_chain_dp = both DP passes (one kernel symbol, as rocprofv3 sees it)
-    chain_ms = prof.get("chain_dp", (0.0, 0))[0] + prof.get("chain_dp_rescue", (0.0, 0))[0]
-    chain_calls = prof.get("chain_dp", (0.0, 0))[1] + prof.get("chain_dp_rescue", (0.0, 0))[1]
-    groups = {"k_chain_dp": (chain_ms, chain_calls, (kernel_bytes["chain_dp"] + kernel_bytes["chain_dp_rescue"]) * args.steps)}
-    for nm in ("sketch", "filter", "seed_count", "seed_write", "sort"):
-        ms, calls = prof.get(nm, (0.0, 0))
-        groups[nm] = (ms, calls, kernel_bytes[nm] * args.steps)
-    dom = max(groups, key=lambda g: groups[g][0])
-    d_ms, d_calls, d_bytes = groups[dom]
+        if calls > 0:
+            per_kernel[name] = {"ms_per_step": ms / args.steps, "launches_per_step": calls / args.steps}
+    cand = {k: v for k, v in prof.items() if k in kernel_bytes and kernel_bytes[k][1] > 0 and v[1] > 0}
+    dom = max(cand, key=lambda k: cand[k][0])
+    d_ms, d_calls = cand[dom]
+    d_sym, d_bytes = kernel_bytes[dom]
     avg_s = d_ms / 1e3 / max(d_calls, 1)
-    bytes_per_launch = d_bytes / max(d_calls, 1)
+    bytes_per_launch = d_bytes * args.steps / max(d_calls, 1)
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    traffic = pmc_traffic(d_sym)
     roofline = {
-        "bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+        "bound": "hbm", "kernel": d_sym, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
         "avg_launch_ms": round(avg_s * 1e3, 4), "alg_bytes_per_launch": int(bytes_per_launch),
     }
     # whole-path algorithmic bytes (SURVEY.md §8d B(read) summed) over the step time

@@ -469,9 +469,12 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     }
     // 4. anchor sort (seeds.rs:58)
     {
-        ProfScope ps(c, "sort");
-        if (getenv("MM2G_OLD_SORT")) LCHK(launch_sort(n, a_off, keys, ktmp, c->keys.cap / 8, c->stream));
-        else LCHK(launch_sort_read(n, a_off, keys, ktmp, kl.qb, c->keys.cap / 8, c->stream));
+        ProfScope ps(c, "sort_small");
+        LCHK(launch_sort_read(0, n, a_off, keys, ktmp, kl.qb, c->keys.cap / 8, c->stream));
+    }
+    {
+        ProfScope ps(c, "sort_large");
+        LCHK(launch_sort_read(1, n, a_off, keys, ktmp, kl.qb, c->keys.cap / 8, c->stream));
     }
     // 5. chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
     build_lut(c, o->k, lut_need);
@@ -513,8 +516,13 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         sb = std::max(1, std::min((int)((n + 3) / 4), sb));
         HIPCHK(hipMemsetAsync(rbest, 0, (size_t)n * 8, c->stream));
         HIPCHK(hipMemsetAsync(lseg_n, 0, 16, c->stream));   // long count (pass 0/1 slot), medium count, medium taken
-        ProfScope ps(c, pass == 0 ? "chain_dp" : "chain_dp_rescue");
-        LCHK(launch_chain(ca, sb, mb, lb, c->stream));
+        static const char* names[2][5] = {{"chain_seg", "chain_med", "chain_lorder", "chain_long", "chain_fin"},
+                                          {"chain_seg_rescue", "chain_med_rescue", "chain_lorder_rescue", "chain_long_rescue", "chain_fin_rescue"}};
+        const int blocks[5] = {sb, mb, 1, lb, 0};
+        for (int stg = 0; stg < 5; ++stg) {
+            ProfScope ps(c, names[pass][stg]);
+            LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));
+        }
     }
     // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
     const bool sep = (H.w != o->w || H.k != o->k);

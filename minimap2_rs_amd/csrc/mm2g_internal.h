@@ -151,11 +151,11 @@ int launch_seed_count(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st);
 // per-read MSD bucket sort on (group, rpos) + per-bucket full-key sort (qb = query bits of the key)
-int launch_sort_read(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb, uint64_t cap_keys, hipStream_t st);
+int launch_sort_read(int stage, uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb, uint64_t cap_keys, hipStream_t st);   // 0 small reads, 1 large
 // MM2G_CHECKED builds: first recorded bounds violation {line, index, cap}; 0 = none
 int mm2g_checked_read(unsigned long long out[4], hipStream_t st);
-// chain DP of one pass: k_chain_seg, k_chain_med, k_lseg_order, k_chain_long, k_chain_fin
-int launch_chain(const mm2g::ChainArgs& a, int seg_blocks, int med_blocks, int long_blocks, hipStream_t st);
+// chain DP of one pass, stage 0..4: k_chain_seg, k_chain_med, k_lseg_order, k_chain_long, k_chain_fin
+int launch_chain_stage(int stage, const mm2g::ChainArgs& a, int blocks, hipStream_t st);
 int chain_max_blocks(int lut_n, int which);   // co-resident workgroups (0 = k_chain_seg, 1 = k_chain_long, 2 = k_chain_med)
 int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStream_t st);
 int launch_dv(const mm2g::DvArgs& a, hipStream_t st);

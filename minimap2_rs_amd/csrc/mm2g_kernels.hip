@@ -1579,11 +1579,10 @@ int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
     LAUNCH_CHECK();
     return 0;
 }
-int launch_sort_read(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb, uint64_t cap_keys, hipStream_t st) {
+int launch_sort_read(int stage, uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb, uint64_t cap_keys, hipStream_t st) {
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_sort_small, dim3(n), dim3(256), 0, st, n, a_off, keys, cap_keys);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_sort_read, dim3(n), dim3(1024), 0, st, n, a_off, keys, tmp, qb, cap_keys);
+    if (stage == 0) hipLaunchKernelGGL(k_sort_small, dim3(n), dim3(256), 0, st, n, a_off, keys, cap_keys);
+    else hipLaunchKernelGGL(k_sort_read, dim3(n), dim3(1024), 0, st, n, a_off, keys, tmp, qb, cap_keys);
     LAUNCH_CHECK();
     return 0;
 }
@@ -1616,17 +1615,15 @@ int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStr
     LAUNCH_CHECK();
     return 0;
 }
-int launch_chain(const ChainArgs& a, int seg_blocks, int med_blocks, int long_blocks, hipStream_t st) {
+int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st) {
     if (a.n == 0) return 0;
-    hipLaunchKernelGGL(k_chain_seg, dim3(seg_blocks), dim3(DP_NW * 64), seg_lds(a.P.lut_n), st, a);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_chain_med, dim3(med_blocks), dim3(256), lut_lds(a.P.lut_n), st, a);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, (const uint32_t*)a.lseg_n, a.lseg_cap, (const uint4*)a.lseg, a.lseg_order);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_chain_long, dim3(long_blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
+    switch (stage) {
+    case 0: hipLaunchKernelGGL(k_chain_seg, dim3(blocks), dim3(DP_NW * 64), seg_lds(a.P.lut_n), st, a); break;
+    case 1: hipLaunchKernelGGL(k_chain_med, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
+    case 2: hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, (const uint32_t*)a.lseg_n, a.lseg_cap, (const uint4*)a.lseg, a.lseg_order); break;
+    case 3: hipLaunchKernelGGL(k_chain_long, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a); break;
+    default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 255) / 256), dim3(256), 0, st, a); break;
+    }
     LAUNCH_CHECK();
     return 0;
 }
