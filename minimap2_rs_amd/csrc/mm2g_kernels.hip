@@ -145,8 +145,16 @@ DEVI uint64_t uni64(uint64_t v) {
 //     ties, B: new minimum, C: expiry + rescan + ties) in position order.
 //   * emissions are counted, wave-scanned and written in reference order.
 // ============================================================================
-constexpr int SK_CH = 16;
+constexpr int SK_CH = 8;
 constexpr int SK_TS = 64 * SK_CH;
+constexpr int SK_HALO = 32;                         // bases before the tile (>= k-1)
+
+// per-wave LDS: X[NB] (x = hash<<8 | span, MAX = no info), LZ[NB] (l | z<<15),
+// B[SK_HALO + SK_TS] (the tile's bases); y = pos<<1 | z is implicit
+__host__ __device__ inline size_t sketch_wave_lds(int w) {
+    const size_t nb = (size_t)SK_TS + (size_t)w;
+    return ((nb * 8 + nb * 2 + SK_HALO + SK_TS) + 15) & ~(size_t)15;
+}
 
 template <bool K32>
 __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
@@ -154,10 +162,9 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
     const int w = a.w, k = a.k;
     const int NB = SK_TS + w;                        // history (w) + tile
     const int wv = wave_id(), lane = lane_id();
-    const size_t per_wave = (((size_t)NB * 14) + 15) & ~(size_t)15;
-    uint64_t* X = (uint64_t*)(smem + per_wave * wv);
-    uint32_t* Y = (uint32_t*)(X + NB);
-    uint16_t* Lc = (uint16_t*)(Y + NB);
+    uint64_t* X = (uint64_t*)(smem + sketch_wave_lds(w) * wv);
+    uint16_t* LZ = (uint16_t*)(X + NB);
+    uint8_t* Bs = (uint8_t*)(LZ + NB);
     const int CAP = w + k;
     const uint64_t mask = (k >= 32) ? U64MAX : ((1ULL << (2 * k)) - 1);
     const uint32_t shift1 = 2u * (uint32_t)(k - 1);
@@ -171,44 +178,60 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
         // history slots = positions [-w, -1]: MAX
         for (int t0 = 0; t0 < w; t0 += 64) {
             const int t = t0 + lane;
-            if (t < w) { X[t] = U64MAX; Y[t] = 0xffffffffu; Lc[t] = 0; }
+            if (t < w) { X[t] = U64MAX; LZ[t] = 0; }
         }
-        wave_lds_sync();
         uint64_t count = 0;
         int32_t l_carry = 0;
         for (int64_t t0 = 0; t0 < L; t0 += SK_TS) {
             const int64_t hbase = t0 - w;            // LDS index = p - hbase
+            const int64_t bbase = t0 - SK_HALO;      // Bs index = p - bbase
+            // ---- stage the tile's bases (+ halo) in LDS: coalesced byte loads
+            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < (SK_HALO + SK_TS + 63) / 64; ++j) {
+                const int bi = j * 64 + lane;
+                const int64_t p = bbase + bi;
+                if (bi < SK_HALO + SK_TS) Bs[bi] = (p >= 0 && p < L) ? s[p] : (uint8_t)'N';
+            }
+            wave_lds_sync();
             const int64_t ps = t0 + (int64_t)lane * SK_CH;
             const int64_t pe = ps + SK_CH < L ? ps + SK_CH : L;
-            // ---- phase 1a: k-mers and per-position flags
-            // warm-up: the last k-1 ACGT bases before ps (the k-mer registers
-            // skip ambiguous bases, src/sketch.rs:75-76,86-88)
+            // ---- phase 1a: k-mers and per-position flags.  Warm-up: the k-mer
+            // registers hold the last k-1 ACGT bases before ps (ambiguous bases
+            // are skipped, src/sketch.rs:75-76,86-88; from the initial zeros at
+            // the read start) -- exactly, since the symmetric-k-mer test that
+            // gates l sees them.  Bytes come from the LDS tile + halo, from HBM
+            // only past the halo (long ambiguous runs).
             uint64_t kf = 0, kr = 0;
-            int64_t wsp = ps;
-            int need = ps < pe ? k - 1 : 0;
-            while (any(need > 0 && wsp > 0)) {
-                if (need > 0 && wsp > 0) { --wsp; if (nt4d(s[wsp]) < 4) --need; }
-            }
-            int64_t pw = wsp;
-            while (any(pw < ps)) {
-                if (pw < ps) {
-                    const uint32_t c = nt4d(s[pw]);
-                    if (c < 4) { kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1); }
-                    ++pw;
+            {
+                auto base_at = [&](int64_t p) -> uint32_t { return p >= bbase ? nt4d(Bs[(int)(p - bbase)]) : nt4d(s[p]); };
+                int64_t wsp = ps;
+                int need = ps < pe ? k - 1 : 0;
+                while (any(need > 0 && wsp > 0)) {
+                    if (need > 0 && wsp > 0) { --wsp; if (base_at(wsp) < 4) --need; }
+                }
+                int64_t pw = wsp;
+                while (any(pw < ps)) {
+                    if (pw < ps) {
+                        const uint32_t c = base_at(pw);
+                        if (c < 4) { kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1); }
+                        ++pw;
+                    }
                 }
             }
             bool rs = false; int32_t lc = 0;
+#pragma unroll
             for (int t = 0; t < SK_CH; ++t) {
                 const int64_t p = ps + t;
                 if (p < pe) {
                     const int ix = (int)(p - hbase);
-                    const uint32_t c = nt4d(s[p]);
-                    uint64_t x = U64MAX; uint32_t z = 0; uint16_t fl = 0;
+                    const uint32_t c = nt4d(Bs[(int)(p - bbase)]);
+                    uint64_t x = U64MAX; uint16_t fl = 0, z = 0;
                     if (c < 4) {
                         kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1);
                         fl = 1;
                         if (kf != kr) {
-                            z = kf < kr ? 0u : 1u;
+                            z = kf < kr ? 0 : 1;
                             const uint64_t km = z ? kr : kf;
                             uint64_t h;
                             if (K32) h = hash64d<uint32_t>((uint32_t)km, (uint32_t)mask);
@@ -217,7 +240,7 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                             fl = 2;
                         }
                     }
-                    X[ix] = x; Y[ix] = ((uint32_t)p << 1) | z; Lc[ix] = fl;
+                    X[ix] = x; LZ[ix] = (uint16_t)(fl | (z << 15));
                     if (fl == 0) { rs = true; lc = 0; } else if (fl == 2) { lc = lc + 1 < CAP ? lc + 1 : CAP; }
                 }
             }
@@ -237,13 +260,15 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
             wave_lds_sync();
             // ---- phase 1b: l per position; invalidate info where l < k
             int32_t lv = lin;
+#pragma unroll
             for (int t = 0; t < SK_CH; ++t) {
                 const int64_t p = ps + t;
                 if (p < pe) {
                     const int ix = (int)(p - hbase);
-                    const uint16_t fl = Lc[ix];
+                    const uint16_t v = LZ[ix];
+                    const uint16_t fl = v & 3u;
                     if (fl == 0) lv = 0; else if (fl == 2) lv = lv + 1 < CAP ? lv + 1 : CAP;
-                    Lc[ix] = (uint16_t)lv;
+                    LZ[ix] = (uint16_t)((v & 0x8000u) | (uint16_t)lv);
                     if (!(fl == 2 && lv >= k)) X[ix] = U64MAX;
                 }
             }
@@ -253,6 +278,7 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                 l_carry = rdl(lv, owner);
             }
             wave_lds_sync();
+#define SK_Y(q) ((((uint32_t)(hbase + (q))) << 1) | (uint32_t)(LZ[(q)] >> 15))
             // ---- phase 2: reference step logic, count then write
             uint32_t myoff = 0, tot = 0;
             for (int pass = 0; pass < 2; ++pass) {
@@ -265,22 +291,22 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                     const int64_t p = ps - w + d;
                     const int q = (int)(p - hbase);
                     const uint64_t x = X[q];
-                    if (mx >= x) { mx = x; my = Y[q]; mp = p; }
+                    if (mx >= x) { mx = x; my = SK_Y(q); mp = p; }
                 }
                 for (int t = 0; t < SK_CH; ++t) {
                     const int64_t i = ps + t;
                     const bool act = i < pe;
                     const int ii = (int)(i - hbase);
                     const uint64_t ix_x = act ? X[ii] : U64MAX;
-                    const uint32_t ix_y = act ? Y[ii] : 0xffffffffu;
-                    const int32_t l = act ? (int32_t)Lc[ii] : 0;
+                    const uint32_t ix_y = act ? SK_Y(ii) : 0xffffffffu;
+                    const int32_t l = act ? (int32_t)(LZ[ii] & 0x7fffu) : 0;
                     // A: first window (sketch.rs:90-93)
                     const bool doA = act && l == w + k - 1 && mx != U64MAX;
                     if (any(doA)) {
                         for (int d = 1; d < w; ++d) {
                             const int q = ii - w + d;
-                            if (doA && X[q] == mx && Y[q] != my) {
-                                if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = Y[q]; }
+                            if (doA && X[q] == mx && SK_Y(q) != my) {
+                                if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = SK_Y(q); }
                                 ++o; ++n_em;
                             }
                         }
@@ -299,15 +325,15 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                         for (int d = 1; d <= w; ++d) {
                             const int q = ii - w + d;
                             const uint64_t x = X[q];
-                            if (nx >= x) { nx = x; ny = Y[q]; np = i - w + d; }
+                            if (nx >= x) { nx = x; ny = SK_Y(q); np = i - w + d; }
                         }
                         if (doC) { mx = nx; my = ny; mp = np; }
                         const bool doT = doC && l >= w + k - 1 && mx != U64MAX;
                         if (any(doT)) {
                             for (int d = 1; d <= w; ++d) {
                                 const int q = ii - w + d;
-                                if (doT && mx == X[q] && my != Y[q]) {
-                                    if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = Y[q]; }
+                                if (doT && mx == X[q] && my != SK_Y(q)) {
+                                    if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = SK_Y(q); }
                                     ++o; ++n_em;
                                 }
                             }
@@ -320,10 +346,10 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
             // ---- move the last w slots to the history area
             wave_lds_sync();
             if (t0 + SK_TS < L) {
-                // source [TS, TS+w) and destination [0, w) never overlap (w < 256 < TS)
+                // source [TS, TS+w) and destination [0, w) never overlap (w < 256 <= TS)
                 for (int b0 = 0; b0 < w; b0 += 64) {
                     const int t = b0 + lane;
-                    if (t < w) { X[t] = X[SK_TS + t]; Y[t] = Y[SK_TS + t]; Lc[t] = Lc[SK_TS + t]; }
+                    if (t < w) { X[t] = X[SK_TS + t]; LZ[t] = LZ[SK_TS + t]; }
                 }
             }
             wave_lds_sync();
@@ -336,7 +362,7 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
             for (int d = 0; d < w; ++d) {
                 const int q = (int)(L - w + d - hbase);
                 const uint64_t x = X[q];
-                if (mx >= x) { mx = x; my = Y[q]; }
+                if (mx >= x) { mx = x; my = SK_Y(q); }
             }
             if (mx != U64MAX) {
                 const uint64_t o = obase + count;
@@ -348,6 +374,7 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                 if (obase + count > oend) atomicOr(a.overflow, 1);
             }
         }
+#undef SK_Y
         wave_lds_sync();
     }
 }
@@ -1557,8 +1584,7 @@ __global__ void k_ix_build(const uint64_t* keys, const uint32_t* offs, const uin
 #define LAUNCH_CHECK() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 
 int launch_sketch(const SketchArgs& a, int n_blocks, hipStream_t st) {
-    const size_t per_wave = (((size_t)(SK_TS + a.w) * 14) + 15) & ~(size_t)15;
-    const size_t lds = per_wave * 4;
+    const size_t lds = sketch_wave_lds(a.w) * 4;
     if (a.k <= 16) hipLaunchKernelGGL(k_sketch<true>, dim3(n_blocks), dim3(256), lds, st, a);
     else hipLaunchKernelGGL(k_sketch<false>, dim3(n_blocks), dim3(256), lds, st, a);
     LAUNCH_CHECK();
