@@ -438,7 +438,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     {
         FilterArgs fa{n, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, tab_off, tkey, tcnt, keep, 10, 0.01f};
         ProfScope ps(c, "filter");
-        LCHK(launch_filter(fa, grid_for(n), c->stream));
+        LCHK(launch_filter(fa, o->k, grid_for(n), c->stream));
     }
     // 3. lookup + anchor count (index.rs:143-154, seeds.rs:42-57)
     uint32_t *mz_n, *mz_poff, *a_cnt; uint64_t* a_off;

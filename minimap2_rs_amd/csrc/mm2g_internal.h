@@ -146,7 +146,7 @@ struct DvArgs {
 // ---- launchers (return 0 or a hipError_t) --------------------------------
 typedef struct ihipStream_t* hipStream_t;
 int launch_sketch(const mm2g::SketchArgs& a, int n_blocks, hipStream_t st);
-int launch_filter(const mm2g::FilterArgs& a, int n_blocks, hipStream_t st);
+int launch_filter(const mm2g::FilterArgs& a, int k, int n_blocks, hipStream_t st);
 int launch_seed_count(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st);

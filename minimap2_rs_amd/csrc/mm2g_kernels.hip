@@ -392,8 +392,10 @@ DEVI uint32_t tab_size_for(uint32_t m, int q_occ_max) {
     return s;
 }
 DEVI uint32_t fslot(uint64_t h, uint32_t tmask) { return (uint32_t)((h * 0x9E3779B97F4A7C15ULL) >> 32) & tmask; }
+constexpr int FT_MAX = 4096;
+DEVI bool filter_lds_ok(uint32_t ts, int k) { return ts > 0 && ts <= (uint32_t)FT_MAX && k <= 16; }
 
-__global__ __launch_bounds__(256) void k_filter(FilterArgs a) {
+__global__ __launch_bounds__(256) void k_filter(FilterArgs a, int a_k) {
     const int lane = lane_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
@@ -402,10 +404,8 @@ __global__ __launch_bounds__(256) void k_filter(FilterArgs a) {
         uint8_t* keep = a.keep + mb;
         const uint64_t tb = uni64(a.tab_off[r]);
         const uint32_t ts = (uint32_t)(uni64(a.tab_off[r + 1]) - tb);
-        if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) {   // seeds.rs:14-15
-            for (uint32_t b0 = 0; b0 < m; b0 += 64) { const uint32_t i = b0 + lane; if (i < m) keep[i] = 1; }
-            continue;
-        }
+        if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) continue;   // seeds.rs:14-15: k_filter_lds
+        if (filter_lds_ok(ts, a_k)) continue;                        // done by k_filter_lds
         uint64_t* tk = a.tab_key + tb; uint32_t* tc = a.tab_cnt + tb;
         for (uint32_t b0 = 0; b0 < ts; b0 += 64) { const uint32_t i = b0 + lane; if (i < ts) { tk[i] = U64MAX; tc[i] = 0; } }
         vm_drain();
@@ -441,6 +441,54 @@ __global__ __launch_bounds__(256) void k_filter(FilterArgs a) {
             }
             if (i < m) keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
         }
+    }
+}
+
+// LDS variant: one 256-thread block per read, for hashes that fit 32 bits
+// (k <= 16) and tables of at most FT_MAX slots; entries pack (count << 32 | hash)
+// so one 64-bit LDS CAS claims a slot.  Other reads are left to k_filter.
+
+__global__ __launch_bounds__(256) void k_filter_lds(FilterArgs a, int k) {
+    __shared__ unsigned long long T[FT_MAX];
+    const uint32_t r = blockIdx.x;
+    if (r >= a.n) return;
+    const uint64_t mb = a.mz_base[r];
+    const uint32_t m = a.mz_cnt[r];
+    const uint64_t tb = a.tab_off[r];
+    const uint32_t ts = (uint32_t)(a.tab_off[r + 1] - tb);
+    uint8_t* keep = a.keep + mb;
+    if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) {      // seeds.rs:14-15 (and m <= q_occ_max)
+        for (uint32_t i = threadIdx.x; i < m; i += 256) keep[i] = 1;
+        return;
+    }
+    if (!filter_lds_ok(ts, k)) return;
+    const uint32_t tmask = ts - 1;
+    for (uint32_t i = threadIdx.x; i < ts; i += 256) T[i] = 0ULL;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += 256) {
+        const uint32_t h = (uint32_t)(a.mz_x[mb + i] >> 8);
+        uint32_t sl = fslot(h, tmask);
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&T[sl], 0ULL, (1ULL << 32) | h);
+            if (prev == 0ULL) break;
+            if ((uint32_t)prev == h) { atomicAdd(&T[sl], 1ULL << 32); break; }
+            sl = (sl + 1) & tmask;
+        }
+    }
+    __syncthreads();
+    const float prod = (float)m * a.q_occ_frac;                       // (m as f32 * q_occ_frac) as usize
+    const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
+    for (uint32_t i = threadIdx.x; i < m; i += 256) {
+        const uint32_t h = (uint32_t)(a.mz_x[mb + i] >> 8);
+        uint32_t sl = fslot(h, tmask);
+        uint32_t c = 0;
+        for (;;) {
+            const unsigned long long e = T[sl];
+            if (e == 0ULL) break;
+            if ((uint32_t)e == h) { c = (uint32_t)(e >> 32); break; }
+            sl = (sl + 1) & tmask;
+        }
+        keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
     }
 }
 
@@ -1490,44 +1538,68 @@ __global__ __launch_bounds__(1024) void k_read_order(uint32_t n, const uint32_t*
 // the minimizer positions of the (idx.w, idx.k) sketch, then the greedy match.
 // ============================================================================
 
-__global__ __launch_bounds__(256) void k_dv(DvArgs a) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+constexpr int DV_LDS = 4096;   // minimizer positions staged per read (longer reads read HBM)
+__global__ __launch_bounds__(64) void k_dv(DvArgs a) {
+    __shared__ int32_t Ps[DV_LDS];
+    const uint32_t r = blockIdx.x;
     if (r >= a.n) return;
-    ReadOut o = a.out[r];
-    const uint32_t m = a.mz_cnt[r];
-    o.m_dv = (int32_t)m;
-    o.flags &= ~RF_DV_FOUND;
-    if (!(o.flags & RF_MAPPED) || (o.flags & RF_PANIC) || m == 0 || o.cm <= 0) { a.out[r] = o; return; }
-#ifdef MM2G_CHECKED
-    if (a.mz_base[r] + m > a.cap_mz || a.a_off[r] + (uint64_t)o.cm > a.cap_keys) { CK(a.mz_base[r] + m, 0); a.out[r] = o; return; }
-#endif
-    const uint32_t* Y = a.mz_y + a.mz_base[r];
-    const uint32_t* CB = a.chain + a.a_off[r];
-    const uint64_t* K = a.keys + a.a_off[r];
-    const uint64_t An = a.a_off[r + 1] - a.a_off[r];
+    const int lane = lane_id();
+    const int32_t flags = uni(a.out[r].flags), cm = uni(a.out[r].cm);
+    const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
+    const bool go = (flags & RF_MAPPED) && !(flags & RF_PANIC) && m > 0 && cm > 0;
+    if (!go) {
+        if (lane == 0) { a.out[r].m_dv = (int32_t)m; a.out[r].flags = flags & ~RF_DV_FOUND; }
+        return;
+    }
+    const uint64_t mzb = uni64(a.mz_base[r]), ab = uni64(a.a_off[r]);
+    const uint64_t An = uni64(a.a_off[r + 1]) - ab;
     (void)An;
+    const uint32_t* Y = a.mz_y + mzb;
+    const uint32_t* CB = a.chain + ab;
+    const uint64_t* K = a.keys + ab;
     const uint64_t qmask = (1ULL << a.kl.qb) - 1;
-    const bool rev = (uint32_t)o.group >= a.kl.n_seq;
-    const int32_t cm = o.cm, qlen = o.qlen, span = a.span;
-    auto fwdq = [&](int32_t t) -> int32_t {   // t-th chain anchor in forward-query order
-        if (!rev) { const int32_t q = (int32_t)(K[CK(CB[cm - 1 - t], An)] & qmask); return q; }
+    const bool rev = (uint32_t)uni(a.out[r].group) >= a.kl.n_seq;
+    const int32_t qlen = uni(a.out[r].qlen), span = a.span;
+    const bool in_lds = m <= (uint32_t)DV_LDS;
+    if (in_lds) {
+        for (uint32_t j0 = 0; j0 < m; j0 += 64) { const uint32_t j = j0 + lane; if (j < m) Ps[j] = (int32_t)(Y[j] >> 1); }
+        __syncthreads();
+    }
+    auto mpos = [&](uint32_t j) -> int32_t { return in_lds ? Ps[j] : (int32_t)(Y[CK(j, m)] >> 1); };
+    // t-th chain anchor in forward-query order (paf.rs:165-176)
+    auto fwdq = [&](int32_t t) -> int32_t {
+        if (!rev) return (int32_t)(K[CK(CB[cm - 1 - t], An)] & qmask);
         const int32_t q = (int32_t)(K[CK(CB[t], An)] & qmask);
         return qlen - 1 - (q + 1 - span);
     };
-    auto mpos = [&](uint32_t j) -> int32_t { return (int32_t)(Y[CK(j, m)] >> 1); };
-    const int32_t first = fwdq(0);
+    const int32_t first = uni(fwdq(0));
+    // Rust >= 1.82 slice::binary_search (base/size halving, no early exit) (paf.rs:178)
     uint32_t size = m, b = 0;
-    while (size > 1) { const uint32_t half = size / 2, mid = b + half; if (!(mpos(mid) > first)) b = mid; size -= half; }
-    if (mpos(b) != first) { a.out[r] = o; return; }
-    uint32_t st = b;
-    while (st > 0 && mpos(st - 1) == first) --st;
-    uint32_t j = st, en = st; int32_t kk = 1, n_match = 1;
-    while (j + 1 < m && kk < cm) {
-        ++j;
-        if (mpos(j) == fwdq(kk)) { ++n_match; en = j; ++kk; }
+    while (size > 1) { const uint32_t half = size / 2, mid = b + half; if (!(uni(mpos(mid)) > first)) b = mid; size -= half; }
+    if (uni(mpos(b)) != first) {
+        if (lane == 0) { a.out[r].m_dv = (int32_t)m; a.out[r].flags = flags & ~RF_DV_FOUND; }
+        return;
     }
-    o.flags |= RF_DV_FOUND; o.n_match = n_match; o.dv_st = (int32_t)st; o.dv_en = (int32_t)en;
-    a.out[r] = o;
+    uint32_t st = b;
+    while (st > 0 && uni(mpos(st - 1)) == first) --st;
+    // greedy match (paf.rs:179-186): the next j with P[j] == C[kk], 64 candidates per ballot
+    uint32_t j = st, en = st;
+    int32_t kk = 1, n_match = 1, kb = 1;
+    int32_t cv = (kb + lane < cm) ? fwdq(kb + lane) : 0;
+    while (kk < cm && j + 1 < m) {
+        if (kk - kb >= 64) { kb = kk; cv = (kb + lane < cm) ? fwdq(kb + lane) : 0; }
+        const int32_t target = rdl(cv, kk - kb);
+        const uint32_t c0 = j + 1;
+        const uint32_t jl = c0 + (uint32_t)lane;
+        const uint64_t hit = ballot(jl < m && mpos(jl) == target);
+        if (hit) { j = c0 + (uint32_t)ctz64(hit); ++n_match; en = j; ++kk; }
+        else j = (c0 + 63 < m - 1) ? c0 + 63 : m - 1;
+    }
+    if (lane == 0) {
+        ReadOut* O = a.out + r;
+        O->m_dv = (int32_t)m;
+        O->flags = flags | RF_DV_FOUND; O->n_match = n_match; O->dv_st = (int32_t)st; O->dv_en = (int32_t)en;
+    }
 }
 
 // ============================================================================
@@ -1590,8 +1662,11 @@ int launch_sketch(const SketchArgs& a, int n_blocks, hipStream_t st) {
     LAUNCH_CHECK();
     return 0;
 }
-int launch_filter(const FilterArgs& a, int n_blocks, hipStream_t st) {
-    hipLaunchKernelGGL(k_filter, dim3(n_blocks), dim3(256), 0, st, a);
+int launch_filter(const FilterArgs& a, int k, int n_blocks, hipStream_t st) {
+    if (a.n == 0) return 0;
+    hipLaunchKernelGGL(k_filter_lds, dim3(a.n), dim3(256), 0, st, a, k);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_filter, dim3(n_blocks), dim3(256), 0, st, a, k);
     LAUNCH_CHECK();
     return 0;
 }
@@ -1655,7 +1730,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
 }
 int launch_dv(const DvArgs& a, hipStream_t st) {
     if (a.n == 0) return 0;
-    hipLaunchKernelGGL(k_dv, dim3((a.n + 255) / 256), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_dv, dim3(a.n), dim3(64), 0, st, a);
     LAUNCH_CHECK();
     return 0;
 }
