@@ -157,8 +157,11 @@ int mm2g_prof_enable(mm2g_ctx* ctx, int on);
 int mm2g_prof_get(mm2g_ctx* ctx, int i, const char** name, double* ms, int64_t* calls);
 int mm2g_prof_reset(mm2g_ctx* ctx);
 /* Batch counters for roofline accounting: [0]=bases [1]=minimizers
- * [2]=kept minimizers [3]=anchors [4]=rescued anchors [5]=dp pair evaluations */
-int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out6);
+ * [2]=kept minimizers [3]=anchors [4]=rescued anchors [5]=dp pair evaluations
+ * [6]=anchors entering the DP (after the sort's singleton filter).
+ * Copies min(n, MM2G_N_COUNTERS) values; returns how many. */
+#define MM2G_N_COUNTERS 7
+int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus
 }

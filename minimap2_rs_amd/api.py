@@ -275,9 +275,9 @@ class Device:
         return out[: 6 * n].reshape(n, 6)
 
     def counters(self) -> dict:
-        buf = (C.c_uint64 * 6)()
-        check(load().mm2g_batch_counters(self._h, buf), "counters")
-        keys = ["bases", "minimizers", "kept_minimizers", "anchors", "rescued_anchors", "dp_pairs"]
+        buf = (C.c_uint64 * 7)()
+        check(load().mm2g_batch_counters(self._h, buf, 7), "counters")
+        keys = ["bases", "minimizers", "kept_minimizers", "anchors", "rescued_anchors", "dp_pairs", "dp_anchors"]
         return dict(zip(keys, list(buf)))
 
 

@@ -61,7 +61,7 @@ struct mm2g_ctx {
     hipStream_t stream = nullptr;
     // index (device copy shared by every context it was shared with, same device)
     const HostIndex* hidx = nullptr;
-    struct DevIndex { DevBuf tab, ix_pos; };
+    struct DevIndex { DevBuf tab, ix_pos, goff; uint32_t cells = 0; };
     std::shared_ptr<DevIndex> dix;
     uint32_t log2cap = 0;
     int32_t mid_occ = 10;
@@ -75,7 +75,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, dv_separate = false;
@@ -90,7 +90,7 @@ struct mm2g_ctx {
     std::map<std::string, int> slot_ix;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> ev_pool; size_t ev_next = 0;
-    uint64_t counters[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t counters[MM2G_N_COUNTERS] = {};
 
     hipEvent_t ev() {
         if (ev_next == ev_pool.size()) { hipEvent_t e; (void)hipEventCreate(&e); ev_pool.push_back(e); }
@@ -280,6 +280,21 @@ int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
         HIPCHK(hipMemcpyAsync(n_, ns.data(), nk * 4, hipMemcpyHostToDevice, c->stream));
     }
     LCHK(launch_ix_build(k_, o_, n_, nk, tab, l2, c->stream));
+    // singleton-filter cells: per group (fwd, rev) a guard cell, ceil(len / 2^CELL_SHIFT) cells, a guard cell
+    {
+        std::vector<uint32_t> goff(2 * (size_t)H.n_seq + 1);
+        uint64_t run = 0;
+        for (uint32_t g = 0; g < 2 * H.n_seq; ++g) {
+            goff[g] = (uint32_t)std::min<uint64_t>(run, 0xffffffffu);
+            run += ((uint64_t)H.seq[g % H.n_seq].len >> CELL_SHIFT) + 3;
+        }
+        goff[2 * H.n_seq] = (uint32_t)std::min<uint64_t>(run, 0xffffffffu);
+        // two bitmaps must fit the LDS budget of k_sort_read next to its static arrays
+        c->dix->cells = (run <= (uint64_t)320 * 1024) ? (uint32_t)run : 0u;
+        uint32_t* dg;
+        ENSURE(c->dix->goff, uint32_t, goff.size(), dg);
+        HIPCHK(hipMemcpyAsync(dg, goff.data(), goff.size() * 4, hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->log2cap = l2;
     c->hidx = &H;
@@ -468,13 +483,20 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         LCHK(launch_seed_write(sa, grid_for(n), c->stream));
     }
     // 4. anchor sort (seeds.rs:58)
+    uint32_t* cnt2; uint64_t* smax;
+    ENSURE(c->cnt2, uint32_t, n, cnt2);
+    ENSURE(c->smax, uint64_t, n, smax);
+    // the singleton filter is off in debug mode (full anchor/DP arrays for the parity tests)
+    SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
+                (c->debug || getenv("MM2G_NO_FILTER")) ? 0u : c->dix->cells, cnt2, smax, 4096u};
+    if (const char* e = getenv("MM2G_SORT_SMALL")) so.small_max = std::min<uint32_t>((uint32_t)atoi(e), 4096u);   // tests
     {
         ProfScope ps(c, "sort_small");
-        LCHK(launch_sort_read(0, n, a_off, keys, ktmp, kl.qb, c->keys.cap / 8, c->stream));
+        LCHK(launch_sort_read(0, so, c->stream));
     }
     {
         ProfScope ps(c, "sort_large");
-        LCHK(launch_sort_read(1, n, a_off, keys, ktmp, kl.qb, c->keys.cap / 8, c->stream));
+        LCHK(launch_sort_read(1, so, c->stream));
     }
     // 5. chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
     build_lut(c, o->k, lut_need);
@@ -503,7 +525,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     LCHK(launch_read_order(n, a_cnt, order, c->stream));
     ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work,
                  std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, nullptr, order, A, std::min<int32_t>((int32_t)n, 4 * 256), tmark,
-                 lseg, lseg_n, lcap, lseg_order, rbest, mseg, lseg_n + 2, lseg_n + 3, mcap2};
+                 lseg, lseg_n, lcap, lseg_order, rbest, cnt2, smax, mseg, lseg_n + 2, lseg_n + 3, mcap2};
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) {
             ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
@@ -603,6 +625,13 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
         for (auto v : mc) cnt[1] += v;
     }
     for (int t = 0; t < 6; ++t) c->counters[t] = cnt[t];
+    {   // anchors left after the sort's singleton filter (the DP input)
+        std::vector<uint32_t> k2(c->n_reads);
+        if (c->n_reads) HIPCHK(hipMemcpy(k2.data(), c->cnt2.p, c->n_reads * 4, hipMemcpyDeviceToHost));
+        uint64_t kept = 0;
+        for (auto v : k2) kept += v;
+        c->counters[6] = kept;
+    }
     return 0;
 }
 
@@ -758,10 +787,10 @@ int64_t mm2g_debug_chain_stats(mm2g_ctx* c, uint32_t* out6, uint32_t n) {
         }
     return (int64_t)c->n_reads;
 }
-int mm2g_batch_counters(mm2g_ctx* c, uint64_t* out6) {
-    if (!c || !out6) return set_err(MM2G_E_ARG, "null argument");
-    for (int t = 0; t < 6; ++t) out6[t] = c->counters[t];
-    return 0;
+int mm2g_batch_counters(mm2g_ctx* c, uint64_t* out, int n) {
+    if (!c || !out || n < 0) return set_err(MM2G_E_ARG, "null argument");
+    for (int t = 0; t < n && t < MM2G_N_COUNTERS; ++t) out[t] = c->counters[t];
+    return n < MM2G_N_COUNTERS ? n : MM2G_N_COUNTERS;
 }
 
 }  // extern "C"

@@ -106,6 +106,20 @@ struct SeedArgs {
     uint64_t cap_keys, cap_pos, cap_mz;   // bounds for the MM2G_CHECKED build
     ReadOut* out;                         // m_kept
 };
+// per-read anchor sort + singleton filter (k_sort_small / k_sort_read)
+constexpr int CELL_SHIFT = 15;   // 32 kb reference cells (>= every max_dist_x the filter is used with)
+struct SortArgs {
+    uint32_t n;
+    const uint64_t* a_off;
+    uint64_t* keys; uint64_t* tmp;
+    uint32_t qb, rb, n_seq;
+    uint64_t cap_keys;
+    const uint32_t* goff;   // per group: first cell (guard cell before and after every group)
+    uint32_t cells;         // 0 = singleton filter off
+    uint32_t* cnt2;         // per read: anchors kept (sorted at keys[a_off[r] ..])
+    uint64_t* smax;         // per read: 1 + largest dropped (singleton) key, 0 = none
+    uint32_t small_max;     // reads with more anchors go to k_sort_read (LDS bitonic below)
+};
 struct ChainArgs {
     uint32_t n;
     const uint64_t* rd_off;
@@ -127,6 +141,8 @@ struct ChainArgs {
     uint32_t lseg_cap;
     uint32_t* lseg_order;    // long segments, longest first
     unsigned long long* rbest;   // per read: packed (f, index) of the last argmax f
+    const uint32_t* cnt2;    // anchors kept per read (k_sort_read's singleton filter)
+    const uint64_t* smax;    // 1 + largest dropped key per read, 0 = none
     uint4* mseg;             // medium-segment queue: (read, s, e, -)
     uint32_t* mseg_n;        // its length (atomic counter)
     uint32_t* mseg_take;     // next entry to hand out (atomic counter)
@@ -149,9 +165,8 @@ int launch_sketch(const mm2g::SketchArgs& a, int n_blocks, hipStream_t st);
 int launch_filter(const mm2g::FilterArgs& a, int k, int n_blocks, hipStream_t st);
 int launch_seed_count(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
-int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st);
 // per-read MSD bucket sort on (group, rpos) + per-bucket full-key sort (qb = query bits of the key)
-int launch_sort_read(int stage, uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb, uint64_t cap_keys, hipStream_t st);   // 0 small reads, 1 large
+int launch_sort_read(int stage, const mm2g::SortArgs& a, hipStream_t st);   // 0 small reads, 1 large
 // MM2G_CHECKED builds: first recorded bounds violation {line, index, cap}; 0 = none
 int mm2g_checked_read(unsigned long long out[4], hipStream_t st);
 // chain DP of one pass, stage 0..4: k_chain_seg, k_chain_med, k_lseg_order, k_chain_long, k_chain_fin

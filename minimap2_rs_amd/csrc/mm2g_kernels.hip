@@ -589,16 +589,18 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
 // ============================================================================
 constexpr int SORT_SMALL = 4096;
 
-__global__ __launch_bounds__(256) void k_sort_small(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t cap_keys) {
+__global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     __shared__ uint64_t s[SORT_SMALL];
     const uint32_t r = blockIdx.x;
-    if (r >= n) return;
-    const uint64_t base = a_off[r];
-    const uint32_t A = (uint32_t)(a_off[r + 1] - base);
-    if (A <= 1 || A > SORT_SMALL) return;
+    if (r >= a.n) return;
+    const uint64_t base = a.a_off[r];
+    const uint32_t A = (uint32_t)(a.a_off[r + 1] - base);
+    if (A > a.small_max) return;
+    if (threadIdx.x == 0) { a.cnt2[r] = A; a.smax[r] = 0; }   // no singleton filter for small reads
+    if (A <= 1) return;
     uint32_t np = 1; while (np < A) np <<= 1;
-    uint64_t* K = keys;
-    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < A ? K[CK(base + i, cap_keys)] : U64MAX;
+    uint64_t* K = a.keys;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < A ? K[CK(base + i, a.cap_keys)] : U64MAX;
     __syncthreads();
     for (uint32_t kk = 2; kk <= np; kk <<= 1) {
         for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
@@ -613,79 +615,7 @@ __global__ __launch_bounds__(256) void k_sort_small(uint32_t n, const uint64_t* 
             __syncthreads();
         }
     }
-    for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) K[CK(base + i, cap_keys)] = s[i];
-}
-
-__global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys) {
-    __shared__ uint32_t hist[256];
-    __shared__ uint32_t woff[16][256];
-    __shared__ uint64_t red_or[16], red_and[16];
-    const uint32_t r = blockIdx.x;
-    if (r >= n) return;
-    const uint64_t base = a_off[r];
-    const uint32_t A = (uint32_t)(a_off[r + 1] - base);
-    if (A <= SORT_SMALL) return;
-#ifdef MM2G_CHECKED
-    if (base + A > cap_keys) { if (threadIdx.x == 0) CK(base + A, cap_keys); return; }
-#endif
-    const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-    uint64_t* src = keys + base;
-    uint64_t* dst = tmp + base;
-    // bits that vary across the segment
-    uint64_t vo = 0, va = U64MAX;
-    for (uint32_t i = tid; i < A; i += 1024) { uint64_t x = src[i]; vo |= x; va &= x; }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { vo |= __shfl_xor(vo, d, 64); va &= __shfl_xor(va, d, 64); }
-    if (lane == 0) { red_or[wv] = vo; red_and[wv] = va; }
-    __syncthreads();
-    vo = 0; va = U64MAX;
-    for (int t = 0; t < 16; ++t) { vo |= red_or[t]; va &= red_and[t]; }
-    const uint64_t vary = vo ^ va;
-    const int top = vary ? 64 - clz64(vary) : 0;
-    bool in_tmp = false;
-    for (int shift = 0; shift < top; shift += 8) {
-        if (((vary >> shift) & 0xffULL) == 0) continue;       // digit constant: order unchanged
-        if (tid < 256) hist[tid] = 0;
-        __syncthreads();
-        for (uint32_t i = tid; i < A; i += 1024) atomicAdd(&hist[(uint32_t)(src[i] >> shift) & 255u], 1u);
-        __syncthreads();
-        if (tid == 0) {   // exclusive scan of 256 bins (serial, tiny)
-            uint32_t run = 0;
-            for (int d = 0; d < 256; ++d) { uint32_t c = hist[d]; hist[d] = run; run += c; }
-        }
-        __syncthreads();
-        for (uint32_t t0 = 0; t0 < A; t0 += 1024) {
-            const uint32_t i = t0 + tid;
-            const bool valid = i < A;
-            const uint64_t x = valid ? src[i] : 0;
-            const uint32_t d = (uint32_t)(x >> shift) & 255u;
-            for (int t = tid; t < 16 * 256; t += 1024) (&woff[0][0])[t] = 0;
-            __syncthreads();
-            uint64_t peers = ballot(valid);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const bool bit = (d >> b) & 1u;
-                const uint64_t mb = ballot(bit);
-                peers &= bit ? mb : ~mb;
-            }
-            const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-            if (valid && (peers & lanemask_lt()) == 0) woff[wv][d] = (uint32_t)__popcll(peers);
-            __syncthreads();
-            if (tid < 256) {
-                uint32_t run = hist[tid];
-                for (int t = 0; t < 16; ++t) { uint32_t c = woff[t][tid]; woff[t][tid] = run; run += c; }
-                hist[tid] = run;
-            }
-            __syncthreads();
-            if (valid) dst[CK(woff[wv][d] + rank, A)] = x;
-            __syncthreads();
-        }
-        uint64_t* t = src; src = dst; dst = t;
-        in_tmp = !in_tmp;
-    }
-    if (in_tmp) {
-        for (uint32_t i = tid; i < A; i += 1024) dst[i] = src[i];   // src is tmp here, dst is keys
-    }
+    for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) K[CK(base + i, a.cap_keys)] = s[i];
 }
 
 // ---- per-read LSD radix sort on (group, rpos), then qpos for ties.
@@ -697,66 +627,170 @@ __global__ __launch_bounds__(1024) void k_sort_large(uint32_t n, const uint64_t*
 // scatter (items in order, lanes ranked by ballot matching).
 constexpr int RS_ITEMS = 8;
 constexpr int RS_CH = 1024 * RS_ITEMS;
-constexpr int RS_MAXP = 8;   // digit passes (64 bits)
+constexpr int RS_DB = 9;                 // digit bits
+constexpr int RS_ND = 1 << RS_DB;
+constexpr int RS_MAXP = 5;               // digit passes: (group, rpos) has at most 7 + 31 bits
 
-__global__ __launch_bounds__(1024) void k_sort_read(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb,
-                                                    uint64_t cap_keys) {
-    __shared__ uint32_t hist[RS_MAXP][256];
-    __shared__ uint32_t wh[16][256];
+// Singleton filter (before sorting): an anchor alone in its 32 kb reference
+// cell, with both neighbouring cells of its group empty, has no other anchor of
+// its read within max_dist_x (<= 20000 in both DP passes) in the same group, so
+// it forms a one-anchor segment in chain_dp_all (f = span, pprev = -1) and
+// affects the result only through the "last argmax f" tie-break, which then
+// picks the largest key of the read.  Such anchors are dropped from the sort
+// and the DP; the largest dropped key is kept (k_chain_fin).  Two LDS bitmaps
+// (cell seen / seen twice) per read; Q19 anchors are always kept.
+// 8 independent loads per thread, then fn(i, x) for each (i < n): hides HBM
+// latency in the block-wide passes of k_sort_read
+template <typename F>
+DEVI void block_pass8(const uint64_t* src, uint32_t n, F fn) {
+    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * 8) {
+        uint64_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; x[u] = i < n ? src[i] : 0; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; if (i < n) fn(i, x[u]); }
+    }
+}
+
+__global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
     __shared__ uint64_t red[32];
+    __shared__ uint32_t kept;
+    // one dynamic region: the filter's two cell bitmaps, then the radix histograms
+    extern __shared__ uint32_t dyn[];
+    uint32_t (*hist)[RS_ND] = (uint32_t (*)[RS_ND])dyn;                 // RS_MAXP x RS_ND
+    uint32_t (*wh)[RS_ND] = (uint32_t (*)[RS_ND])(dyn + RS_MAXP * RS_ND);  // 16 x RS_ND
+    uint32_t* bm = dyn;                                                   // 2 x ceil(cells / 32) words
     const uint32_t r = blockIdx.x;
-    if (r >= n) return;
-    const uint64_t base = a_off[r];
-    const uint32_t A = (uint32_t)(a_off[r + 1] - base);
-    if (A <= SORT_SMALL) return;     // k_sort_small
+    if (r >= a.n) return;
+    const uint64_t base = a.a_off[r];
+    const uint32_t A0 = (uint32_t)(a.a_off[r + 1] - base);
+    if (A0 <= a.small_max) return;    // k_sort_small
 #ifdef MM2G_CHECKED
-    if (base + A > cap_keys) { if (threadIdx.x == 0) CK(base + A, cap_keys); return; }
+    if (base + A0 > a.cap_keys) { if (threadIdx.x == 0) CK(base + A0, a.cap_keys); return; }
 #endif
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    uint64_t* src = keys + base;
-    uint64_t* dst = tmp + base;
+    const uint32_t qb = a.qb, gsh = a.qb + a.rb;
+    const uint64_t rmask = (1ULL << a.rb) - 1;
+    uint64_t* K = a.keys + base;
+    uint64_t* T = a.tmp + base;
+    uint64_t* src = K;
+    uint64_t* dst = T;
+    uint32_t A = A0;
+    if (tid == 0) kept = 0;
+    const uint32_t nw = (a.cells + 31) >> 5;
+    uint32_t* B1 = bm;
+    uint32_t* B2 = bm + nw;
+    const bool filt = a.cells != 0;
+    uint64_t smx = 0;     // 1 + largest dropped key
+    if (filt) {
+        for (uint32_t i = tid; i < 2 * nw; i += 1024) bm[i] = 0;
+        __syncthreads();
+        block_pass8(K, A0, [&](uint32_t, uint64_t x) {
+            const uint32_t g = (uint32_t)(x >> gsh);
+            if (g < 2u * a.n_seq) {
+                const uint32_t c = a.goff[g] + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
+                const uint32_t bit = 1u << (c & 31);
+                if (atomicOr(&B1[c >> 5], bit) & bit) atomicOr(&B2[c >> 5], bit);
+            }
+        });
+        __syncthreads();
+        // keep non-singletons (compacted into T, order irrelevant: sorted below)
+        for (uint32_t j0 = 0; j0 < A0; j0 += 1024 * 8) {
+          uint64_t xs[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) { const uint32_t i = j0 + (uint32_t)u * 1024 + tid; xs[u] = i < A0 ? K[i] : 0; }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint32_t i = j0 + (uint32_t)u * 1024 + tid;
+            bool keep = false;
+            uint64_t x = 0;
+            if (i < A0) {
+                x = xs[u];
+                const uint32_t g = (uint32_t)(x >> gsh);
+                keep = true;
+                if (g < 2u * a.n_seq) {
+                    const uint32_t c = a.goff[g] + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
+                    const bool twice = (B2[c >> 5] >> (c & 31)) & 1u;
+                    const bool left = (B1[(c - 1) >> 5] >> ((c - 1) & 31)) & 1u;
+                    const bool right = (B1[(c + 1) >> 5] >> ((c + 1) & 31)) & 1u;
+                    keep = twice || left || right;
+                }
+                if (!keep) smx = x + 1 > smx ? x + 1 : smx;
+            }
+            const uint64_t km = ballot(keep);
+            uint32_t wbase = 0;
+            if (lane == 0 && km) wbase = atomicAdd(&kept, (uint32_t)__popcll(km));
+            wbase = (uint32_t)__shfl((int)wbase, 0, 64);
+            if (keep) T[CK(wbase + (uint32_t)__popcll(km & lanemask_lt()), A0)] = x;
+          }
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(smx, d, 64); smx = o > smx ? o : smx; }
+        __syncthreads();
+        if (lane == 0) red[wv] = smx;
+        __syncthreads();
+        smx = 0;
+        for (int t = 0; t < 16; ++t) smx = red[t] > smx ? red[t] : smx;
+        A = kept;
+        src = T; dst = K;
+        __syncthreads();
+    }
+    if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
+    __syncthreads();                                   // the bitmaps are dead from here
+    for (int t = tid; t < RS_MAXP * RS_ND; t += 1024) (&hist[0][0])[t] = 0;
     // bits of (group, rpos) that vary, and all digit histograms in one pass
     uint64_t vo = 0, va = U64MAX;
-    for (uint32_t i = tid; i < A; i += 1024) { const uint64_t h = src[i] >> qb; vo |= h; va &= h; }
+    block_pass8(src, A, [&](uint32_t, uint64_t x) { const uint64_t h = x >> qb; vo |= h; va &= h; });
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) { vo |= __shfl_xor(vo, d, 64); va &= __shfl_xor(va, d, 64); }
+    __syncthreads();
     if (lane == 0) { red[wv] = vo; red[16 + wv] = va; }
-    for (int t = tid; t < RS_MAXP * 256; t += 1024) (&hist[0][0])[t] = 0;
     __syncthreads();
     vo = 0; va = U64MAX;
     for (int t = 0; t < 16; ++t) { vo |= red[t]; va &= red[16 + t]; }
-    const uint64_t vary = vo ^ va;
+    const uint64_t vary = A ? (vo ^ va) : 0;
     const int top = vary ? 64 - clz64(vary) : 0;
-    const int npass = (top + 7) >> 3;
-    for (uint32_t i = tid; i < A; i += 1024) {
-        const uint64_t h = src[i] >> qb;
+    const int npass = (top + RS_DB - 1) / RS_DB;
+    const uint64_t dmask = (uint64_t)RS_ND - 1;
+    block_pass8(src, A, [&](uint32_t, uint64_t x) {
+        const uint64_t h = x >> qb;
         for (int k = 0; k < npass; ++k)
-            if ((vary >> (8 * k)) & 0xffULL) atomicAdd(&hist[k][(uint32_t)(h >> (8 * k)) & 255u], 1u);
-    }
+            if ((vary >> (RS_DB * k)) & dmask) atomicAdd(&hist[k][(uint32_t)(h >> (RS_DB * k)) & (uint32_t)dmask], 1u);
+    });
     __syncthreads();
     if (tid < npass) {
         uint32_t run = 0;
-        for (int d = 0; d < 256; ++d) { const uint32_t c = hist[tid][d]; hist[tid][d] = run; run += c; }
+        for (int d = 0; d < RS_ND; ++d) { const uint32_t c = hist[tid][d]; hist[tid][d] = run; run += c; }
     }
     __syncthreads();
-    bool in_tmp = false;
     for (int k = 0; k < npass; ++k) {
-        if (((vary >> (8 * k)) & 0xffULL) == 0) continue;       // constant digit: order unchanged
-        const int sh = (int)qb + 8 * k;
+        if (((vary >> (RS_DB * k)) & dmask) == 0) continue;       // constant digit: order unchanged
+        const int sh = (int)qb + RS_DB * k;
+        uint64_t x[RS_ITEMS];
+        {   // first chunk
+            const uint32_t w0 = (uint32_t)wv * 64 * RS_ITEMS;
+#pragma unroll
+            for (int it = 0; it < RS_ITEMS; ++it) { const uint32_t i = w0 + (uint32_t)it * 64 + (uint32_t)lane; x[it] = i < A ? src[i] : 0; }
+        }
         for (uint32_t c0 = 0; c0 < A; c0 += RS_CH) {
             const uint32_t w0 = c0 + (uint32_t)wv * 64 * RS_ITEMS;
 #pragma unroll
-            for (int t0 = 0; t0 < 256; t0 += 64) wh[wv][t0 + lane] = 0;
+            for (int t0 = 0; t0 < RS_ND; t0 += 64) wh[wv][t0 + lane] = 0;
             wave_lds_sync();
-            uint64_t x[RS_ITEMS];
 #pragma unroll
             for (int it = 0; it < RS_ITEMS; ++it) {
                 const uint32_t i = w0 + (uint32_t)it * 64 + (uint32_t)lane;
-                x[it] = i < A ? src[i] : 0;
-                if (i < A) atomicAdd(&wh[wv][(uint32_t)(x[it] >> sh) & 255u], 1u);
+                if (i < A) atomicAdd(&wh[wv][(uint32_t)(x[it] >> sh) & (uint32_t)dmask], 1u);
+            }
+            // prefetch the next chunk while the offsets are formed
+            uint64_t nx[RS_ITEMS];
+            {
+                const uint32_t n0 = w0 + RS_CH;
+#pragma unroll
+                for (int it = 0; it < RS_ITEMS; ++it) { const uint32_t i = n0 + (uint32_t)it * 64 + (uint32_t)lane; nx[it] = i < A ? src[i] : 0; }
             }
             __syncthreads();
-            if (tid < 256) {
+            if (tid < RS_ND) {
                 uint32_t run = hist[k][tid];
                 for (int w = 0; w < 16; ++w) { const uint32_t c = wh[w][tid]; wh[w][tid] = run; run += c; }
                 hist[k][tid] = run;
@@ -766,28 +800,29 @@ __global__ __launch_bounds__(1024) void k_sort_read(uint32_t n, const uint64_t* 
             for (int it = 0; it < RS_ITEMS; ++it) {
                 const uint32_t i = w0 + (uint32_t)it * 64 + (uint32_t)lane;
                 const bool valid = i < A;
-                const uint32_t d = (uint32_t)(x[it] >> sh) & 255u;
+                const uint32_t d = (uint32_t)(x[it] >> sh) & (uint32_t)dmask;
                 uint64_t peers = ballot(valid);
 #pragma unroll
-                for (int bb = 0; bb < 8; ++bb) {
+                for (int bb = 0; bb < RS_DB; ++bb) {
                     const bool bit = (d >> bb) & 1u;
                     const uint64_t mb = ballot(bit);
                     peers &= bit ? mb : ~mb;
                 }
                 const uint64_t lt = peers & lanemask_lt();
                 const uint32_t pos = wh[wv][d] + (uint32_t)__popcll(lt);
-                if (valid) dst[CK(pos, A)] = x[it];
+                if (valid) dst[CK(pos, A0)] = x[it];
                 wave_lds_sync();
                 if (valid && lt == 0) wh[wv][d] += (uint32_t)__popcll(peers);
                 wave_lds_sync();
             }
+#pragma unroll
+            for (int it = 0; it < RS_ITEMS; ++it) x[it] = nx[it];
             __syncthreads();
         }
         uint64_t* t = src; src = dst; dst = t;
-        in_tmp = !in_tmp;
+        __syncthreads();
     }
     // sorted by (group, rpos) in src; order runs of equal (group, rpos) by the full key
-    uint64_t* out = keys + base;
     for (uint32_t i = tid; i < A; i += 1024) {
         const uint64_t h = src[i] >> qb;
         const bool start = (i == 0 || (src[i - 1] >> qb) != h) && (i + 1 < A && (src[i + 1] >> qb) == h);
@@ -803,7 +838,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(uint32_t n, const uint64_t* 
         }
     }
     __syncthreads();
-    if (in_tmp) for (uint32_t i = tid; i < A; i += 1024) out[i] = src[i];
+    if (src != K) block_pass8(src, A, [&](uint32_t i, uint64_t x) { K[i] = x; });
 }
 
 // ============================================================================
@@ -981,7 +1016,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
         if (t < (uint32_t)a.n_prio) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
         const uint64_t base = uni64(a.a_off[r]);
-        const int32_t A = (int32_t)(uni64(a.a_off[r + 1]) - base);
+        const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);      // anchors kept by the singleton filter
         if (A == 0) continue;
 #ifdef MM2G_CHECKED
         if (base + (uint64_t)A > a.cap_keys) { if (lane == 0) CK(base + A, a.cap_keys); continue; }
@@ -1477,16 +1512,30 @@ __global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const uint32_t gsh = rb + qb;
     const int32_t span = P.span;
-    const unsigned long long bk = a.rbest[r];
-    const int32_t best_f = (int32_t)((uint32_t)(bk >> 32) ^ 0x80000000u), best_i = (int32_t)(uint32_t)bk;
-    const uint64_t* K = a.keys + base;
+    const int32_t A2 = (int32_t)a.cnt2[r];          // anchors in the DP (singleton filter)
+    const uint64_t sm = a.smax[r];                  // 1 + largest dropped key, 0 = none
+    uint64_t* K = (uint64_t*)a.keys + base;       // writable: slot A2 receives a dropped best
     const int32_t* PP = a.pp + base;
     uint32_t* CB = a.chain + base;
-    int32_t idx = best_i, root = best_i, cm = 0;
-    while (idx >= 0 && cm < A) {
-        CB[cm] = (uint32_t)idx;
-        ++cm; root = idx;
-        idx = PP[CK(idx, A)];
+    int32_t best_f = span, best_i = -1;
+    if (A2 > 0) {
+        const unsigned long long bk = a.rbest[r];
+        best_f = (int32_t)((uint32_t)(bk >> 32) ^ 0x80000000u); best_i = (int32_t)(uint32_t)bk;
+    }
+    // "last argmax f" over all anchors: a dropped singleton (f = span) wins when
+    // every kept anchor also has f == span and its key is the largest
+    const bool single = sm != 0 && (A2 == 0 || (best_f == span && sm - 1 > K[CK(A2 - 1, A)]));
+    int32_t idx, root, cm = 0;
+    if (single) {
+        K[CK(A2, A)] = sm - 1;                      // slot A2 is free (A2 < A); k_dv reads it via CB
+        CB[0] = (uint32_t)A2; cm = 1; root = A2; best_i = A2; best_f = span;
+    } else {
+        idx = best_i; root = best_i;
+        while (idx >= 0 && cm < A2) {
+            CB[cm] = (uint32_t)idx;
+            ++cm; root = idx;
+            idx = PP[CK(idx, A)];
+        }
     }
     const uint64_t kb = K[CK(best_i, A)], kr = K[CK(root, A)];
     const uint32_t g = (uint32_t)(kb >> gsh);
@@ -1680,18 +1729,13 @@ int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
     LAUNCH_CHECK();
     return 0;
 }
-int launch_sort_read(int stage, uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint32_t qb, uint64_t cap_keys, hipStream_t st) {
-    if (n == 0) return 0;
-    if (stage == 0) hipLaunchKernelGGL(k_sort_small, dim3(n), dim3(256), 0, st, n, a_off, keys, cap_keys);
-    else hipLaunchKernelGGL(k_sort_read, dim3(n), dim3(1024), 0, st, n, a_off, keys, tmp, qb, cap_keys);
-    LAUNCH_CHECK();
-    return 0;
-}
-int launch_sort(uint32_t n, const uint64_t* a_off, uint64_t* keys, uint64_t* tmp, uint64_t cap_keys, hipStream_t st) {
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_sort_small, dim3(n), dim3(256), 0, st, n, a_off, keys, cap_keys);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_sort_large, dim3(n), dim3(1024), 0, st, n, a_off, keys, tmp, cap_keys);
+int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
+    if (a.n == 0) return 0;
+    if (stage == 0) hipLaunchKernelGGL(k_sort_small, dim3(a.n), dim3(256), 0, st, a);
+    else {
+        const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4, hb = (size_t)(RS_MAXP + 16) * RS_ND * 4;
+        hipLaunchKernelGGL(k_sort_read, dim3(a.n), dim3(1024), bmb > hb ? bmb : hb, st, a);
+    }
     LAUNCH_CHECK();
     return 0;
 }

@@ -92,6 +92,18 @@ def small_world(tmp_path_factory):
     return ref, reads, rnames, rseqs
 
 
+def _map_nodebug(dev, rnames, rseqs):
+    """Map with debug off: the production path, incl. the singleton filter of the sort."""
+    dev.set_debug(False)
+    dev.set_reads(rseqs)
+    res = dev.map(M.map_opts())
+    return dev.paf(rnames, res), res
+
+
+_RES_FIELDS = ("flags", "n_anchors", "score", "cm", "qs", "qe", "ts", "te", "rid", "rev", "n_match", "dv_st", "dv_en",
+               "m_dv", "sum_k", "qlen", "dv")
+
+
 def _dp_diff(gf, gpp, f, pp, want_a):
     bad = np.nonzero((gf != f) | (gpp.astype(np.int64) != pp))[0]
     if len(bad) == 0:
@@ -131,6 +143,7 @@ def test_pipeline_parity(dev, small_world, tmp_path):
     oi.align_fasta(reads, want_paf)
     got = dev.paf(rnames, res)
     assert got == open(want_paf).read()
+    assert _map_nodebug(dev, rnames, rseqs)[0] == got          # production path (singleton filter on)
 
 
 def test_pipeline_determinism(dev, small_world):
@@ -217,6 +230,8 @@ def test_pipeline_parity_dense(dev, dense_world, tmp_path, mid_occ):
     want_paf = str(tmp_path / "want.paf")
     _, counts, _ = oi.align_fasta(reads, want_paf, mid_occ=mid_occ)
     assert dev.paf(rnames, res) == open(want_paf).read()
+    assert _map_nodebug(dev, rnames, rseqs)[0] == open(want_paf).read()
+    dev.set_debug(True)
     # the DP pair counter behind bench.py's pairs/s equals the reference's inner-loop iterations
     assert dev.counters()["dp_pairs"] == counts["inner_iters"]
 
@@ -261,6 +276,32 @@ def test_golden_world_gpu(dev, tmp_path):
         assert bool(res[i].flags & 2) == r["rescued"], r["name"]
     got = dev.paf([r["name"] for r in gold["reads"]], res).splitlines()
     assert got == [r["paf"] for r in gold["reads"] if r["paf"]]
+    assert _map_nodebug(dev, [r["name"] for r in gold["reads"]], seqs)[0].splitlines() == got
+
+
+def test_singleton_filter_is_transparent(dev, small_world, dense_world):
+    """Every per-read result field is identical with the sort's singleton
+    filter on (production) and off (debug): dropped anchors only ever form
+    one-anchor segments, and the largest dropped key settles f == span ties."""
+    os.environ["MM2G_SORT_SMALL"] = "1"        # every read through k_sort_read (the filtering sort)
+    try:
+        _filter_transparent(dev, small_world, dense_world)
+    finally:
+        del os.environ["MM2G_SORT_SMALL"]
+
+
+def _filter_transparent(dev, small_world, dense_world):
+    for world, mid in ((small_world, None), (dense_world, 5000), (dense_world, 20)):
+        ref, reads, rnames, rseqs = world
+        idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+        dev.upload_index(idx, mid if mid is not None else max(idx.calc_mid_occ(2e-4), 10))
+        dev.set_debug(True)
+        dev.set_reads(rseqs)
+        r1 = dev.map(M.map_opts())
+        a = [tuple(getattr(r1[i], f) for f in _RES_FIELDS) for i in range(len(rseqs))]
+        _, r2 = _map_nodebug(dev, rnames, rseqs)
+        b = [tuple(getattr(r2[i], f) for f in _RES_FIELDS) for i in range(len(rseqs))]
+        assert a == b
 
 
 def test_cli_align_gpu(small_world, tmp_path):
