@@ -914,6 +914,9 @@ constexpr int KRING = 512;        // per-wave LDS ring of the newest anchor keys
 constexpr int TQ = 128;           // per-wave LDS queue per tiny length class (2 | 3-4 | 5-8 anchors)
 constexpr int MEDB = 128;         // per-wave LDS buffer of medium segments before the global append
 constexpr int64_t EST_LANE = 2048;   // estimated DP pairs above which a segment goes to a whole wave
+// rescue pass (few reads, GPU otherwise idle): latency matters, so only small
+// segments stay on one lane
+constexpr int64_t EST_LANE_RESCUE = 96;
 
 // Scalar chain_dp_all (lchain.rs:73-90) of one segment of <= TINY anchors held
 // in registers (keys from the wave's LDS key ring); `act` lanes only.  Local indices; marks t[pprev[j]] = i are a
@@ -1078,7 +1081,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
                 const int64_t bp = p1 - p0 > 0 ? (int64_t)(p1 - p0) : 1;
                 int64_t win = ((int64_t)len * maxdx + bp - 1) / bp;
                 win = win < len ? win : len;
-                med = (int64_t)len * win / 2 <= EST_LANE;
+                med = (int64_t)len * win / 2 <= (P.pass == 0 ? EST_LANE : EST_LANE_RESCUE);
             }
             const bool big = emit && len > TINY && !med;
             const uint64_t medM = ballot(med);
