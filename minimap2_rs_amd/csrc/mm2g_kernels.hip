@@ -544,9 +544,10 @@ DEVI uint64_t pack_anchor(uint64_t rr, uint32_t my, int32_t qlen, int span, cons
 }
 
 __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
-    __shared__ uint32_t s_inc[4][64];
+    __shared__ uint32_t s_inc[4][64], s_poff[4][64], s_y[4][64];
     const int lane = lane_id(), wv = wave_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
+    constexpr int U = 4;   // output batches whose position gathers are in flight together
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wv; r < a.n; r += nwaves) {
         const uint64_t mb = uni64(a.mz_base[r]);
         const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
@@ -556,23 +557,36 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
         uint64_t run = 0;
         for (uint32_t c0 = 0; c0 < m; c0 += 64) {
             const uint32_t i = c0 + lane;
-            const uint32_t n = i < m ? a.mz_n[CK(mb + i, a.cap_mz)] : 0;
+            const bool vi = i < m;
+            const uint32_t n = vi ? a.mz_n[CK(mb + i, a.cap_mz)] : 0;
+            const uint32_t po = vi ? a.mz_poff[CK(mb + i, a.cap_mz)] : 0;
+            const uint32_t yy = vi ? a.mz_y[CK(mb + i, a.cap_mz)] : 0;
             uint32_t tot;
             const uint32_t ex = wave_excl_sum(n, tot);
-            s_inc[wv][lane] = ex + n;
+            s_inc[wv][lane] = ex + n; s_poff[wv][lane] = po; s_y[wv][lane] = yy;
             wave_lds_sync();
-            for (uint32_t tb = 0; tb < tot; tb += 64) {
-                const uint32_t t = tb + lane;
-                if (t < tot) {
-                    // owner = number of inclusive offsets <= t (first lane whose offset exceeds t)
-                    uint32_t lo = 0;
+            for (uint32_t tb = 0; tb < tot; tb += 64 * U) {
+                uint64_t rr[U];
+                uint32_t own[U];
 #pragma unroll
-                    for (uint32_t step = 32; step >= 1; step >>= 1)
-                        if (s_inc[wv][lo + step - 1] <= t) lo += step;
-                    const uint32_t mi = c0 + lo;
-                    const uint32_t exo = lo ? s_inc[wv][lo - 1] : 0;
-                    const uint64_t rr = a.ix_pos[CK((uint64_t)a.mz_poff[CK(mb + mi, a.cap_mz)] + (t - exo), a.cap_pos)];
-                    out[CK(obase + run + t, a.cap_keys)] = pack_anchor(rr, a.mz_y[CK(mb + mi, a.cap_mz)], qlen, a.span, a.kl);
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t t = tb + (uint32_t)u * 64 + (uint32_t)lane;
+                    rr[u] = 0; own[u] = 0;
+                    if (t < tot) {
+                        // owner = number of inclusive offsets <= t (first lane whose offset exceeds t)
+                        uint32_t lo = 0;
+#pragma unroll
+                        for (uint32_t step = 32; step >= 1; step >>= 1)
+                            if (s_inc[wv][lo + step - 1] <= t) lo += step;
+                        const uint32_t exo = lo ? s_inc[wv][lo - 1] : 0;
+                        own[u] = lo;
+                        rr[u] = a.ix_pos[CK((uint64_t)s_poff[wv][lo] + (t - exo), a.cap_pos)];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t t = tb + (uint32_t)u * 64 + (uint32_t)lane;
+                    if (t < tot) out[CK(obase + run + t, a.cap_keys)] = pack_anchor(rr[u], s_y[wv][own[u]], qlen, a.span, a.kl);
                 }
             }
             run += tot;
