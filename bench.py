@@ -88,15 +88,22 @@ def reduce_step_time(dist, elapsed: float, n_bases: int, world: int, device):
 SORT_SMALL = 4096   # reads up to this many anchors are sorted by k_sort_small (mm2g_kernels.hip)
 
 
-def pmc_traffic(kernel: str):
+def bench_config_tag(args) -> str:
+    return f"reads={args.reads},read_len={args.read_len},streams={max(1, args.streams)},scale={args.scale}"
+
+
+def pmc_traffic(kernel: str, tag: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
     passes (profiles/pmc_traffic.json, written by tools/pmc_traffic.py:
     2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md §HBM), or None when no PMC profile of it exists."""
+    MI355X_MICROARCH.md §HBM) when they were taken with this bench
+    configuration; otherwise None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             t = json.load(fh)
+        if t.get("bench_config") != tag:
+            return None
         return t["kernels"][kernel]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
@@ -123,9 +130,17 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # one process per GPU; MM2G_DIST_BACKEND=gloo rehearses the launch on fewer GPUs
+    backend = os.environ.get("MM2G_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
 
     import minimap2_rs_amd as M
     from minimap2_rs_amd import _lib as L
@@ -151,7 +166,7 @@ def main():
     n_bases = int(roffs[-1])
 
     S = max(1, args.streams)
-    devs = [M.Device(local) for _ in range(S)]
+    devs = [M.Device(gpu) for _ in range(S)]
     t0 = time.time()
     devs[0].upload_index(idx, mid)
     for d in devs[1:]:
@@ -231,7 +246,7 @@ def main():
         fl = np.array([sh["res"][i].flags for sh in shards for i in range(sh["n"])], dtype=np.int64)
         np.savez(args.stats, chain=cs, n_anchors=na, flags=fl)
 
-    elapsed, all_bases = reduce_step_time(dist, elapsed, n_bases, world, "cuda")
+    elapsed, all_bases = reduce_step_time(dist, elapsed, n_bases, world, red_dev)
     total_bases = all_bases * args.steps
 
     value = total_bases / elapsed / 1e9
@@ -266,7 +281,7 @@ def main():
     avg_s = d_ms / 1e3 / max(d_calls, 1)
     bytes_per_launch = d_bytes * args.steps / max(d_calls, 1)
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic = pmc_traffic(d_sym)
+    traffic = pmc_traffic(d_sym, bench_config_tag(args))
     roofline = {
         "bound": "hbm", "kernel": d_sym, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,

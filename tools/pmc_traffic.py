@@ -36,12 +36,13 @@ def main():
     ap.add_argument("write_csv")
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
     ap.add_argument("--cmd", default="")
+    ap.add_argument("--config", default="", help='bench config the counters were taken with, e.g. "reads=10000,streams=3,scale=1.0"')
     a = ap.parse_args()
     f = per_kernel(a.fetch_csv, "FETCH_SIZE")
     w = per_kernel(a.write_csv, "WRITE_SIZE")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs, --kernel-trace)",
            "correction": "hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE = half of wide-read bytes)",
-           "command": a.cmd, "kernels": {}}
+           "command": a.cmd, "bench_config": a.config, "kernels": {}}
     for k in sorted(set(f) | set(w)):
         fb, fn = f.get(k, (0.0, 0))
         wb, wn = w.get(k, (0.0, 0))
