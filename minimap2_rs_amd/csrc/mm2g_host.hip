@@ -140,6 +140,53 @@ struct ProfScope {
     }
 };
 
+// MM2G_SORT_PROF: phase times of k_sort_read (wall clock, 100 MHz) to stderr
+static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
+    std::vector<uint64_t> h((size_t)n * 8);
+    if (hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) return;
+    (void)hipFree(d);
+    double ph[5] = {0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0;
+    uint64_t t_lo = ~0ULL, t_hi = 0;
+    uint32_t m = 0;
+    for (uint32_t r = 0; r < n; ++r) {
+        const uint64_t* p = &h[(size_t)r * 8];
+        if (!p[5]) continue;
+        ++m;
+        for (int k = 0; k < 5; ++k) ph[k] += (double)(p[k + 1] - p[k]);
+        tot += (double)(p[5] - p[0]);
+        a0 += (double)p[6]; a2 += (double)(uint32_t)p[7]; np += (double)(p[7] >> 32);
+        t_lo = std::min(t_lo, p[0]); t_hi = std::max(t_hi, p[5]);
+    }
+    if (!m) return;
+    fprintf(stderr, "[sort_prof] reads=%u A0=%.0f A=%.0f npass=%.2f us/read: filter=%.1f hist=%.1f radix=%.1f tiefix=%.1f copy=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
+            m, a0 / m, a2 / m, np / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
+            tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
+}
+
+// MM2G_SKETCH_PROF: phase times of k_sketch summed over each read's tiles
+static void dump_sketch_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
+    std::vector<uint64_t> h((size_t)n * 8);
+    if (hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) return;
+    (void)hipFree(d);
+    double ph[5] = {0, 0, 0, 0, 0}, L = 0;
+    uint32_t m = 0;
+    uint64_t t_hi = 0;
+    for (uint32_t r = 0; r < n; ++r) {
+        const uint64_t* p = &h[(size_t)r * 8];
+        if (!p[5]) continue;
+        ++m;
+        for (int k = 0; k < 5; ++k) ph[k] += (double)p[k];
+        L += (double)p[5];
+        t_hi = std::max(t_hi, p[6]);
+    }
+    if (!m) return;
+    double tot = ph[0] + ph[1] + ph[2] + ph[3] + ph[4];
+    fprintf(stderr, "[sketch_prof] reads=%u len=%.0f us/read: stage=%.1f warmup=%.1f phase1=%.1f phase2=%.1f tail=%.1f total=%.1f\n",
+            m, L / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100, tot / m / 100);
+}
+
 static inline uint32_t bit_width(uint64_t x) { uint32_t b = 0; while (x) { ++b; x >>= 1; } return b; }
 static inline int grid_for(uint32_t n) { int b = (int)((n + 3) / 4); return std::max(1, std::min(b, 4096)); }
 
@@ -363,7 +410,10 @@ static int run_sketch(mm2g_ctx* c, int w, int k, DevBuf& b_base, DevBuf& b_end, 
     SketchArgs a{(const uint8_t*)c->rd_seq.p, (const uint64_t*)c->rd_off.p, n, w, k, base, end, x, y, cnt, ovf};
     {
         ProfScope ps(c, "sketch");
+        uint64_t* skp = nullptr;
+        if (getenv("MM2G_SKETCH_PROF")) { HIPCHK(hipMalloc(&skp, (size_t)n * 64)); HIPCHK(hipMemsetAsync(skp, 0, (size_t)n * 64, c->stream)); a.prof = skp; }
         LCHK(launch_sketch(a, grid_for(n), c->stream));
+        if (skp) dump_sketch_prof(c, skp, n);
     }
     HIPCHK(hipMemcpyAsync(c->h_small, ovf, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -488,7 +538,9 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->smax, uint64_t, n, smax);
     // the singleton filter is off in debug mode (full anchor/DP arrays for the parity tests)
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
-                (c->debug || getenv("MM2G_NO_FILTER")) ? 0u : c->dix->cells, cnt2, smax, 4096u};
+                (c->debug || getenv("MM2G_NO_FILTER")) ? 0u : c->dix->cells, cnt2, smax, 4096u, nullptr};
+    uint64_t* sprof = nullptr;
+    if (getenv("MM2G_SORT_PROF")) { HIPCHK(hipMalloc(&sprof, (size_t)n * 64)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 64, c->stream)); so.prof = sprof; }
     if (const char* e = getenv("MM2G_SORT_SMALL")) so.small_max = std::min<uint32_t>((uint32_t)atoi(e), 4096u);   // tests
     {
         ProfScope ps(c, "sort_small");
@@ -498,6 +550,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         ProfScope ps(c, "sort_large");
         LCHK(launch_sort_read(1, so, c->stream));
     }
+    if (sprof) dump_sort_prof(c, sprof, n);
     // 5. chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
     build_lut(c, o->k, lut_need);
     int16_t* lut; uint32_t* work;

@@ -83,6 +83,7 @@ struct SketchArgs {
     uint32_t* mz_y;             // i<<1 | z   (rid is implicit / added by caller)
     uint32_t* mz_cnt;           // per sequence
     int32_t* overflow;
+    uint64_t* prof;             // MM2G_SKETCH_PROF: per sequence 8 phase-time sums (else null)
 };
 struct FilterArgs {
     uint32_t n;
@@ -119,6 +120,7 @@ struct SortArgs {
     uint32_t* cnt2;         // per read: anchors kept (sorted at keys[a_off[r] ..])
     uint64_t* smax;         // per read: 1 + largest dropped (singleton) key, 0 = none
     uint32_t small_max;     // reads with more anchors go to k_sort_read (LDS bitonic below)
+    uint64_t* prof;         // MM2G_SORT_PROF: per read 8 wall-clock stamps of k_sort_read's phases (else null)
 };
 struct ChainArgs {
     uint32_t n;

@@ -147,24 +147,56 @@ DEVI uint64_t uni64(uint64_t v) {
 // ============================================================================
 constexpr int SK_CH = 8;
 constexpr int SK_TS = 64 * SK_CH;
-constexpr int SK_HALO = 32;                         // bases before the tile (>= k-1)
 
-// per-wave LDS: X[NB] (x = hash<<8 | span, MAX = no info), LZ[NB] (l | z<<15),
-// B[SK_HALO + SK_TS] (the tile's bases); y = pos<<1 | z is implicit
+// per-wave LDS: X[NB] (x = hash<<8 | span, MAX = no info), LZ[NB] (l | z<<15);
+// y = pos<<1 | z is implicit.  Bases stay in registers (8 per lane).
 __host__ __device__ inline size_t sketch_wave_lds(int w) {
     const size_t nb = (size_t)SK_TS + (size_t)w;
-    return ((nb * 8 + nb * 2 + SK_HALO + SK_TS) + 15) & ~(size_t)15;
+    return ((nb * 8 + nb * 2) + 15) & ~(size_t)15;
 }
 
+// reverse the order of the 32 2-bit groups of x
+DEVI uint64_t rev2_64(uint64_t x) {
+    x = ((x >> 2) & 0x3333333333333333ULL) | ((x & 0x3333333333333333ULL) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0FULL) | ((x & 0x0F0F0F0F0F0F0F0FULL) << 4);
+    return __builtin_bswap64(x);
+}
+// 8 bases (byte u = position p0+u, 'N' outside [0, L)) -> 2-bit codes, latest
+// base lowest (code16 = sum c_u << 2(7-u)), and validity (bit u) of nt4 (src/nt4.rs)
+DEVI uint64_t load_bases8(const uint8_t* s, int64_t p0, int64_t L) {
+    uint64_t v;
+    if (p0 >= 0 && p0 + 8 <= L) __builtin_memcpy(&v, s + p0, 8);
+    else {
+        v = 0;
+        for (int u = 0; u < 8; ++u) {
+            const int64_t p = p0 + u;
+            v |= (uint64_t)((p >= 0 && p < L) ? s[p] : (uint8_t)'N') << (8 * u);
+        }
+    }
+    return v;
+}
+DEVI void codes8(uint64_t v, uint32_t& code16, uint32_t& valid8) {
+    code16 = 0; valid8 = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const uint32_t c = nt4d((uint32_t)(v >> (8 * u)) & 0xffu);
+        code16 |= (c & 3u) << (2 * (7 - u));
+        valid8 |= (c < 4 ? 1u : 0u) << u;
+    }
+}
+DEVI uint32_t rev8(uint32_t v) { return __builtin_bitreverse32(v) >> 24; }
+
 template <bool K32>
-__global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
+#ifndef SK_WPE
+#define SK_WPE 4            // waves per SIMD: caps k_sketch at 128 VGPRs
+#endif
+__global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int w = a.w, k = a.k;
     const int NB = SK_TS + w;                        // history (w) + tile
     const int wv = wave_id(), lane = lane_id();
     uint64_t* X = (uint64_t*)(smem + sketch_wave_lds(w) * wv);
     uint16_t* LZ = (uint16_t*)(X + NB);
-    uint8_t* Bs = (uint8_t*)(LZ + NB);
     const int CAP = w + k;
     const uint64_t mask = (k >= 32) ? U64MAX : ((1ULL << (2 * k)) - 1);
     const uint32_t shift1 = 2u * (uint32_t)(k - 1);
@@ -175,6 +207,8 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
         const int64_t L = (int64_t)(uni64(a.rd_off[r + 1]) - roff);
         const uint64_t obase = uni64(a.out_base[r]), oend = uni64(a.out_end[r]);
         if (L == 0) { if (lane == 0) a.mz_cnt[r] = 0; continue; }
+        uint64_t pt[6] = {0, 0, 0, 0, 0, 0}, tz = a.prof ? wall_clock64() : 0;
+#define SK_PT(ph) do { if (a.prof) { const uint64_t t_ = wall_clock64(); pt[ph] += t_ - tz; tz = t_; } } while (0)
         // history slots = positions [-w, -1]: MAX
         for (int t0 = 0; t0 < w; t0 += 64) {
             const int t = t0 + lane;
@@ -182,52 +216,74 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
         }
         uint64_t count = 0;
         int32_t l_carry = 0;
+        // bases of this lane's chunk, prefetched one tile ahead; lanes 0-3 also
+        // keep the previous tile's last 32 bases (codes | reversed validity << 16)
+        uint32_t code16, valid8;
+        codes8(load_bases8(s, (int64_t)lane * SK_CH, L), code16, valid8);
+        uint32_t halo = 0;
         for (int64_t t0 = 0; t0 < L; t0 += SK_TS) {
+            // opaque per tile: keeps lane-derived values from being hoisted and held
+            // in registers across the read loop (VGPR pressure)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
             const int64_t hbase = t0 - w;            // LDS index = p - hbase
-            const int64_t bbase = t0 - SK_HALO;      // Bs index = p - bbase
-            // ---- stage the tile's bases (+ halo) in LDS: coalesced byte loads
-            wave_lds_sync();
-#pragma unroll
-            for (int j = 0; j < (SK_HALO + SK_TS + 63) / 64; ++j) {
-                const int bi = j * 64 + lane;
-                const int64_t p = bbase + bi;
-                if (bi < SK_HALO + SK_TS) Bs[bi] = (p >= 0 && p < L) ? s[p] : (uint8_t)'N';
-            }
-            wave_lds_sync();
-            const int64_t ps = t0 + (int64_t)lane * SK_CH;
+            const int64_t ps = t0 + (int64_t)ln * SK_CH;
             const int64_t pe = ps + SK_CH < L ? ps + SK_CH : L;
+            // next tile's bases: loaded now, decoded before this tile's first store
+            // (vmcnt also counts stores: decoding later would wait for them)
+            const uint64_t nbytes = t0 + SK_TS < L ? load_bases8(s, ps + SK_TS, L) : 0;
+            const uint32_t own = code16 | (rev8(valid8) << 16);
+            wave_lds_sync();
+            SK_PT(0);
             // ---- phase 1a: k-mers and per-position flags.  Warm-up: the k-mer
             // registers hold the last k-1 ACGT bases before ps (ambiguous bases
             // are skipped, src/sketch.rs:75-76,86-88; from the initial zeros at
             // the read start) -- exactly, since the symmetric-k-mer test that
-            // gates l sees them.  Bytes come from the LDS tile + halo, from HBM
-            // only past the halo (long ambiguous runs).
-            uint64_t kf = 0, kr = 0;
+            // gates l sees them.  Fast path: those k-1 bases are the ACGT bases
+            // of the four chunks before ps (ln shuffles); otherwise a walk back
+            // over HBM.
+            uint64_t kf, kr;
             {
-                auto base_at = [&](int64_t p) -> uint32_t { return p >= bbase ? nt4d(Bs[(int)(p - bbase)]) : nt4d(s[p]); };
-                int64_t wsp = ps;
-                int need = ps < pe ? k - 1 : 0;
-                while (any(need > 0 && wsp > 0)) {
-                    if (need > 0 && wsp > 0) { --wsp; if (base_at(wsp) < 4) --need; }
+                uint64_t W = 0; uint32_t V = 0;
+#pragma unroll
+                for (int d = 1; d <= 4; ++d) {
+                    const uint32_t o1 = (uint32_t)__shfl((int)own, (ln - d) & 63, 64);
+                    const uint32_t o2 = (uint32_t)__shfl((int)halo, (ln - d + 4) & 63, 64);
+                    const uint32_t pk = ln >= d ? o1 : o2;
+                    W |= (uint64_t)(pk & 0xffffu) << (16 * (d - 1));
+                    V |= (pk >> 16) << (8 * (d - 1));
                 }
-                int64_t pw = wsp;
-                while (any(pw < ps)) {
-                    if (pw < ps) {
-                        const uint32_t c = base_at(pw);
-                        if (c < 4) { kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1); }
-                        ++pw;
+                const uint32_t need_bits = (k - 1 >= 32) ? 0xffffffffu : ((1u << (k - 1)) - 1u);
+                const bool slow = ps < pe && (ps < k - 1 || (V & need_bits) != need_bits);
+                kf = W & ((k - 1 >= 32) ? U64MAX : ((1ULL << (2 * (k - 1))) - 1));
+                kr = (rev2_64(~W) >> (64 - 2 * k)) & ~3ULL;
+                if (any(slow)) {
+                    if (slow) { kf = 0; kr = 0; }
+                    int64_t wsp = ps;
+                    int need = slow ? k - 1 : 0;
+                    while (any(need > 0 && wsp > 0)) {
+                        if (need > 0 && wsp > 0) { --wsp; if (nt4d(s[wsp]) < 4) --need; }
+                    }
+                    int64_t pw = slow ? wsp : ps;
+                    while (any(pw < ps)) {
+                        if (pw < ps) {
+                            const uint32_t c = nt4d(s[pw]);
+                            if (c < 4) { kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1); }
+                            ++pw;
+                        }
                     }
                 }
             }
+            SK_PT(1);
             bool rs = false; int32_t lc = 0;
 #pragma unroll
             for (int t = 0; t < SK_CH; ++t) {
                 const int64_t p = ps + t;
                 if (p < pe) {
                     const int ix = (int)(p - hbase);
-                    const uint32_t c = nt4d(Bs[(int)(p - bbase)]);
+                    const uint32_t c = (code16 >> (2 * (7 - t))) & 3u;
                     uint64_t x = U64MAX; uint16_t fl = 0, z = 0;
-                    if (c < 4) {
+                    if ((valid8 >> t) & 1u) {
                         kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1);
                         fl = 1;
                         if (kf != kr) {
@@ -251,10 +307,10 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
 #pragma unroll
                 for (int d = 1; d < 64; d <<= 1) {
                     const int32_t orr = __shfl_up(ir, d, 64), oc = __shfl_up(ic, d, 64);
-                    if (lane >= d && !ir) { ic = oc + ic < CAP ? oc + ic : CAP; ir = orr; }
+                    if (ln >= d && !ir) { ic = oc + ic < CAP ? oc + ic : CAP; ir = orr; }
                 }
                 er = __shfl_up(ir, 1, 64); ec = __shfl_up(ic, 1, 64);
-                if (lane == 0) { er = 0; ec = 0; }
+                if (ln == 0) { er = 0; ec = 0; }
             }
             const int32_t lin = er ? ec : (l_carry + ec < CAP ? l_carry + ec : CAP);
             wave_lds_sync();
@@ -278,14 +334,92 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                 l_carry = rdl(lv, owner);
             }
             wave_lds_sync();
+            SK_PT(2);
 #define SK_Y(q) ((((uint32_t)(hbase + (q))) << 1) | (uint32_t)(LZ[(q)] >> 15))
+            uint32_t code16n, valid8n;
+            codes8(nbytes, code16n, valid8n);
             // ---- phase 2: reference step logic, count then write
             uint32_t myoff = 0, tot = 0;
-            for (int pass = 0; pass < 2; ++pass) {
+            bool fast_done = false;
+#define SK_EMIT(xv, yv) do { if (WR && o < oend) { a.mz_x[o] = (xv); a.mz_y[o] = (yv); } ++o; ++n_em; } while (0)
+            if (w > SK_CH) {
+                // The reference's `min` after step i is the newest minimum of slots
+                // [i-w+1, i] (DESIGN.md "Sketch").  Window = [i-w+1, ps-1] u [ps, i]:
+                // suffix minima of the history part come from one backward scan
+                // (s*[u] for j = ps-w+u), prefix minima of the chunk part are kept
+                // while stepping; both carry the multiplicity of the minimum, so
+                // tie scans run only where the minimum really occurs twice.
+                // s*: (x, LDS slot | multiple<<16) of the newest minimum of [j, ps-1]
+                uint64_t sx[SK_CH + 1]; uint32_t sp[SK_CH + 1];
+                {
+                    uint64_t cx = U64MAX; uint32_t cp = 0xffffffffu;
+                    const int q0 = (int)(ps - hbase);
+                    for (int d = 1; d < w - SK_CH; ++d) {          // slot q0 - d (newest first)
+                        const uint64_t x = X[q0 - d];
+                        if (cp == 0xffffffffu || x < cx) { cx = x; cp = (uint32_t)(q0 - d); } else if (x == cx) cp |= 0x10000u;
+                    }
+#pragma unroll
+                    for (int t = 0; t <= SK_CH; ++t) {
+                        const int d = w - SK_CH + t;                 // j = ps - w + (SK_CH - t)
+                        const uint64_t x = X[q0 - d];
+                        if (cp == 0xffffffffu || x < cx) { cx = x; cp = (uint32_t)(q0 - d); } else if (x == cx) cp |= 0x10000u;
+                        sx[SK_CH - t] = cx; sp[SK_CH - t] = cp;
+                    }
+                }
+                // B/C emissions only (at most one per position: recorded as a bit and
+                // the LDS slot of the emitted minimum); ties (A, or T after C) take
+                // the exact path below for the whole wave
+                bool need = false;
+                uint32_t em = 0, eq[SK_CH / 2] = {};
+                {
+                    uint64_t px = U64MAX; uint32_t pp = 0xffffffffu;   // prefix minimum of [ps, i]
+                    uint64_t mxo = sx[0]; int mqo = (int)(sp[0] & 0xffffu);
+#pragma unroll
+                    for (int t = 0; t < SK_CH; ++t) {
+                        const int64_t i = ps + t;
+                        const bool act = i < pe;
+                        const int ii = (int)(i - hbase);
+                        const uint64_t xi = act ? X[ii] : U64MAX;
+                        const int32_t l = act ? (int32_t)(LZ[ii] & 0x7fffu) : 0;
+                        need |= act && l == w + k - 1 && mxo != U64MAX;                 // A (sketch.rs:90-93)
+                        const bool doB = act && xi <= mxo;                              // B (94-96)
+                        const bool doC = act && !doB && mqo == ii - w;                  // C (97-105)
+                        if ((doB && l >= w + k && mxo != U64MAX) || (doC && l >= w + k - 1)) {
+                            em |= 1u << t; eq[t >> 1] |= (uint32_t)mqo << (16 * (t & 1));
+                        }
+                        if (act) {
+                            if (pp == 0xffffffffu || xi < px) { px = xi; pp = (uint32_t)ii; }
+                            else if (xi == px) pp = (uint32_t)ii | 0x10000u;
+                        }
+                        uint64_t mxn; uint32_t mpn;
+                        if (px < sx[t + 1]) { mxn = px; mpn = pp; }
+                        else if (px > sx[t + 1]) { mxn = sx[t + 1]; mpn = sp[t + 1]; }
+                        else { mxn = px; mpn = pp | 0x10000u; }
+                        need |= doC && l >= w + k - 1 && mxn != U64MAX && (mpn & 0x10000u);   // T
+                        mxo = mxn; mqo = (int)(mpn & 0xffffu);
+                    }
+                }
+                if (!any(need)) {
+                    myoff = wave_excl_sum((uint32_t)__popc(em), tot);
+                    uint64_t o = obase + count + myoff;
+#pragma unroll
+                    for (int t = 0; t < SK_CH; ++t) {
+                        if ((em >> t) & 1u) {
+                            const int q = (int)((eq[t >> 1] >> (16 * (t & 1))) & 0xffffu);
+                            if (o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = SK_Y(q); }
+                            ++o;
+                        }
+                    }
+                    fast_done = true;
+                }
+            }
+            if (!fast_done) {
+              myoff = 0; tot = 0;
+              for (int pass = 0; pass < 2; ++pass) {
                 const bool WR = pass == 1;
                 uint64_t o = obase + count + myoff;
                 uint32_t n_em = 0;
-                // newest minimum of the w slots before the chunk (same for every lane count)
+                // newest minimum of the w slots before the chunk (same for every ln count)
                 uint64_t mx = U64MAX; uint32_t my = 0xffffffffu; int64_t mp = ps - w - 1;
                 for (int d = 0; d < w; ++d) {
                     const int64_t p = ps - w + d;
@@ -300,25 +434,16 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                     const uint64_t ix_x = act ? X[ii] : U64MAX;
                     const uint32_t ix_y = act ? SK_Y(ii) : 0xffffffffu;
                     const int32_t l = act ? (int32_t)(LZ[ii] & 0x7fffu) : 0;
-                    // A: first window (sketch.rs:90-93)
                     const bool doA = act && l == w + k - 1 && mx != U64MAX;
                     if (any(doA)) {
                         for (int d = 1; d < w; ++d) {
                             const int q = ii - w + d;
-                            if (doA && X[q] == mx && SK_Y(q) != my) {
-                                if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = SK_Y(q); }
-                                ++o; ++n_em;
-                            }
+                            if (doA && X[q] == mx && SK_Y(q) != my) SK_EMIT(X[q], SK_Y(q));
                         }
                     }
-                    // B: new minimum (sketch.rs:94-96)
                     const bool doB = act && ix_x <= mx;
-                    // C: the minimum's slot is overwritten (sketch.rs:97-105)
                     const bool doC = act && !doB && mp == i - w;
-                    if ((doB && l >= w + k && mx != U64MAX) || (doC && l >= w + k - 1)) {
-                        if (WR && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
-                        ++o; ++n_em;
-                    }
+                    if ((doB && l >= w + k && mx != U64MAX) || (doC && l >= w + k - 1)) SK_EMIT(mx, my);
                     if (doB) { mx = ix_x; my = ix_y; mp = i; }
                     if (any(doC)) {
                         uint64_t nx = U64MAX; uint32_t ny = 0; int64_t np = mp;
@@ -332,23 +457,26 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                         if (any(doT)) {
                             for (int d = 1; d <= w; ++d) {
                                 const int q = ii - w + d;
-                                if (doT && mx == X[q] && my != SK_Y(q)) {
-                                    if (WR && o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = SK_Y(q); }
-                                    ++o; ++n_em;
-                                }
+                                if (doT && mx == X[q] && my != SK_Y(q)) SK_EMIT(X[q], SK_Y(q));
                             }
                         }
                     }
                 }
                 if (!WR) myoff = wave_excl_sum(n_em, tot);
+              }
             }
+#undef SK_EMIT
             count += tot;
+            SK_PT(3);
+            // ---- next tile: its halo = this tile's chunks 60-63; prefetched bases
+            halo = (uint32_t)__shfl((int)own, (ln + 60) & 63, 64);
+            code16 = code16n; valid8 = valid8n;
             // ---- move the last w slots to the history area
             wave_lds_sync();
             if (t0 + SK_TS < L) {
                 // source [TS, TS+w) and destination [0, w) never overlap (w < 256 <= TS)
                 for (int b0 = 0; b0 < w; b0 += 64) {
-                    const int t = b0 + lane;
+                    const int t = b0 + ln;
                     if (t < w) { X[t] = X[SK_TS + t]; LZ[t] = LZ[SK_TS + t]; }
                 }
             }
@@ -374,6 +502,13 @@ __global__ __launch_bounds__(256) void k_sketch(SketchArgs a) {
                 if (obase + count > oend) atomicOr(a.overflow, 1);
             }
         }
+        SK_PT(4);
+        if (a.prof && lane == 0) {
+            for (int q = 0; q < 5; ++q) a.prof[(uint64_t)r * 8 + q] = pt[q];
+            a.prof[(uint64_t)r * 8 + 5] = (uint64_t)L;
+            a.prof[(uint64_t)r * 8 + 6] = wall_clock64();
+        }
+#undef SK_PT
 #undef SK_Y
         wave_lds_sync();
     }
@@ -683,6 +818,8 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
     if (base + A0 > a.cap_keys) { if (threadIdx.x == 0) CK(base + A0, a.cap_keys); return; }
 #endif
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+#define SORT_STAMP(ph) do { if (a.prof && tid == 0) a.prof[(uint64_t)r * 8 + (ph)] = wall_clock64(); } while (0)
+    SORT_STAMP(0);
     const uint32_t qb = a.qb, gsh = a.qb + a.rb;
     const uint64_t rmask = (1ULL << a.rb) - 1;
     uint64_t* K = a.keys + base;
@@ -750,6 +887,7 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
         __syncthreads();
     }
     if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
+    SORT_STAMP(1);
     __syncthreads();                                   // the bitmaps are dead from here
     for (int t = tid; t < RS_MAXP * RS_ND; t += 1024) (&hist[0][0])[t] = 0;
     // bits of (group, rpos) that vary, and all digit histograms in one pass
@@ -772,6 +910,7 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
             if ((vary >> (RS_DB * k)) & dmask) atomicAdd(&hist[k][(uint32_t)(h >> (RS_DB * k)) & (uint32_t)dmask], 1u);
     });
     __syncthreads();
+    SORT_STAMP(2);
     if (tid < npass) {
         uint32_t run = 0;
         for (int d = 0; d < RS_ND; ++d) { const uint32_t c = hist[tid][d]; hist[tid][d] = run; run += c; }
@@ -836,6 +975,7 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
         uint64_t* t = src; src = dst; dst = t;
         __syncthreads();
     }
+    SORT_STAMP(3);
     // sorted by (group, rpos) in src; order runs of equal (group, rpos) by the full key
     for (uint32_t i = tid; i < A; i += 1024) {
         const uint64_t h = src[i] >> qb;
@@ -852,7 +992,10 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
         }
     }
     __syncthreads();
+    SORT_STAMP(4);
     if (src != K) block_pass8(src, A, [&](uint32_t i, uint64_t x) { K[i] = x; });
+    if (a.prof && tid == 0) { a.prof[(uint64_t)r * 8 + 5] = wall_clock64(); a.prof[(uint64_t)r * 8 + 6] = A0; a.prof[(uint64_t)r * 8 + 7] = ((uint64_t)npass << 32) | A; }
+#undef SORT_STAMP
 }
 
 // ============================================================================
