@@ -139,7 +139,9 @@ int mm2g_batch_sketch(mm2g_ctx* ctx, int w, int k, uint32_t rid, uint64_t* out_o
                       uint64_t cap);
 /* After mm2g_batch_map with debug enabled: the sorted anchors of read r
  * (build_anchors_filtered, src/seeds.rs:42-60) as (x, y) pairs, and the DP
- * arrays f/pprev of the final chain_dp_all pass (src/lchain.rs:59-91). */
+ * arrays f/pprev of the final chain_dp_all pass (src/lchain.rs:59-91).
+ * With debug off, mm2g_debug_anchors returns the sorted anchors the DP ran on
+ * (those kept by the sort's singleton filter). */
 int mm2g_ctx_set_debug(mm2g_ctx* ctx, int on);
 int64_t mm2g_debug_anchors(mm2g_ctx* ctx, uint32_t r, uint64_t* xy, int64_t cap);
 int64_t mm2g_debug_dp(mm2g_ctx* ctx, uint32_t r, int32_t* f, int32_t* pprev, int64_t cap);

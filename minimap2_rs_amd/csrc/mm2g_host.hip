@@ -159,7 +159,15 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
         t_lo = std::min(t_lo, p[0]); t_hi = std::max(t_hi, p[5]);
     }
     if (!m) return;
-    fprintf(stderr, "[sort_prof] reads=%u A0=%.0f A=%.0f npass=%.2f us/read: filter=%.1f hist=%.1f radix=%.1f tiefix=%.1f copy=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
+    {   // quantiles of the per-read anchor counts before / after the singleton filter
+        std::vector<uint32_t> q0, q2;
+        for (uint32_t r = 0; r < n; ++r) { const uint64_t* p = &h[(size_t)r * 8]; if (p[5]) { q0.push_back((uint32_t)p[6]); q2.push_back((uint32_t)p[7]); } }
+        std::sort(q0.begin(), q0.end()); std::sort(q2.begin(), q2.end());
+        auto Q = [](const std::vector<uint32_t>& v, double f) { return v[std::min(v.size() - 1, (size_t)(f * v.size()))]; };
+        fprintf(stderr, "[sort_prof] A0 q10/50/90/99/max=%u/%u/%u/%u/%u  A q10/50/90/99/max=%u/%u/%u/%u/%u\n",
+                Q(q0, .1), Q(q0, .5), Q(q0, .9), Q(q0, .99), q0.back(), Q(q2, .1), Q(q2, .5), Q(q2, .9), Q(q2, .99), q2.back());
+    }
+    fprintf(stderr, "[sort_prof] reads=%u A0=%.0f A=%.0f nbig=%.2f us/read: p1-2=%.1f p3=%.1f p4a=%.1f p4b=%.1f tail=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
             m, a0 / m, a2 / m, np / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
             tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
 }
@@ -329,13 +337,16 @@ int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
     LCHK(launch_ix_build(k_, o_, n_, nk, tab, l2, c->stream));
     // singleton-filter cells: per group (fwd, rev) a guard cell, ceil(len / 2^CELL_SHIFT) cells, a guard cell
     {
-        std::vector<uint32_t> goff(2 * (size_t)H.n_seq + 1);
+        std::vector<uint32_t> goff(2 * (size_t)H.n_seq + 2);
         uint64_t run = 0;
         for (uint32_t g = 0; g < 2 * H.n_seq; ++g) {
             goff[g] = (uint32_t)std::min<uint64_t>(run, 0xffffffffu);
             run += ((uint64_t)H.seq[g % H.n_seq].len >> CELL_SHIFT) + 3;
         }
+        // the Q19 pseudo-group 2 * n_seq (odd rids, both strands, rpos = pos)
         goff[2 * H.n_seq] = (uint32_t)std::min<uint64_t>(run, 0xffffffffu);
+        run += ((uint64_t)H.max_len >> CELL_SHIFT) + 3;
+        goff[2 * H.n_seq + 1] = (uint32_t)std::min<uint64_t>(run, 0xffffffffu);
         // two bitmaps must fit the LDS budget of k_sort_read next to its static arrays
         c->dix->cells = (run <= (uint64_t)320 * 1024) ? (uint32_t)run : 0u;
         uint32_t* dg;
@@ -538,10 +549,11 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->smax, uint64_t, n, smax);
     // the singleton filter is off in debug mode (full anchor/DP arrays for the parity tests)
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
-                (c->debug || getenv("MM2G_NO_FILTER")) ? 0u : c->dix->cells, cnt2, smax, 4096u, nullptr};
+                (c->debug || getenv("MM2G_NO_FILTER")) ? 0u : c->dix->cells, cnt2, smax, 4096u, nullptr, 0u, SEG_THREAD, nullptr};
     uint64_t* sprof = nullptr;
     if (getenv("MM2G_SORT_PROF")) { HIPCHK(hipMalloc(&sprof, (size_t)n * 64)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 64, c->stream)); so.prof = sprof; }
     if (const char* e = getenv("MM2G_SORT_SMALL")) so.small_max = std::min<uint32_t>((uint32_t)atoi(e), 4096u);   // tests
+    if (const char* e = getenv("MM2G_SEG_SMALL")) so.seg_small = std::max(1u, std::min<uint32_t>((uint32_t)atoi(e), SEG_THREAD));   // tests
     {
         ProfScope ps(c, "sort_small");
         LCHK(launch_sort_read(0, so, c->stream));
@@ -551,6 +563,9 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         LCHK(launch_sort_read(1, so, c->stream));
     }
     if (sprof) dump_sort_prof(c, sprof, n);
+    // the sorted anchors are in the tmp buffer: swap the roles for everything downstream
+    std::swap(c->keys.p, c->keys_tmp.p); std::swap(c->keys.cap, c->keys_tmp.cap);
+    std::swap(keys, ktmp);
     // 5. chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
     build_lut(c, o->k, lut_need);
     int16_t* lut; uint32_t* work;
@@ -775,7 +790,12 @@ int64_t mm2g_debug_anchors(mm2g_ctx* c, uint32_t r, uint64_t* xy, int64_t cap) {
     HIPCHK(hipSetDevice(c->device));
     uint64_t off[2];
     HIPCHK(hipMemcpy(off, (uint64_t*)c->a_off.p + r, 16, hipMemcpyDeviceToHost));
-    const int64_t A = (int64_t)(off[1] - off[0]);
+    int64_t A = (int64_t)(off[1] - off[0]);
+    if (!c->debug) {   // production sort: only the anchors kept by the singleton filter are sorted
+        uint32_t kept = 0;
+        HIPCHK(hipMemcpy(&kept, (uint32_t*)c->cnt2.p + r, 4, hipMemcpyDeviceToHost));
+        A = kept;
+    }
     if (!xy) return A;
     std::vector<uint64_t> k((size_t)A);
     if (A) HIPCHK(hipMemcpy(k.data(), (uint64_t*)c->keys.p + off[0], A * 8, hipMemcpyDeviceToHost));

@@ -108,6 +108,7 @@ struct SeedArgs {
     ReadOut* out;                         // m_kept
 };
 // per-read anchor sort + singleton filter (k_sort_small / k_sort_read)
+constexpr uint32_t SEG_THREAD = 1024;   // cell segments up to this length: one thread per anchor (default seg_small)
 constexpr int CELL_SHIFT = 15;   // 32 kb reference cells (>= every max_dist_x the filter is used with)
 struct SortArgs {
     uint32_t n;
@@ -115,12 +116,15 @@ struct SortArgs {
     uint64_t* keys; uint64_t* tmp;
     uint32_t qb, rb, n_seq;
     uint64_t cap_keys;
-    const uint32_t* goff;   // per group: first cell (guard cell before and after every group)
+    const uint32_t* goff;   // per group incl. the Q19 pseudo-group 2*n_seq: first cell (guard cell on either side); [2*n_seq+1] = cells
     uint32_t cells;         // 0 = singleton filter off
     uint32_t* cnt2;         // per read: anchors kept (sorted at keys[a_off[r] ..])
     uint64_t* smax;         // per read: 1 + largest dropped (singleton) key, 0 = none
     uint32_t small_max;     // reads with more anchors go to k_sort_read (LDS bitonic below)
     uint64_t* prof;         // MM2G_SORT_PROF: per read 8 wall-clock stamps of k_sort_read's phases (else null)
+    uint32_t lds_words;     // dynamic LDS of k_sort_read (set by launch_sort_read)
+    uint32_t seg_small;     // cell segments up to this length (<= 1024) are ranked one thread per anchor
+    uint32_t* meta;         // per anchor scratch (the DP's f buffer): kept-cell rank of each scattered key
 };
 struct ChainArgs {
     uint32_t n;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <limits.h>
+#include <algorithm>
 #include "mm2g_internal.h"
 
 using namespace mm2g;
@@ -746,6 +747,7 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     const uint32_t A = (uint32_t)(a.a_off[r + 1] - base);
     if (A > a.small_max) return;
     if (threadIdx.x == 0) { a.cnt2[r] = A; a.smax[r] = 0; }   // no singleton filter for small reads
+    if (A == 1 && threadIdx.x == 0) a.tmp[CK(base, a.cap_keys)] = a.keys[CK(base, a.cap_keys)];
     if (A <= 1) return;
     uint32_t np = 1; while (np < A) np <<= 1;
     uint64_t* K = a.keys;
@@ -764,131 +766,135 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
             __syncthreads();
         }
     }
-    for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) K[CK(base + i, a.cap_keys)] = s[i];
+    for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) a.tmp[CK(base + i, a.cap_keys)] = s[i];   // sorted keys live in tmp
 }
 
-// ---- per-read LSD radix sort on (group, rpos), then qpos for ties.
-// The query bits are left out of the radix passes (two fewer passes for
-// 10 kb reads); runs of equal (group, rpos) — rare — are ordered by qpos
-// afterwards, which gives exactly the (x, y) order of src/seeds.rs:58.
-// All digit histograms come from one read pass; a pass processes chunks of
-// RS_CH keys: per-wave digit counts -> per-(wave, digit) offsets -> stable
-// scatter (items in order, lanes ranked by ballot matching).
-constexpr int RS_ITEMS = 8;
+// ---- per-read sort of the large reads (A0 > small_max): cell buckets.
+//
+// Keys are (group, rpos, q).  The reference coordinate space of every group
+// (forward / reverse per contig, plus the Q19 pseudo-group) is cut into 32 kb
+// cells (goff: first cell of each group, a guard cell on either side).
+//   P1  two LDS bitmaps over all cells: seen, seen twice.
+//   KC  kept cells: seen and (seen twice or a neighbouring cell seen).  An
+//       anchor in any other cell has no other anchor of its read in the same
+//       group within 32 kb >= max_dist_x (both DP passes), so it is a
+//       one-anchor segment of chain_dp_all (f = span, pprev = -1) and affects
+//       the result only through the "last argmax f" tie-break, which then picks
+//       the largest such key (k_chain_fin gets 1 + the largest dropped key).
+//       Ranks of the kept cells come from a word prefix of popcounts.
+//   P2  per kept cell an anchor count (u16 pairs in LDS), scanned to offsets.
+//   P3  scatter of the kept anchors to T, grouped by cell in key order.
+//   P4  every cell segment is sorted on its own (cells are ordered, so the
+//       concatenation is the full order of src/seeds.rs:58):
+//       <= 1024 anchors: one thread per anchor counts its rank inside the
+//       segment (its cell rank, written beside T in P3, gives the bounds),
+//       over windows of T staged in LDS and cut at segment ends;
+//       larger: block-wide rank count over the LDS-staged segment, or the LSD
+//       radix below for segments beyond 2048 anchors.
+// Reads that do not fit (A0 > 65535, too many kept cells for the LDS budget,
+// or no cell table) take the radix path over the whole read.
+//
+// LSD radix (fallback): 9-bit digits over the varying bits of (group, rpos);
+// runs of equal (group, rpos) are then ordered by the full key.
+constexpr int RS_ITEMS = 4;
 constexpr int RS_CH = 1024 * RS_ITEMS;
 constexpr int RS_DB = 9;                 // digit bits
 constexpr int RS_ND = 1 << RS_DB;
 constexpr int RS_MAXP = 5;               // digit passes: (group, rpos) has at most 7 + 31 bits
+constexpr uint32_t SEG_TINY = 16;        // segments up to this length: ranked by a scan
+constexpr uint32_t SEG_RANK = 2048;      // up to this: block-wide rank count; beyond: radix
+constexpr int BIG_MAX = 128;             // larger segments listed per read (more: radix over the read)
+constexpr int GOFF_LDS = 256;            // group offsets staged in LDS when 2 * n_seq + 2 fits
+constexpr int SORT_LDS = 150 * 1024;     // dynamic LDS of k_sort_read (one workgroup per CU)
 
-// Singleton filter (before sorting): an anchor alone in its 32 kb reference
-// cell, with both neighbouring cells of its group empty, has no other anchor of
-// its read within max_dist_x (<= 20000 in both DP passes) in the same group, so
-// it forms a one-anchor segment in chain_dp_all (f = span, pprev = -1) and
-// affects the result only through the "last argmax f" tie-break, which then
-// picks the largest key of the read.  Such anchors are dropped from the sort
-// and the DP; the largest dropped key is kept (k_chain_fin).  Two LDS bitmaps
-// (cell seen / seen twice) per read; Q19 anchors are always kept.
 // 8 independent loads per thread, then fn(i, x) for each (i < n): hides HBM
 // latency in the block-wide passes of k_sort_read
-template <typename F>
+template <int U = 8, typename F>
 DEVI void block_pass8(const uint64_t* src, uint32_t n, F fn) {
-    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * 8) {
-        uint64_t x[8];
+    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * U) {
+        uint64_t x[U];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; x[u] = i < n ? src[i] : 0; }
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; x[u] = i < n ? src[i] : 0; }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; if (i < n) fn(i, x[u]); }
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; if (i < n) fn(i, x[u]); }
     }
 }
 
-__global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
-    __shared__ uint64_t red[32];
-    __shared__ uint32_t kept;
-    // one dynamic region: the filter's two cell bitmaps, then the radix histograms
-    extern __shared__ uint32_t dyn[];
-    uint32_t (*hist)[RS_ND] = (uint32_t (*)[RS_ND])dyn;                 // RS_MAXP x RS_ND
-    uint32_t (*wh)[RS_ND] = (uint32_t (*)[RS_ND])(dyn + RS_MAXP * RS_ND);  // 16 x RS_ND
-    uint32_t* bm = dyn;                                                   // 2 x ceil(cells / 32) words
-    const uint32_t r = blockIdx.x;
-    if (r >= a.n) return;
-    const uint64_t base = a.a_off[r];
-    const uint32_t A0 = (uint32_t)(a.a_off[r + 1] - base);
-    if (A0 <= a.small_max) return;    // k_sort_small
-#ifdef MM2G_CHECKED
-    if (base + A0 > a.cap_keys) { if (threadIdx.x == 0) CK(base + A0, a.cap_keys); return; }
-#endif
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-#define SORT_STAMP(ph) do { if (a.prof && tid == 0) a.prof[(uint64_t)r * 8 + (ph)] = wall_clock64(); } while (0)
-    SORT_STAMP(0);
-    const uint32_t qb = a.qb, gsh = a.qb + a.rb;
-    const uint64_t rmask = (1ULL << a.rb) - 1;
-    uint64_t* K = a.keys + base;
-    uint64_t* T = a.tmp + base;
-    uint64_t* src = K;
-    uint64_t* dst = T;
-    uint32_t A = A0;
-    if (tid == 0) kept = 0;
-    const uint32_t nw = (a.cells + 31) >> 5;
-    uint32_t* B1 = bm;
-    uint32_t* B2 = bm + nw;
-    const bool filt = a.cells != 0;
-    uint64_t smx = 0;     // 1 + largest dropped key
-    if (filt) {
-        for (uint32_t i = tid; i < 2 * nw; i += 1024) bm[i] = 0;
-        __syncthreads();
-        block_pass8(K, A0, [&](uint32_t, uint64_t x) {
-            const uint32_t g = (uint32_t)(x >> gsh);
-            if (g < 2u * a.n_seq) {
-                const uint32_t c = a.goff[g] + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
-                const uint32_t bit = 1u << (c & 31);
-                if (atomicOr(&B1[c >> 5], bit) & bit) atomicOr(&B2[c >> 5], bit);
-            }
-        });
-        __syncthreads();
-        // keep non-singletons (compacted into T, order irrelevant: sorted below)
-        for (uint32_t j0 = 0; j0 < A0; j0 += 1024 * 8) {
-          uint64_t xs[8];
+// bitonic sort of one key per lane across the wave, carrying a payload
+DEVI void wave_bitonic64(uint64_t& x, uint32_t& p) {
+    const int lane = lane_id();
 #pragma unroll
-          for (int u = 0; u < 8; ++u) { const uint32_t i = j0 + (uint32_t)u * 1024 + tid; xs[u] = i < A0 ? K[i] : 0; }
+    for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const uint32_t i = j0 + (uint32_t)u * 1024 + tid;
-            bool keep = false;
-            uint64_t x = 0;
-            if (i < A0) {
-                x = xs[u];
-                const uint32_t g = (uint32_t)(x >> gsh);
-                keep = true;
-                if (g < 2u * a.n_seq) {
-                    const uint32_t c = a.goff[g] + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
-                    const bool twice = (B2[c >> 5] >> (c & 31)) & 1u;
-                    const bool left = (B1[(c - 1) >> 5] >> ((c - 1) & 31)) & 1u;
-                    const bool right = (B1[(c + 1) >> 5] >> ((c + 1) & 31)) & 1u;
-                    keep = twice || left || right;
-                }
-                if (!keep) smx = x + 1 > smx ? x + 1 : smx;
-            }
-            const uint64_t km = ballot(keep);
-            uint32_t wbase = 0;
-            if (lane == 0 && km) wbase = atomicAdd(&kept, (uint32_t)__popcll(km));
-            wbase = (uint32_t)__shfl((int)wbase, 0, 64);
-            if (keep) T[CK(wbase + (uint32_t)__popcll(km & lanemask_lt()), A0)] = x;
-          }
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t yl = (uint32_t)__shfl_xor((int)(uint32_t)x, j, 64);
+            const uint32_t yh = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), j, 64);
+            const uint32_t q = (uint32_t)__shfl_xor((int)p, j, 64);
+            const uint64_t y = ((uint64_t)yh << 32) | yl;
+            const bool up = (lane & k) == 0, low = (lane & j) == 0;
+            if ((low == up) ? (y < x) : (y > x)) { x = y; p = q; }
         }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(smx, d, 64); smx = o > smx ? o : smx; }
-        __syncthreads();
-        if (lane == 0) red[wv] = smx;
-        __syncthreads();
-        smx = 0;
-        for (int t = 0; t < 16; ++t) smx = red[t] > smx ? red[t] : smx;
-        A = kept;
-        src = T; dst = K;
-        __syncthreads();
     }
-    if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
-    SORT_STAMP(1);
-    __syncthreads();                                   // the bitmaps are dead from here
+}
+
+// number of keys in the sorted S[lo, hi) below x (or <= x when incl)
+DEVI uint32_t count_below(const uint64_t* S, uint32_t lo, uint32_t hi, uint64_t x, bool incl) {
+    uint32_t b = lo, n = hi - lo;
+    while (n) {
+        const uint32_t h = n >> 1;
+        const uint64_t y = S[b + h];
+        if (y < x || (incl && y == x)) { b += h + 1; n -= h + 1; } else n = h;
+    }
+    return b - lo;
+}
+
+// as block_pass8, but fn(i, x, valid) runs on every lane (block-uniform trip
+// count) so that fn may ballot / shuffle
+template <int U = 4, typename F>
+DEVI void block_pass_u(const uint64_t* src, uint32_t n, F fn) {
+    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * U) {
+        uint64_t x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; x[u] = i < n ? src[i] : 0; }
+#pragma unroll
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; fn(i, x[u], i < n); }
+    }
+}
+
+// exclusive scan over a 1024-thread block (all threads call it: it holds barriers)
+DEVI uint32_t block_excl_sum(uint32_t v, uint32_t& total, uint32_t* sc) {
+    const int lane = lane_id(), wv = wave_id();
+    uint32_t wt;
+    const uint32_t ex = wave_excl_sum(v, wt);
+    __syncthreads();
+    if (lane == 0) sc[wv] = wt;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) { const uint32_t q = sc[t]; pre += t < wv ? q : 0u; tot += q; }
+    total = tot;
+    return pre + ex;
+}
+
+DEVI uint64_t block_max64(uint64_t v, uint64_t* red) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(v, d, 64); v = o > v ? o : v; }
+    __syncthreads();
+    if (lane_id() == 0) red[wave_id()] = v;
+    __syncthreads();
+    v = 0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) v = red[t] > v ? red[t] : v;
+    return v;
+}
+
+// LSD radix of [src, src+A) by (group, rpos), ties by the full key; the sorted
+// keys end in `out` (== src or dst).  dyn: (RS_MAXP + 16) * RS_ND words.
+DEVI void radix_range(uint64_t* src, uint64_t* dst, uint64_t* out, uint32_t A, uint32_t qb, uint32_t* dyn, uint64_t* red) {
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    uint32_t (*hist)[RS_ND] = (uint32_t (*)[RS_ND])dyn;                   // RS_MAXP x RS_ND
+    uint32_t (*wh)[RS_ND] = (uint32_t (*)[RS_ND])(dyn + RS_MAXP * RS_ND);  // 16 x RS_ND
+    __syncthreads();
     for (int t = tid; t < RS_MAXP * RS_ND; t += 1024) (&hist[0][0])[t] = 0;
     // bits of (group, rpos) that vary, and all digit histograms in one pass
     uint64_t vo = 0, va = U64MAX;
@@ -910,7 +916,6 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
             if ((vary >> (RS_DB * k)) & dmask) atomicAdd(&hist[k][(uint32_t)(h >> (RS_DB * k)) & (uint32_t)dmask], 1u);
     });
     __syncthreads();
-    SORT_STAMP(2);
     if (tid < npass) {
         uint32_t run = 0;
         for (int d = 0; d < RS_ND; ++d) { const uint32_t c = hist[tid][d]; hist[tid][d] = run; run += c; }
@@ -963,7 +968,7 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
                 }
                 const uint64_t lt = peers & lanemask_lt();
                 const uint32_t pos = wh[wv][d] + (uint32_t)__popcll(lt);
-                if (valid) dst[CK(pos, A0)] = x[it];
+                if (valid) dst[CK(pos, A)] = x[it];
                 wave_lds_sync();
                 if (valid && lt == 0) wh[wv][d] += (uint32_t)__popcll(peers);
                 wave_lds_sync();
@@ -975,7 +980,6 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
         uint64_t* t = src; src = dst; dst = t;
         __syncthreads();
     }
-    SORT_STAMP(3);
     // sorted by (group, rpos) in src; order runs of equal (group, rpos) by the full key
     for (uint32_t i = tid; i < A; i += 1024) {
         const uint64_t h = src[i] >> qb;
@@ -992,9 +996,298 @@ __global__ __launch_bounds__(1024, 8) void k_sort_read(SortArgs a) {
         }
     }
     __syncthreads();
+    if (src != out) block_pass8(src, A, [&](uint32_t i, uint64_t x) { out[i] = x; });
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
+    __shared__ uint64_t red[32];
+    __shared__ uint32_t s_sc[16], s_kept, s_nbig;
+    __shared__ uint2 s_big[BIG_MAX];
+    __shared__ uint32_t s_goff[GOFF_LDS];
+    extern __shared__ uint64_t dyn64[];
+    uint32_t* dyn = (uint32_t*)dyn64;
+    const uint32_t r = blockIdx.x;
+    if (r >= a.n) return;
+    const uint64_t base = a.a_off[r];
+    const uint32_t A0 = (uint32_t)(a.a_off[r + 1] - base);
+    if (A0 <= a.small_max) return;    // k_sort_small
+#ifdef MM2G_CHECKED
+    if (base + A0 > a.cap_keys) { if (threadIdx.x == 0) CK(base + A0, a.cap_keys); return; }
+#endif
+    const int tid = threadIdx.x, lane = lane_id();
+#define SORT_STAMP(ph) do { if (a.prof && tid == 0) a.prof[(uint64_t)r * 8 + (ph)] = wall_clock64(); } while (0)
+    SORT_STAMP(0);
+    const uint32_t qb = a.qb, gsh = a.qb + a.rb;
+    const uint64_t rmask = (1ULL << a.rb) - 1;
+    uint64_t* K = a.keys + base;      // unsorted anchors (seed_write); scratch once read for the last time
+    uint64_t* O = a.tmp + base;       // sorted output
+    const bool filt = a.cells != 0;
+    const uint32_t ng = 2u * a.n_seq + 2u;
+    const uint32_t* goff = a.goff;
+    if (filt && ng <= (uint32_t)GOFF_LDS) {
+        for (uint32_t i = tid; i < ng; i += 1024) s_goff[i] = a.goff[i];
+        goff = s_goff;
+    }
+    if (tid == 0) { s_nbig = 0; s_kept = 0; }
+    __syncthreads();
+    // cell of a key (every group incl. the Q19 pseudo-group 2 * n_seq has cells)
+    auto cell_of = [&](uint64_t x) -> uint32_t {
+        return goff[(uint32_t)(x >> gsh)] + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
+    };
+    const uint32_t nw = (a.cells + 31) >> 5;
+    const uint32_t LW = a.lds_words;
+    uint32_t* B1 = dyn;
+    uint32_t* B2 = dyn + nw;
+    bool legacy = !filt || A0 > 65535u;
+    if (!legacy) {
+        // ---- P1: seen / seen-twice bitmaps
+        for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
+        __syncthreads();
+        block_pass8<8>(K, A0, [&](uint32_t, uint64_t x) {
+            const uint32_t c = cell_of(x), w = c >> 5, bit = 1u << (c & 31);
+            bool seen = (B1[w] & bit) != 0;
+            if (!seen) seen = (atomicOr(&B1[w], bit) & bit) != 0;
+            if (seen && !(B2[w] & bit)) atomicOr(&B2[w], bit);
+        });
+        __syncthreads();
+        // ---- KC (in place of B2) and the word prefix of its popcounts (in place of B1)
+        const uint32_t per = (nw + 1023) >> 10;
+        const uint32_t wa = min(nw, (uint32_t)tid * per), wb = min(nw, wa + per);
+        uint32_t loc = 0;
+        for (uint32_t w = wa; w < wb; ++w) {
+            const uint32_t b1 = B1[w];
+            const uint32_t nb = (b1 << 1) | (w ? B1[w - 1] >> 31 : 0u) | (b1 >> 1) | (w + 1 < nw ? B1[w + 1] << 31 : 0u);
+            const uint32_t kc = b1 & (B2[w] | nb);
+            B2[w] = kc;
+            loc += (uint32_t)__popc(kc);
+        }
+        uint32_t nkc;
+        uint32_t run = block_excl_sum(loc, nkc, s_sc);      // its barriers end the B1 reads
+        for (uint32_t w = wa; w < wb; ++w) { B1[w] = run; run += (uint32_t)__popc(B2[w]); }
+        const uint32_t cw = (nkc + 1) >> 1;                  // u16 counts, two per word
+        const uint32_t wofs = (2 * nw + cw + 1) & ~1u;       // 8-byte aligned window area
+        const uint32_t W = wofs < LW ? (LW - wofs) >> 1 : 0u;   // keys per window
+        legacy = W < SEG_RANK;
+        if (!legacy) {
+            uint32_t* C = dyn + 2 * nw;
+            uint64_t* S = dyn64 + (wofs >> 1);
+            for (uint32_t i = tid; i < cw; i += 1024) C[i] = 0;
+            __syncthreads();
+            auto rank_of = [&](uint32_t c, bool& kept) -> uint32_t {
+                const uint32_t w = c >> 5, b = c & 31, kw = B2[w];
+                kept = (kw >> b) & 1u;
+                return B1[w] + (uint32_t)__popc(kw & ((1u << b) - 1u));
+            };
+            auto c16 = [&](uint32_t rk) -> uint32_t { return (C[rk >> 1] >> ((rk & 1) << 4)) & 0xffffu; };
+            // ---- P2: counts per kept cell; the largest dropped key
+            uint64_t smx = 0;
+            block_pass8<8>(K, A0, [&](uint32_t, uint64_t x) {
+                bool kept;
+                const uint32_t rk = rank_of(cell_of(x), kept);
+                if (kept) atomicAdd(&C[rk >> 1], 1u << ((rk & 1) << 4));
+                else smx = x + 1 > smx ? x + 1 : smx;
+            });
+            smx = block_max64(smx, red);
+            // exclusive scan of the u16 counts, in place (offsets < A0 <= 65535)
+            const uint32_t per2 = (cw + 1023) >> 10;
+            const uint32_t ca = min(cw, (uint32_t)tid * per2), cb = min(cw, ca + per2);
+            uint32_t l2 = 0;
+            for (uint32_t i = ca; i < cb; ++i) { const uint32_t v = C[i]; l2 += (v & 0xffffu) + (v >> 16); }
+            uint32_t A;
+            uint32_t o = block_excl_sum(l2, A, s_sc);
+            for (uint32_t i = ca; i < cb; ++i) {
+                const uint32_t v = C[i], lo = v & 0xffffu;
+                C[i] = o | ((o + lo) << 16);
+                o += lo + (v >> 16);
+            }
+            if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
+            __syncthreads();
+            SORT_STAMP(1);
+            // ---- P3/P4: windows of whole kept cells (<= W keys), each gathered from K
+            // into LDS by cell (C turns from start into end offsets as cells are
+            // filled), chunk-sorted and ranked per cell segment into O.
+            auto offx = [&](uint32_t rk) -> uint32_t { return rk < nkc ? c16(rk) : A; };   // start of an unfilled cell
+            uint32_t ra = 0;
+            while (ra < nkc) {
+                const uint32_t oa = c16(ra);
+                uint32_t lo = ra + 1, hi = nkc;                       // last rb with offx(rb) <= oa + W
+                while (lo < hi) { const uint32_t mid = (lo + hi + 1) >> 1; if (offx(mid) <= oa + W) lo = mid; else hi = mid - 1; }
+                const uint32_t rb = lo;
+                const uint32_t ob = offx(rb);
+                if (ob > oa + W) {
+                    // cell ra alone exceeds the window: gather it into O unsorted (P4b sorts it)
+                    __syncthreads();
+                    if (tid == 0) s_kept = 0;
+                    __syncthreads();
+                    block_pass_u<8>(K, A0, [&](uint32_t, uint64_t x, bool valid) {
+                        bool kept = false;
+                        const uint32_t rk = valid ? rank_of(cell_of(x), kept) : 0u;
+                        const bool mine = valid && kept && rk == ra;
+                        const uint64_t mb = ballot(mine);
+                        uint32_t wb0 = 0;
+                        if (lane == 0 && mb) wb0 = atomicAdd(&s_kept, (uint32_t)__popcll(mb));
+                        wb0 = (uint32_t)__shfl((int)wb0, 0, 64);
+                        if (mine) O[CK(oa + wb0 + (uint32_t)__popcll(mb & lanemask_lt()), A0)] = x;
+                    });
+                    __syncthreads();
+                    if (tid == 0) {
+                        const uint32_t sh = (ra & 1) << 4;
+                        C[ra >> 1] = (C[ra >> 1] & ~(0xffffu << sh)) | (ob << sh);   // now its end offset
+                        const uint32_t slot = s_nbig++;
+                        if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa, ob);
+                    }
+                    __syncthreads();
+                    ra = ra + 1;
+                    continue;
+                }
+                const uint32_t nwin = ob - oa;
+                __syncthreads();
+                block_pass8<8>(K, A0, [&](uint32_t, uint64_t x) {
+                    bool kept;
+                    const uint32_t rk = rank_of(cell_of(x), kept);
+                    if (kept && rk >= ra && rk < rb) {
+                        const uint32_t sh = (rk & 1) << 4;
+                        const uint32_t pos = ((atomicAdd(&C[rk >> 1], 1u << sh) >> sh) & 0xffffu) - oa;
+                        S[pos] = x;
+                    }
+                });
+                __syncthreads();
+                // segment [s, e) of a key, window-relative (C holds end offsets for ranks < rb)
+                auto seg_of = [&](uint64_t x, uint32_t& s, uint32_t& e) {
+                    bool kept;
+                    const uint32_t rk = rank_of(cell_of(x), kept);
+                    s = (rk ? c16(rk - 1) : 0u) - oa;
+                    e = c16(rk) - oa;
+                };
+                // A: chunks holding a segment longer than SEG_TINY: one wave sorts 64 keys
+                const uint32_t nch = (nwin + 63) >> 6;
+                for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 16) {
+                    const uint32_t i = q * 64 + (uint32_t)lane;
+                    const bool valid = i < nwin;
+                    uint64_t x = valid ? S[i] : U64MAX;
+                    uint32_t s = 0, e = 0;
+                    if (valid) seg_of(x, s, e);
+                    if (!any(valid && e - s > SEG_TINY && e - s <= a.seg_small)) continue;
+                    uint32_t dummy = 0;
+                    wave_bitonic64(x, dummy);
+                    if (valid) S[i] = x;
+                }
+                __syncthreads();
+                // B: ranks inside the segments
+                for (uint32_t i = tid; i < nwin; i += 1024) {
+                    const uint64_t x = S[i];
+                    uint32_t s, e;
+                    seg_of(x, s, e);
+                    const uint32_t L = e - s;
+                    if (L > a.seg_small) {             // P4b; copied unsorted
+                        O[oa + i] = x;
+                        if (i == s) {
+                            const uint32_t slot = atomicAdd(&s_nbig, 1u);
+                            if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s, oa + e);
+                        }
+                        continue;
+                    }
+                    uint32_t rank = 0;
+                    if (L <= SEG_TINY) {
+                        for (uint32_t j = s; j < e; ++j) { const uint64_t y = S[j]; rank += (y < x || (y == x && j < i)) ? 1u : 0u; }
+                    } else {
+                        const uint32_t co = i >> 6;
+                        rank = i - max(s, co << 6);
+                        for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
+                            if (c == co) continue;
+                            rank += count_below(S, max(s, c << 6), min(e, (c << 6) + 64), x, c < co);
+                        }
+                    }
+                    O[oa + s + rank] = x;
+                }
+                __syncthreads();
+                ra = rb;
+            }
+            SORT_STAMP(2);
+            SORT_STAMP(3);
+            // ---- P4b: cells over seg_small, one at a time by the whole block (K is scratch now)
+            const uint32_t nbig = s_nbig;
+            if (nbig > (uint32_t)BIG_MAX) {
+                radix_range(O, K, O, A, qb, dyn, red);
+            } else {
+                for (uint32_t b = 0; b < nbig; ++b) {
+                    const uint2 sg = s_big[b];
+                    const uint32_t L = sg.y - sg.x;
+                    if (L <= SEG_RANK) {
+                        __syncthreads();
+                        block_pass8<4>(O + sg.x, L, [&](uint32_t i, uint64_t x) { dyn64[i] = x; });
+                        __syncthreads();
+                        const uint32_t i0 = (uint32_t)tid, i1 = (uint32_t)tid + 1024;
+                        const uint64_t x0 = i0 < L ? dyn64[i0] : U64MAX, x1 = i1 < L ? dyn64[i1] : U64MAX;
+                        uint32_t r0 = 0, r1 = 0;
+                        if (L > 1024) {
+                            for (uint32_t j = 0; j < L; ++j) {
+                                const uint64_t y = dyn64[j];
+                                r0 += (y < x0 || (y == x0 && j < i0)) ? 1u : 0u;
+                                r1 += (y < x1 || (y == x1 && j < i1)) ? 1u : 0u;
+                            }
+                        } else {
+                            for (uint32_t j = 0; j < L; ++j) { const uint64_t y = dyn64[j]; r0 += (y < x0 || (y == x0 && j < i0)) ? 1u : 0u; }
+                        }
+                        __syncthreads();
+                        if (i0 < L) O[sg.x + r0] = x0;
+                        if (i1 < L) O[sg.x + r1] = x1;
+                    } else {
+                        radix_range(O + sg.x, K + sg.x, O + sg.x, L, qb, dyn, red);
+                    }
+                }
+            }
+            SORT_STAMP(4);
+            if (a.prof && tid == 0) { a.prof[(uint64_t)r * 8 + 5] = wall_clock64(); a.prof[(uint64_t)r * 8 + 6] = A0; a.prof[(uint64_t)r * 8 + 7] = ((uint64_t)nbig << 32) | A; }
+            return;
+        }
+        __syncthreads();
+    }
+    // ---- radix path over the whole read (with the bitmap singleton filter when cells exist)
+    uint64_t* src = K;
+    uint64_t* dst = O;
+    uint32_t A = A0;
+    uint64_t smx = 0;     // 1 + largest dropped key
+    if (filt) {
+        if (tid == 0) s_kept = 0;
+        for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
+        __syncthreads();
+        block_pass8<4>(K, A0, [&](uint32_t, uint64_t x) {
+            const uint32_t c = cell_of(x);
+            const uint32_t bit = 1u << (c & 31);
+            if (atomicOr(&B1[c >> 5], bit) & bit) atomicOr(&B2[c >> 5], bit);
+        });
+        __syncthreads();
+        // keep non-singletons (compacted into O, order irrelevant: sorted below)
+        block_pass_u<4>(K, A0, [&](uint32_t, uint64_t x, bool valid) {
+            bool keep = false;
+            if (valid) {
+                const uint32_t c = cell_of(x);
+                const bool twice = (B2[c >> 5] >> (c & 31)) & 1u;
+                const bool left = (B1[(c - 1) >> 5] >> ((c - 1) & 31)) & 1u;
+                const bool right = (B1[(c + 1) >> 5] >> ((c + 1) & 31)) & 1u;
+                keep = twice || left || right;
+                if (!keep) smx = x + 1 > smx ? x + 1 : smx;
+            }
+            const uint64_t km = ballot(keep);
+            uint32_t wbase = 0;
+            if (lane == 0 && km) wbase = atomicAdd(&s_kept, (uint32_t)__popcll(km));
+            wbase = (uint32_t)__shfl((int)wbase, 0, 64);
+            if (keep) O[CK(wbase + (uint32_t)__popcll(km & lanemask_lt()), A0)] = x;
+        });
+        smx = block_max64(smx, red);
+        A = s_kept;
+        src = O; dst = K;
+        __syncthreads();
+    }
+    if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
+    SORT_STAMP(1);
+    SORT_STAMP(2);
+    radix_range(src, dst, O, A, qb, dyn, red);
+    SORT_STAMP(3);
     SORT_STAMP(4);
-    if (src != K) block_pass8(src, A, [&](uint32_t i, uint64_t x) { K[i] = x; });
-    if (a.prof && tid == 0) { a.prof[(uint64_t)r * 8 + 5] = wall_clock64(); a.prof[(uint64_t)r * 8 + 6] = A0; a.prof[(uint64_t)r * 8 + 7] = ((uint64_t)npass << 32) | A; }
+    if (a.prof && tid == 0) { a.prof[(uint64_t)r * 8 + 5] = wall_clock64(); a.prof[(uint64_t)r * 8 + 6] = A0; a.prof[(uint64_t)r * 8 + 7] = (0xffffULL << 32) | A; }
 #undef SORT_STAMP
 }
 
@@ -1893,8 +2186,12 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
     if (a.n == 0) return 0;
     if (stage == 0) hipLaunchKernelGGL(k_sort_small, dim3(a.n), dim3(256), 0, st, a);
     else {
+        // one workgroup per CU: 160 KiB LDS less the static arrays
         const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4, hb = (size_t)(RS_MAXP + 16) * RS_ND * 4;
-        hipLaunchKernelGGL(k_sort_read, dim3(a.n), dim3(1024), bmb > hb ? bmb : hb, st, a);
+        size_t lds = std::max<size_t>({(size_t)SORT_LDS, bmb, hb});
+        SortArgs b = a;
+        b.lds_words = (uint32_t)(lds / 4);
+        hipLaunchKernelGGL(k_sort_read, dim3(a.n), dim3(1024), lds, st, b);
     }
     LAUNCH_CHECK();
     return 0;

@@ -316,3 +316,54 @@ def test_cli_align_gpu(small_world, tmp_path):
     g = subprocess.run([mm2rs, "align", mmi, reads], check=True, capture_output=True, text=True).stdout
     c = subprocess.run([cpu, "align", ref, reads], check=True, capture_output=True, text=True).stdout
     assert g == c and g.count("\n") > 50
+
+
+def _singleton_keep(a: np.ndarray) -> np.ndarray:
+    """The sort's singleton filter restated on (x, y) anchors: keep an anchor
+    iff its 32 kb cell of its (rid, strand) group -- or of the Q19
+    pseudo-group -- holds another anchor, or a neighbouring cell does."""
+    x = a[:, 0]
+    hi = x >> np.uint64(32)
+    gid = np.where(hi == np.uint64(0xffffffff), np.uint64(1 << 33), hi)
+    cell = (gid << np.uint64(20)) | ((x & np.uint64(0x7fffffff)) >> np.uint64(15))
+    u, inv, cnt = np.unique(cell, return_inverse=True, return_counts=True)
+    occ = set(u.tolist())
+    left = np.array([(c - 1) in occ for c in cell.tolist()], dtype=bool)
+    right = np.array([(c + 1) in occ for c in cell.tolist()], dtype=bool)
+    return (cnt[inv] >= 2) | left | right
+
+
+@pytest.mark.parametrize("seg_small", [1024, 64, 8, 1])
+def test_filtered_sort_parity(dev, small_world, dense_world, seg_small):
+    """Production sort (cell buckets + per-segment ranking, singleton filter
+    on): the anchors the DP runs on equal the oracle's sorted anchors minus
+    the singletons, for every path -- thread-ranked small segments, block-
+    ranked and radix-sorted big ones, the whole-read radix when too many big
+    segments (seg_small 1) or too many anchors (> 65535) appear."""
+    os.environ["MM2G_SORT_SMALL"] = "1"
+    os.environ["MM2G_SEG_SMALL"] = str(seg_small)
+    try:
+        rng = random.Random(5)
+        for world, mids in ((small_world, (None,)), (dense_world, (20, 5000, 100000))):
+            ref, reads, rnames, rseqs = world
+            qs = list(rseqs)
+            if world is dense_world:
+                qs += [rseqs[0] * 3, rseqs[8] + rseqs[16], _rand_seq(rng, 20000)]
+            oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+            idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+            for mid in mids:
+                mid = mid if mid is not None else max(idx.calc_mid_occ(2e-4), 10)
+                dev.upload_index(idx, mid)
+                dev.set_debug(False)
+                dev.set_reads(qs)
+                dev.map(M.map_opts())
+                for r, q in enumerate(qs):
+                    want, _ = oi.anchors(q, 10, 15, mid)
+                    if len(want) > 1:
+                        want = want[_singleton_keep(want)]
+                    got = dev.debug_anchors(r)
+                    assert np.array_equal(got, want), (seg_small, mid, r, len(got), len(want))
+    finally:
+        del os.environ["MM2G_SORT_SMALL"]
+        del os.environ["MM2G_SEG_SMALL"]
+        dev.set_debug(True)
