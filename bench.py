@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     p.add_argument("--stats", default="", help="write per-read chain statistics (npz) to this path")
-    p.add_argument("--streams", type=int, default=3,
+    p.add_argument("--streams", type=int, default=2,
                    help="contexts (HIP streams) per GPU, each mapping a contiguous share of the step's reads "
                         "from its own host thread against one shared device index")
     return p.parse_args()

@@ -75,7 +75,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, dv_separate = false;
@@ -593,7 +593,12 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     LCHK(launch_read_order(n, a_cnt, order, c->stream));
     ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work,
                  std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, nullptr, order, A, std::min<int32_t>((int32_t)n, 4 * 256), tmark,
-                 lseg, lseg_n, lcap, lseg_order, rbest, cnt2, smax, mseg, lseg_n + 2, lseg_n + 3, mcap2};
+                 lseg, lseg_n, lcap, lseg_order, rbest, cnt2, smax, mseg, lseg_n + 2, lseg_n + 3, mcap2, nullptr, 0u};
+    if (!c->debug && !getenv("MM2G_NO_PRUNE")) {
+        int32_t* fmin;
+        ENSURE(c->fmin, int32_t, n, fmin);
+        ca.fmin = fmin;
+    }
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) {
             ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
@@ -609,9 +614,28 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         static const char* names[2][5] = {{"chain_seg", "chain_med", "chain_lorder", "chain_long", "chain_fin"},
                                           {"chain_seg_rescue", "chain_med_rescue", "chain_lorder_rescue", "chain_long_rescue", "chain_fin_rescue"}};
         const int blocks[5] = {sb, mb, 1, lb, 0};
+        if (pass == 1) ca.fmin = nullptr;   // the rescue pass runs on few reads: its bound costs more than it saves
+        if (ca.fmin) {   // lower bound of each read's best f: prunes segments (not in debug mode)
+            ProfScope ps(c, pass ? "chain_lb_rescue" : "chain_lb");
+            LCHK(launch_chain_stage(5, ca, (int)std::min<uint32_t>((n + 3) / 4, 2048u), c->stream));
+        }
+        ca.lseg_prof = getenv("MM2G_LSEG_PROF") ? 1u : 0u;
         for (int stg = 0; stg < 5; ++stg) {
             ProfScope ps(c, names[pass][stg]);
             LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));
+        }
+        if (ca.lseg_prof) {   // the slowest long segments of this pass
+            uint32_t nl = 0;
+            HIPCHK(hipMemcpyAsync(&nl, ca.lseg_n, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            nl = std::min(nl, lcap);
+            std::vector<uint4> ls(nl);
+            if (nl) HIPCHK(hipMemcpy(ls.data(), lseg, (size_t)nl * 16, hipMemcpyDeviceToHost));
+            std::sort(ls.begin(), ls.end(), [](const uint4& x, const uint4& y) { return x.w > y.w; });
+            double tot = 0; for (auto& v : ls) tot += v.w;
+            fprintf(stderr, "[lseg_prof] pass %d: %u long segments, sum %.0f us; slowest:", pass, nl, tot / 100);
+            for (size_t i = 0; i < ls.size() && i < 8; ++i) fprintf(stderr, " (read %u len %u %.0f us)", ls[i].x, ls[i].z - ls[i].y, ls[i].w / 100.0);
+            fprintf(stderr, "\n");
         }
     }
     // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)

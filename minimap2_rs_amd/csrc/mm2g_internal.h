@@ -153,6 +153,8 @@ struct ChainArgs {
     uint32_t* mseg_n;        // its length (atomic counter)
     uint32_t* mseg_take;     // next entry to hand out (atomic counter)
     uint32_t mseg_cap;
+    int32_t* fmin;           // per read: a lower bound of max f (k_chain_lb); null = no segment pruning
+    uint32_t lseg_prof;      // MM2G_LSEG_PROF: k_chain_long stores each long segment's wall-clock ticks in lseg[].w
 };
 struct DvArgs {
     uint32_t n;

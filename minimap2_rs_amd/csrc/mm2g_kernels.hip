@@ -1352,6 +1352,20 @@ DEVI void scan_nskip(int32_t& a, int32_t& b) {
 #undef NS_STEP
 }
 
+// the same composition scan with the additive part clamped at NEG (a chain of
+// "no predecessor" steps must not overflow)
+DEVI void scan_lb(int32_t& a, int32_t& b) {
+    constexpr int32_t NEG = -(1 << 29);
+#define LB_STEP(CTRL, RM)                                                   \
+    {                                                                       \
+        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
+        b = max(ob + a, b); a = max(oa + a, NEG);                           \
+    }
+    LB_STEP(0x111, 0xf) LB_STEP(0x112, 0xf) LB_STEP(0x114, 0xf) LB_STEP(0x118, 0xf)
+    LB_STEP(0x142, 0xa) LB_STEP(0x143, 0xc)
+#undef LB_STEP
+}
+
 constexpr int TINY = CHAIN_TINY;  // segments up to this many anchors: one lane, registers
 constexpr int MED = CHAIN_MED;    // up to this many: one lane, state machine over HBM; longer: whole wave
 
@@ -1364,8 +1378,8 @@ constexpr int KRING = 512;        // per-wave LDS ring of the newest anchor keys
 constexpr int TQ = 128;           // per-wave LDS queue per tiny length class (2 | 3-4 | 5-8 anchors)
 constexpr int MEDB = 128;         // per-wave LDS buffer of medium segments before the global append
 constexpr int64_t EST_LANE = 2048;   // estimated DP pairs above which a segment goes to a whole wave
-// rescue pass (few reads, GPU otherwise idle): latency matters, so only small
-// segments stay on one lane
+// rescue pass (few reads, GPU otherwise idle) and pruned pass 0 (few segments
+// survive): latency matters, so only small segments stay on one lane
 constexpr int64_t EST_LANE_RESCUE = 96;
 
 // Scalar chain_dp_all (lchain.rs:73-90) of one segment of <= TINY anchors held
@@ -1479,6 +1493,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
         uint64_t pairs = 0;
         uint32_t n_big = 0;
         int32_t max_seg = 0;
+        const int32_t fm = a.fmin ? uni(a.fmin[r]) : 0;   // segments with len * span < fm are skipped
         int32_t bf = INT_MIN, bi = -1;      // per-lane best (singletons and tiny segments)
         int32_t pend = -1;                  // start of the open segment
         int32_t th0 = 0, th1 = 0, th2 = 0, tt0 = 0, tt1 = 0, tt2 = 0;   // tiny class queue heads / tails
@@ -1515,6 +1530,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
         // route completed segments [sl, el) of the emitting lanes
         auto route = [&](bool emit, int32_t sl, int32_t el) {
             const int32_t len = el - sl;
+            emit = emit && (int64_t)len * span >= (int64_t)fm;   // pruned: cannot hold the read's best f
             if (emit && len == 1) { F[sl] = span; PP[sl] = -1; best_merge(bf, bi, span, sl); }
             const bool c0 = emit && len == 2, c1 = emit && len >= 3 && len <= 4, c2 = emit && len >= 5 && len <= TINY;
             const uint64_t m0 = ballot(c0), m1 = ballot(c1), m2 = ballot(c2);
@@ -1531,7 +1547,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
                 const int64_t bp = p1 - p0 > 0 ? (int64_t)(p1 - p0) : 1;
                 int64_t win = ((int64_t)len * maxdx + bp - 1) / bp;
                 win = win < len ? win : len;
-                med = (int64_t)len * win / 2 <= (P.pass == 0 ? EST_LANE : EST_LANE_RESCUE);
+                med = (int64_t)len * win / 2 <= ((P.pass == 0 && !a.fmin) ? EST_LANE : EST_LANE_RESCUE);
             }
             const bool big = emit && len > TINY && !med;
             const uint64_t medM = ballot(med);
@@ -1615,6 +1631,74 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
                 if (P.pass == 0) O->pad2 = st6; else O->n_deep = st6;
             }
         }
+    }
+}
+
+// ---- 5a'. a lower bound of the read's best f, for segment pruning.
+// In chain_dp_all (lchain.rs:73-90) the first predecessor visited for a
+// non-isolated anchor i is j = i - 1 (the n_skip break needs > max_skip
+// visits first), so f[i] >= max(span, f[i-1] + sc(i, i-1)) whenever comput_sc
+// (lchain.rs:17-34) accepts (i, i-1), and f[i] >= span always.  LB[i] =
+// max(span, LB[i-1] + sc) is a composition scan of x -> max(x + a, b) over
+// the wave.  A segment of len anchors has f <= len * span (every step adds at
+// most span), so one with len * span < max LB can hold neither the read's
+// largest f nor a tie of it: k_chain_seg skips it (not in debug mode, where
+// the full f/pprev arrays are kept).
+__global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const ChainKParams P = a.P;
+    int16_t* lut = (int16_t*)smem;
+    for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
+    __syncthreads();
+    const int lane = lane_id();
+    const uint32_t qb = a.kl.qb, rb = a.kl.rb;
+    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
+    const uint32_t gsh = rb + qb;
+    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    constexpr int32_t NEG = -(1 << 29);
+    constexpr int U = 4;                      // blocks of 64 keys loaded together
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
+        if (P.pass == 1 && !(uni(a.out[r].flags) & RF_RESCUED)) continue;
+        const uint64_t base = uni64(a.a_off[r]);
+        const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);
+        const uint64_t* K = a.keys + base;
+        int32_t carry = NEG, best = span;
+        uint32_t prev_lo = 0, prev_hi = 0;
+        for (int32_t i00 = 0; i00 < A; i00 += 64 * U) {
+            uint64_t kk[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) { const int32_t il = i00 + u * 64 + lane; kk[u] = il < A ? K[il] : 0; }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t ak = kk[u];
+                const int32_t il = i00 + u * 64 + lane;
+                const bool valid = il < A;
+                const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)prev_hi) << 32) |
+                                    (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)prev_lo);
+                const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
+                const int32_t p = (int32_t)((ak >> qb) & rmask), pj = (int32_t)((pk >> qb) & rmask);
+                const int32_t q = (int32_t)(ak & qmask), qj = (int32_t)(pk & qmask);
+                const bool iso = il == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx);
+                int32_t sa = NEG;
+                if (valid && !iso) {
+                    const int32_t dq = q - qj, dr = p - pj;
+                    const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                    if (dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw) {
+                        const int32_t dg = dr < dq ? dr : dq;
+                        sa = (span < dg ? span : dg) - (int32_t)lut[dd];
+                    }
+                }
+                int32_t sb = valid ? span : NEG;
+                scan_lb(sa, sb);
+                const int32_t lb = max(carry + sa, sb);
+                best = max(best, lb);
+                carry = rdl(lb, 63);
+                prev_lo = rdlu((uint32_t)ak, 63); prev_hi = rdlu((uint32_t)(ak >> 32), 63);
+            }
+        }
+        const int32_t m = rdl(scan_max(best), 63);
+        if (lane == 0) a.fmin[r] = m;
     }
 }
 
@@ -1792,6 +1876,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
         uint32_t n_steps = 0, n_deep = 0;
         int32_t best_f = INT_MIN, best_i = -1;
         (void)A; (void)n_deep;
+        const uint64_t seg_t0 = wall_clock64();
         // ---- cooperative DP of segment [s, e): anchor s is isolated, every
         // later anchor has a candidate predecessor.  The 64 newest
         // predecessors (rpos, qpos, f, pprev; lane l <-> j = i-1-l) live in
@@ -1936,6 +2021,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
             best_merge(best_f, best_i, bm, i0 + 63 - clz64(ballot(valid && fv == bm)));
         }
         if (lane == 0) {
+            if (a.lseg_prof) a.lseg[q].w = (uint32_t)min<uint64_t>(wall_clock64() - seg_t0, 0xffffffffull);   // MM2G_LSEG_PROF
             atomicMax(a.rbest + r, best_key(best_f, best_i));
             atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)cpairs);
             atomicAdd(&a.out[r].n_noniso, (uint32_t)(e - s - 1));
@@ -2224,6 +2310,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 1: hipLaunchKernelGGL(k_chain_med, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 2: hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, (const uint32_t*)a.lseg_n, a.lseg_cap, (const uint4*)a.lseg, a.lseg_order); break;
     case 3: hipLaunchKernelGGL(k_chain_long, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a); break;
+    case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 255) / 256), dim3(256), 0, st, a); break;
     }
     LAUNCH_CHECK();
