@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--reads", type=int, default=10000, help="reads per GPU per step (metric: 10k x 10 kb)")
     p.add_argument("--read-len", type=int, default=10000)
     p.add_argument("--scale", type=float, default=1.0, help="reference size relative to hg38 (1.0 = 3.1 Gb)")
+    p.add_argument("--preset", default="hg38", choices=["hg38", "ecoli"],
+                   help="synthetic reference: hg38-shaped (C3/C5 configs) or E. coli-shaped (C2)")
     p.add_argument("--ref-seed", type=int, default=38)
     p.add_argument("--read-seed", type=int, default=3)
     p.add_argument("--threads", type=int, default=0, help="host threads for index build (0 = auto)")
@@ -153,7 +155,7 @@ def main():
 
     # ---- reference + index (outside the timed region) ----------------------
     t0 = time.time()
-    names, lens, gbuf = simdata.genome("hg38", args.scale, args.ref_seed, threads=thr)
+    names, lens, gbuf = simdata.genome(args.preset, args.scale, args.ref_seed, threads=thr)
     log(f"rank {rank}: reference {lens.sum() / 1e9:.3f} Gb, {len(lens)} contigs in {time.time() - t0:.1f}s")
     t0 = time.time()
     idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr)
@@ -313,7 +315,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic (hg38-shaped reference, seeded ONT-shaped reads; SURVEY.md §8d)",
             "config": {
-                "workload": f"hg38-shaped {lens.sum() / 1e9:.2f} Gb reference index in HBM + "
+                "workload": f"{args.preset}-shaped {lens.sum() / 1e9:.2f} Gb reference index in HBM + "
                             f"{args.reads}x{args.read_len // 1000} kb ONT reads per GPU per step",
                 "reads_per_gpu_step": args.reads, "read_len": args.read_len, "ref_bases": int(lens.sum()),
                 "mid_occ": mid, "parallelism": f"reads sharded x{world} (index replicated), {S} streams per GPU",

@@ -75,7 +75,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, dv_separate = false;
@@ -123,6 +123,8 @@ struct mm2g_ctx {
 // MM2G_SYNC=1: synchronise after every stage and report the first failing
 // stage (and, in MM2G_CHECKED builds, the first out-of-range index).
 static bool g_sync_each = getenv("MM2G_SYNC") && atoi(getenv("MM2G_SYNC")) != 0;
+// a debug/tuning switch is on when the variable is set to a non-zero number
+static bool env_on(const char* name) { const char* v = getenv(name); return v && atoi(v) != 0; }
 struct ProfScope {
     mm2g_ctx* c; int i; hipEvent_t e0{}; const char* name;
     ProfScope(mm2g_ctx* c_, const char* n) : c(c_), name(n) { i = c->prof_begin(n, e0); }
@@ -422,7 +424,7 @@ static int run_sketch(mm2g_ctx* c, int w, int k, DevBuf& b_base, DevBuf& b_end, 
     {
         ProfScope ps(c, "sketch");
         uint64_t* skp = nullptr;
-        if (getenv("MM2G_SKETCH_PROF")) { HIPCHK(hipMalloc(&skp, (size_t)n * 64)); HIPCHK(hipMemsetAsync(skp, 0, (size_t)n * 64, c->stream)); a.prof = skp; }
+        if (env_on("MM2G_SKETCH_PROF")) { HIPCHK(hipMalloc(&skp, (size_t)n * 64)); HIPCHK(hipMemsetAsync(skp, 0, (size_t)n * 64, c->stream)); a.prof = skp; }
         LCHK(launch_sketch(a, grid_for(n), c->stream));
         if (skp) dump_sketch_prof(c, skp, n);
     }
@@ -549,9 +551,9 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->smax, uint64_t, n, smax);
     // the singleton filter is off in debug mode (full anchor/DP arrays for the parity tests)
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
-                (c->debug || getenv("MM2G_NO_FILTER")) ? 0u : c->dix->cells, cnt2, smax, 4096u, nullptr, 0u, SEG_THREAD, nullptr};
+                (c->debug || env_on("MM2G_NO_FILTER")) ? 0u : c->dix->cells, cnt2, smax, 4096u, nullptr, 0u, SEG_THREAD, nullptr};
     uint64_t* sprof = nullptr;
-    if (getenv("MM2G_SORT_PROF")) { HIPCHK(hipMalloc(&sprof, (size_t)n * 64)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 64, c->stream)); so.prof = sprof; }
+    if (env_on("MM2G_SORT_PROF")) { HIPCHK(hipMalloc(&sprof, (size_t)n * 64)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 64, c->stream)); so.prof = sprof; }
     if (const char* e = getenv("MM2G_SORT_SMALL")) so.small_max = std::min<uint32_t>((uint32_t)atoi(e), 4096u);   // tests
     if (const char* e = getenv("MM2G_SEG_SMALL")) so.seg_small = std::max(1u, std::min<uint32_t>((uint32_t)atoi(e), SEG_THREAD));   // tests
     {
@@ -593,12 +595,15 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     LCHK(launch_read_order(n, a_cnt, order, c->stream));
     ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work,
                  std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, nullptr, order, A, std::min<int32_t>((int32_t)n, 4 * 256), tmark,
-                 lseg, lseg_n, lcap, lseg_order, rbest, cnt2, smax, mseg, lseg_n + 2, lseg_n + 3, mcap2, nullptr, 0u};
-    if (!c->debug && !getenv("MM2G_NO_PRUNE")) {
-        int32_t* fmin;
-        ENSURE(c->fmin, int32_t, n, fmin);
-        ca.fmin = fmin;
-    }
+                 lseg, lseg_n, lcap, lseg_order, rbest, cnt2, smax, mseg, lseg_n + 2, lseg_n + 3, mcap2, nullptr, 0u,
+                 (c->debug || env_on("MM2G_NO_LAZY")) ? 0u : 1u, nullptr, 0u};
+    int32_t* fmin_buf = nullptr;
+    if (!c->debug && !env_on("MM2G_NO_PRUNE")) ENSURE(c->fmin, int32_t, n, fmin_buf);
+    uint32_t* item_off;
+    ENSURE(c->item_off, uint32_t, n + 1, item_off);
+    ca.item_off = item_off;
+    ca.seg_chunk = (uint32_t)SEG_CHUNK;
+    if (const char* e = getenv("MM2G_SEG_CHUNK")) ca.seg_chunk = std::max(64u, (uint32_t)atoi(e) & ~63u);   // tests
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) {
             ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
@@ -608,18 +613,25 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         if (sb <= 0) sb = 1024;
         if (lb <= 0) lb = 1024;
         if (mb <= 0) mb = 1024;
-        sb = std::max(1, std::min((int)((n + 3) / 4), sb));
+        sb = std::max(1, std::min((int)((n * 4 + 3) / 4), sb));   // items: up to ~4 chunks per read
         HIPCHK(hipMemsetAsync(rbest, 0, (size_t)n * 8, c->stream));
         HIPCHK(hipMemsetAsync(lseg_n, 0, 16, c->stream));   // long count (pass 0/1 slot), medium count, medium taken
         static const char* names[2][5] = {{"chain_seg", "chain_med", "chain_lorder", "chain_long", "chain_fin"},
                                           {"chain_seg_rescue", "chain_med_rescue", "chain_lorder_rescue", "chain_long_rescue", "chain_fin_rescue"}};
         const int blocks[5] = {sb, mb, 1, lb, 0};
-        if (pass == 1) ca.fmin = nullptr;   // the rescue pass runs on few reads: its bound costs more than it saves
-        if (ca.fmin) {   // lower bound of each read's best f: prunes segments (not in debug mode)
-            ProfScope ps(c, pass ? "chain_lb_rescue" : "chain_lb");
-            LCHK(launch_chain_stage(5, ca, (int)std::min<uint32_t>((n + 3) / 4, 2048u), c->stream));
+        {
+            ProfScope ps(c, pass ? "chain_items_rescue" : "chain_items");
+            LCHK(launch_chain_stage(6, ca, 1, c->stream));
         }
-        ca.lseg_prof = getenv("MM2G_LSEG_PROF") ? 1u : 0u;
+        // lower bound of each read's best f: prunes segments (pass 0, not in debug
+        // mode; the rescue pass runs on few reads, where it costs more than it saves)
+        ca.fmin = pass == 0 ? fmin_buf : nullptr;
+        if (ca.fmin) {
+            HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
+            ProfScope ps(c, "chain_lb");
+            LCHK(launch_chain_stage(5, ca, 2048, c->stream));
+        }
+        ca.lseg_prof = env_on("MM2G_LSEG_PROF") ? 1u : 0u;
         for (int stg = 0; stg < 5; ++stg) {
             ProfScope ps(c, names[pass][stg]);
             LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));
@@ -634,7 +646,12 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
             std::sort(ls.begin(), ls.end(), [](const uint4& x, const uint4& y) { return x.w > y.w; });
             double tot = 0; for (auto& v : ls) tot += v.w;
             fprintf(stderr, "[lseg_prof] pass %d: %u long segments, sum %.0f us; slowest:", pass, nl, tot / 100);
-            for (size_t i = 0; i < ls.size() && i < 8; ++i) fprintf(stderr, " (read %u len %u %.0f us)", ls[i].x, ls[i].z - ls[i].y, ls[i].w / 100.0);
+            for (size_t i = 0; i < ls.size() && i < 8; ++i) {
+                ReadOut ro;
+                HIPCHK(hipMemcpy(&ro, out + ls[i].x, sizeof ro, hipMemcpyDeviceToHost));
+                fprintf(stderr, " (read %u len %u %.0f us, read j-steps %u pairs %llu)", ls[i].x, ls[i].z - ls[i].y, ls[i].w / 100.0,
+                        ro.n_steps, (unsigned long long)ro.dp_pairs);
+            }
             fprintf(stderr, "\n");
         }
     }

@@ -108,6 +108,7 @@ struct SeedArgs {
     ReadOut* out;                         // m_kept
 };
 // per-read anchor sort + singleton filter (k_sort_small / k_sort_read)
+constexpr int32_t SEG_CHUNK = 4096;     // anchors per work item of the streaming chain kernels
 constexpr uint32_t SEG_THREAD = 1024;   // cell segments up to this length: one thread per anchor (default seg_small)
 constexpr int CELL_SHIFT = 15;   // 32 kb reference cells (>= every max_dist_x the filter is used with)
 struct SortArgs {
@@ -155,6 +156,9 @@ struct ChainArgs {
     uint32_t mseg_cap;
     int32_t* fmin;           // per read: a lower bound of max f (k_chain_lb); null = no segment pruning
     uint32_t lseg_prof;      // MM2G_LSEG_PROF: k_chain_long stores each long segment's wall-clock ticks in lseg[].w
+    uint32_t lazy;           // k_chain_long: skip deep windows no predecessor of which can beat max_f (not in debug mode)
+    uint32_t* item_off;      // k_seg_items: first work item (chunk) of order[t]; [n] = total
+    uint32_t seg_chunk;      // anchors per work item (multiple of 64; SEG_CHUNK)
 };
 struct DvArgs {
     uint32_t n;

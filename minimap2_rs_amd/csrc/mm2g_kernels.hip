@@ -1444,6 +1444,42 @@ DEVI unsigned long long best_key(int32_t f, int32_t i) {
     return ((unsigned long long)((uint32_t)f ^ 0x80000000u) << 32) | (uint32_t)i;
 }
 
+// ---- work items of the streaming chain kernels: reads in `order` (heaviest
+// first) cut into chunks of SEG_CHUNK anchors, so that several waves share a
+// heavy read (k_chain_lb, k_chain_seg).  In the rescue pass only rescued reads
+// have items.  item_off[t] = first item of order[t]; item_off[n] = total.
+__global__ __launch_bounds__(1024) void k_seg_items(ChainArgs a) {
+    __shared__ uint32_t sc[16];
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < a.n; t0 += 1024) {
+        const uint32_t t = t0 + (uint32_t)tid;
+        uint32_t c = 0;
+        if (t < a.n) {
+            const uint32_t r = a.order[t];
+            const bool on = a.P.pass == 0 || (a.out[r].flags & RF_RESCUED);
+            c = on ? (a.cnt2[r] + a.seg_chunk - 1) / a.seg_chunk : 0u;
+        }
+        uint32_t wt;
+        const uint32_t ex = wave_excl_sum(c, wt);
+        if (lane == 0) sc[wv] = wt;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+        for (int w = 0; w < 16; ++w) { pre += w < wv ? sc[w] : 0u; tot += sc[w]; }
+        if (t < a.n) a.item_off[t] = carry + pre + ex;
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0) a.item_off[a.n] = carry;
+}
+
+// item -> (position in order, chunk): last t with item_off[t] <= it
+DEVI uint32_t item_owner(const uint32_t* item_off, uint32_t n, uint32_t it) {
+    uint32_t lo = 0, hi = n;          // item_off[lo] <= it < item_off[hi]
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (item_off[mid] <= it) lo = mid; else hi = mid; }
+    return lo;
+}
+
 // ---- 5a. per read, one streaming pass over the sorted anchors: isolated
 // anchors (st(i) == i: i == 0, another (rid, strand) group than i-1, or
 // rpos_i > rpos_{i-1} + max_dist_x) delimit independent segments — the DP of
@@ -1473,18 +1509,22 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const uint32_t gsh = rb + qb;
     const int32_t maxdx = P.max_dist_x, span = P.span;
-    // Static, wave-uniform assignment of reads in `order` (heaviest first).
+    // Static, wave-uniform assignment of work items: chunks of SEG_CHUNK anchors
+    // of the reads in `order` (heaviest first).  A wave starts its chunk at the
+    // first isolated anchor at or after c0 and finishes the segment open at c1.
     const uint32_t nwaves = gridDim.x * DP_NW;
-    for (uint32_t t = blockIdx.x * DP_NW + wv; t < a.n; t += nwaves) {
-        const uint32_t r = a.order ? (uint32_t)uni((int32_t)a.order[t]) : t;
-        const int32_t flags0 = uni(a.out[r].flags);
-        if (P.pass == 1 && !(flags0 & RF_RESCUED)) continue;
+    const uint32_t n_items = (uint32_t)uni((int32_t)a.item_off[a.n]);
+    for (uint32_t it = blockIdx.x * DP_NW + wv; it < n_items; it += nwaves) {
+        const uint32_t t = (uint32_t)uni((int32_t)item_owner(a.item_off, a.n, it));
+        const uint32_t r = (uint32_t)uni((int32_t)a.order[t]);
+        const int32_t c0 = (int32_t)(it - (uint32_t)uni((int32_t)a.item_off[t])) * (int32_t)a.seg_chunk;
         const uint64_t t_start = wall_clock64();
         if (t < (uint32_t)a.n_prio) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
         const uint64_t base = uni64(a.a_off[r]);
         const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);      // anchors kept by the singleton filter
-        if (A == 0) continue;
+        const int32_t c1 = min(A, c0 + (int32_t)a.seg_chunk);
+        if (c0 >= A) continue;
 #ifdef MM2G_CHECKED
         if (base + (uint64_t)A > a.cap_keys) { if (lane == 0) CK(base + A, a.cap_keys); continue; }
 #endif
@@ -1590,9 +1630,13 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
                 tiny_batch(2, th2, n2 < 64 ? n2 : 64);
             }
         };
-        uint32_t prev_lo = 0, prev_hi = 0;
-        uint64_t nk = lane < A ? K[lane] : 0;
-        for (int32_t i0 = 0; i0 < A; i0 += 64) {
+        const uint64_t kprev = c0 > 0 ? K[c0 - 1] : 0;
+        uint32_t prev_lo = (uint32_t)uni((int32_t)(uint32_t)kprev), prev_hi = (uint32_t)uni((int32_t)(uint32_t)(kprev >> 32));
+        uint64_t nk = c0 + lane < A ? K[c0 + lane] : 0;
+        bool closed = false;
+        for (int32_t i0 = c0; i0 < A; i0 += 64) {
+            const bool ext = i0 >= c1;      // past the chunk: only close the open segment
+            if (ext && pend < 0) { closed = true; break; }
             const uint64_t ak = nk;
             const int32_t il = i0 + lane;
             const bool valid = il < A;
@@ -1602,8 +1646,12 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
                                 (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)prev_lo);
             const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
             const int32_t p = (int32_t)((ak >> qb) & rmask), pprv = (int32_t)((pk >> qb) & rmask);
-            const bool iso = valid && (il == 0 || g != gp || p > (int32_t)((uint32_t)pprv + (uint32_t)maxdx));
-            const uint64_t isoM = ballot(iso);
+            bool iso = valid && (il == 0 || g != gp || p > (int32_t)((uint32_t)pprv + (uint32_t)maxdx));
+            uint64_t isoM = ballot(iso);
+            if (ext && isoM) {              // the first isolated anchor closes it; nothing opens
+                isoM &= (~isoM + 1);
+                iso = ((isoM >> lane) & 1ULL) != 0;
+            }
             // an isolated anchor closes the segment opened by the previous one
             const uint64_t lower = isoM & lanemask_lt();
             const int32_t sl = lower ? i0 + 63 - clz64(lower) : pend;
@@ -1613,8 +1661,9 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
             prev_lo = rdlu((uint32_t)ak, 63); prev_hi = rdlu((uint32_t)(ak >> 32), 63);
             // the next block overwrites ring slots of anchors < i0 + 128 - KRING
             drain(i0 + 192 - KRING, false);
+            if (ext && isoM) { closed = true; break; }
         }
-        route(lane == 0, pend, A);          // the last segment
+        if (!closed && pend >= 0) route(lane == 0, pend, A);          // the read's last segment
         drain(0, true);
         if (nmb > 0) flush_med(nmb);
         // the read's best over its singletons and tiny segments
@@ -1658,14 +1707,18 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     constexpr int32_t NEG = -(1 << 29);
     constexpr int U = 4;                      // blocks of 64 keys loaded together
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
-        if (P.pass == 1 && !(uni(a.out[r].flags) & RF_RESCUED)) continue;
+    const uint32_t n_items = (uint32_t)uni((int32_t)a.item_off[a.n]);
+    for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + wave_id(); it < n_items; it += nwaves) {
+        const uint32_t t = (uint32_t)uni((int32_t)item_owner(a.item_off, a.n, it));
+        const uint32_t r = (uint32_t)uni((int32_t)a.order[t]);
+        const int32_t c0 = (int32_t)(it - (uint32_t)uni((int32_t)a.item_off[t])) * (int32_t)a.seg_chunk;
         const uint64_t base = uni64(a.a_off[r]);
-        const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);
+        const int32_t A = min((int32_t)uni((int32_t)a.cnt2[r]), c0 + (int32_t)a.seg_chunk);
         const uint64_t* K = a.keys + base;
-        int32_t carry = NEG, best = span;
-        uint32_t prev_lo = 0, prev_hi = 0;
-        for (int32_t i00 = 0; i00 < A; i00 += 64 * U) {
+        int32_t carry = NEG, best = span;      // LB restarts at span at a chunk start: still a lower bound
+        uint64_t k0 = c0 > 0 ? K[c0 - 1] : 0;
+        uint32_t prev_lo = (uint32_t)uni((int32_t)(uint32_t)k0), prev_hi = (uint32_t)uni((int32_t)(uint32_t)(k0 >> 32));
+        for (int32_t i00 = c0; i00 < A; i00 += 64 * U) {
             uint64_t kk[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) { const int32_t il = i00 + u * 64 + lane; kk[u] = il < A ? K[il] : 0; }
@@ -1679,7 +1732,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
                 const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
                 const int32_t p = (int32_t)((ak >> qb) & rmask), pj = (int32_t)((pk >> qb) & rmask);
                 const int32_t q = (int32_t)(ak & qmask), qj = (int32_t)(pk & qmask);
-                const bool iso = il == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx);
+                const bool iso = il == 0 || il == c0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx);
                 int32_t sa = NEG;
                 if (valid && !iso) {
                     const int32_t dq = q - qj, dr = p - pj;
@@ -1698,7 +1751,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
             }
         }
         const int32_t m = rdl(scan_max(best), 63);
-        if (lane == 0) a.fmin[r] = m;
+        if (lane == 0) atomicMax(a.fmin + r, m);
     }
 }
 
@@ -1990,6 +2043,31 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     if (nmm) { const int L = 63 - clz64(nmm); max_f = rdl(sv, L); max_j = jtop - L; }
                     cpairs += (uint64_t)__popcll(brkM ? (inrM & (eff | (1ULL << ctz64(brkM)))) : inrM);
                     if (brkM) break;
+                    // Deeper predecessors can only change (f[i], pprev[i]) if one of them
+                    // beats max_f (sv > max_f): marks and n_skip merely end the loop
+                    // early.  A cheap scan of the whole deep window (no scans, no
+                    // marks) settles most anchors of dense, unchained windows here.
+                    if (a.lazy && jtop == i - 1 && jtop - 64 >= lo) {
+                        bool cand = false;
+                        for (int32_t jd = jtop - 64; jd >= lo && !cand; jd -= 64) {
+                            const int32_t j = jd - lane;
+                            const bool inr2 = j >= lo;
+                            const bool deep = inr2 && j < ring_lo;
+                            if (any(deep) && !drained) { vm_drain(); drained = true; }
+                            uint64_t kj = 0; int32_t fj2 = 0;
+                            if (inr2) {
+                                if (!deep) { kj = rkey[j & (RK - 1)]; fj2 = rfp[j & (RK - 1)].x; }
+                                else { kj = K[CK(j, A)]; fj2 = F[CK(j, A)]; }
+                            }
+                            const int32_t dq2 = qi - (int32_t)(kj & qmask), dr2 = pi - (int32_t)((kj >> qb) & rmask);
+                            const int32_t dd2 = dr2 - dq2 < 0 ? dq2 - dr2 : dr2 - dq2;
+                            const bool ok2 = inr2 && dq2 > 0 && dq2 <= maxdx && dr2 != 0 && dq2 <= maxdy && dd2 <= bw;
+                            const int32_t dg2 = dr2 < dq2 ? dr2 : dq2;
+                            const int32_t sv2 = (span < dg2 ? span : dg2) - (int32_t)lut[ok2 ? dd2 : 0] + fj2;
+                            cand = any(ok2 && sv2 > max_f);
+                        }
+                        if (!cand) break;
+                    }
                     // a deeper step follows: record this step's marks below its window
                     if (jtop - 64 >= lo) {
                         const bool mk_out = mk && !mk_in;
@@ -2311,6 +2389,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 2: hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, (const uint32_t*)a.lseg_n, a.lseg_cap, (const uint4*)a.lseg, a.lseg_order); break;
     case 3: hipLaunchKernelGGL(k_chain_long, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a); break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
+    case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 255) / 256), dim3(256), 0, st, a); break;
     }
     LAUNCH_CHECK();

@@ -368,3 +368,38 @@ def test_filtered_sort_parity(dev, small_world, dense_world, seg_small):
         del os.environ["MM2G_SORT_SMALL"]
         del os.environ["MM2G_SEG_SMALL"]
         dev.set_debug(True)
+
+
+@pytest.mark.parametrize("chunk", [64, 192])
+def test_chunked_chain_items(dev, small_world, dense_world, tmp_path, chunk):
+    """Reads cut into many small work items (a wave per chunk, each finishing
+    the segment open at its end; the lower bound restarting per chunk): DP
+    arrays (debug) and PAF (production, pruning on) still equal the oracle's."""
+    os.environ["MM2G_SEG_CHUNK"] = str(chunk)
+    try:
+        for world, mid in ((small_world, None), (dense_world, 5000), (dense_world, 20)):
+            ref, reads, rnames, rseqs = world
+            oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+            idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+            mid = mid if mid is not None else max(idx.calc_mid_occ(2e-4), 10)
+            dev.upload_index(idx, mid)
+            dev.set_debug(True)
+            dev.set_reads(rseqs)
+            res = dev.map(M.map_opts())
+            for r, q in enumerate(rseqs):
+                want_a, _ = oi.anchors(q, 10, 15, mid)
+                if len(want_a) == 0:
+                    continue
+                rescued = bool(res[r].flags & 2)
+                f, pp, _, _, _ = O.chain_dp(want_a, 15, bw=(20000 if rescued else 500))
+                gf, gpp = dev.debug_dp(r)
+                assert np.array_equal(gf, f) and np.array_equal(gpp.astype(np.int64), pp), \
+                    f"chunk {chunk}: DP differs for read {r}: " + _dp_diff(gf, gpp, f, pp, want_a)
+            want_paf = str(tmp_path / "want.paf")
+            oi.align_fasta(reads, want_paf, mid_occ=mid)
+            want = open(want_paf).read()
+            assert dev.paf(rnames, res) == want
+            assert _map_nodebug(dev, rnames, rseqs)[0] == want
+    finally:
+        del os.environ["MM2G_SEG_CHUNK"]
+        dev.set_debug(True)
