@@ -1939,6 +1939,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
         int32_t st = s, stb = INT_MIN / 2, skv = INT_MIN / 2;   // st window [stb, stb+63], valid up to skv
         uint64_t sk = 0;
         int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
+        bool try_simple = true;
         uint64_t nk = (s + lane < e) ? K[s + lane] : 0;
         for (int32_t i0 = s; i0 < e; i0 += 64) {
             const uint64_t ak = nk;
@@ -1981,6 +1982,50 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
                 int32_t max_f = span, max_j = -1, n_skip = 0;
                 bool marks = false;
+                // Simple path: n_skip only rises on a marked target, and every mark
+                // comes from a valid j with pprev[j] >= lo.  With <= max_skip such
+                // sources in the whole window no break can happen, so (f[i], pprev[i])
+                // is the plain running maximum in visiting order: the largest sv,
+                // first visited (largest j) among equal ones.  No prefix scans, no
+                // marks.  Tried while it keeps succeeding (and every 16th anchor).
+                bool done = false;
+                if (a.lazy && (try_simple || (i & 15) == 0)) {
+                    int32_t bv = INT_MIN, bj = -1;
+                    uint32_t nmk = 0;
+                    for (int32_t jtop = i - 1; jtop >= lo && nmk <= (uint32_t)P.max_skip; jtop -= 64) {
+                        const int32_t j = jtop - lane;
+                        const bool inr = j >= lo;
+                        int32_t pj, qj, fj, ppj;
+                        if (jtop == i - 1) { pj = wp; qj = wq; fj = wf; ppj = wpp; }
+                        else {
+                            const bool deep = inr && j < ring_lo;
+                            if (any(deep) && !drained) { vm_drain(); drained = true; }
+                            uint64_t kj = 0;
+                            int2 fpj = make_int2(0, -1);
+                            if (inr) {
+                                if (!deep) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
+                                else { kj = K[CK(j, A)]; fpj = make_int2(F[CK(j, A)], PP[CK(j, A)]); }
+                            }
+                            pj = (int32_t)((kj >> qb) & rmask); qj = (int32_t)(kj & qmask); fj = fpj.x; ppj = fpj.y;
+                        }
+                        const int32_t dq = qi - qj, dr = pi - pj;
+                        bool ok = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy;
+                        const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                        ok = ok && dd <= bw;
+                        const int32_t dg = dr < dq ? dr : dq;
+                        const int32_t sv = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0] + fj;
+                        nmk += (uint32_t)__popcll(ballot(ok && ppj >= lo));
+                        const int32_t v = ok ? sv : INT_MIN;
+                        const int32_t m = rdl(scan_max(v), 63);
+                        if (m > bv) { bv = m; bj = jtop - ctz64(ballot(v == m)); }
+                        cpairs += (uint64_t)__popcll(ballot(inr));
+                        ++n_steps;
+                    }
+                    done = nmk <= (uint32_t)P.max_skip;
+                    if (done && bv > span) { max_f = bv; max_j = bj; }
+                    try_simple = done;
+                }
+                if (!done)
                 for (int32_t jtop = i - 1; jtop >= lo; jtop -= 64) {
                     const int32_t j = jtop - lane;
                     const bool inr = j >= lo;
