@@ -531,52 +531,54 @@ DEVI uint32_t fslot(uint64_t h, uint32_t tmask) { return (uint32_t)((h * 0x9E377
 constexpr int FT_MAX = 4096;
 DEVI bool filter_lds_ok(uint32_t ts, int k) { return ts > 0 && ts <= (uint32_t)FT_MAX && k <= 16; }
 
-__global__ __launch_bounds__(256) void k_filter(FilterArgs a, int a_k) {
-    const int lane = lane_id();
-    const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
-        const uint64_t mb = uni64(a.mz_base[r]);
-        const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
-        uint8_t* keep = a.keep + mb;
-        const uint64_t tb = uni64(a.tab_off[r]);
-        const uint32_t ts = (uint32_t)(uni64(a.tab_off[r + 1]) - tb);
-        if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) continue;   // seeds.rs:14-15: k_filter_lds
-        if (filter_lds_ok(ts, a_k)) continue;                        // done by k_filter_lds
-        uint64_t* tk = a.tab_key + tb; uint32_t* tc = a.tab_cnt + tb;
-        for (uint32_t b0 = 0; b0 < ts; b0 += 64) { const uint32_t i = b0 + lane; if (i < ts) { tk[i] = U64MAX; tc[i] = 0; } }
-        vm_drain();
-        const uint32_t tmask = ts - 1;
-        for (uint32_t b0 = 0; b0 < m; b0 += 64) {
-            const uint32_t i = b0 + lane;
-            bool done = i >= m;
-            const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
-            uint32_t sl = fslot(h, tmask);
-            while (any(!done)) {
-                if (!done) {
-                    const unsigned long long prev = atomicCAS((unsigned long long*)&tk[sl], (unsigned long long)U64MAX, (unsigned long long)h);
-                    if (prev == U64MAX || prev == h) { atomicAdd(&tc[sl], 1u); done = true; }
-                    else sl = (sl + 1) & tmask;
-                }
+__global__ __launch_bounds__(1024) void k_filter(FilterArgs a, int a_k) {
+    // one 1024-thread block per read whose table does not fit k_filter_lds (large m)
+    const uint32_t r = blockIdx.x;
+    if (r >= a.n) return;
+    const int tid = threadIdx.x;
+    const uint64_t mb = a.mz_base[r];
+    const uint32_t m = a.mz_cnt[r];
+    uint8_t* keep = a.keep + mb;
+    const uint64_t tb = a.tab_off[r];
+    const uint32_t ts = (uint32_t)(a.tab_off[r + 1] - tb);
+    if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) return;   // seeds.rs:14-15: k_filter_lds
+    if (filter_lds_ok(ts, a_k)) return;                        // done by k_filter_lds
+    uint64_t* tk = a.tab_key + tb; uint32_t* tc = a.tab_cnt + tb;
+    for (uint32_t i = tid; i < ts; i += 1024) { tk[i] = U64MAX; tc[i] = 0; }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t tmask = ts - 1;
+    for (uint32_t b0 = 0; b0 < m; b0 += 1024) {
+        const uint32_t i = b0 + tid;
+        bool done = i >= m;
+        const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
+        uint32_t sl = fslot(h, tmask);
+        while (any(!done)) {
+            if (!done) {
+                const unsigned long long prev = atomicCAS((unsigned long long*)&tk[sl], (unsigned long long)U64MAX, (unsigned long long)h);
+                if (prev == U64MAX || prev == h) { atomicAdd(&tc[sl], 1u); done = true; }
+                else sl = (sl + 1) & tmask;
             }
         }
-        vm_drain();
-        const float prod = (float)m * a.q_occ_frac;
-        const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
-        for (uint32_t b0 = 0; b0 < m; b0 += 64) {
-            const uint32_t i = b0 + lane;
-            bool done = i >= m;
-            const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
-            uint32_t sl = fslot(h, tmask), c = 0;
-            while (any(!done)) {
-                if (!done) {
-                    const uint64_t kk = __hip_atomic_load(&tk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (kk == h) { c = __hip_atomic_load(&tc[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); done = true; }
-                    else if (kk == U64MAX) done = true;
-                    else sl = (sl + 1) & tmask;
-                }
+    }
+    __threadfence_block();
+    __syncthreads();
+    const float prod = (float)m * a.q_occ_frac;
+    const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
+    for (uint32_t b0 = 0; b0 < m; b0 += 1024) {
+        const uint32_t i = b0 + tid;
+        bool done = i >= m;
+        const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
+        uint32_t sl = fslot(h, tmask), c = 0;
+        while (any(!done)) {
+            if (!done) {
+                const uint64_t kk = __hip_atomic_load(&tk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (kk == h) { c = __hip_atomic_load(&tc[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); done = true; }
+                else if (kk == U64MAX) done = true;
+                else sl = (sl + 1) & tmask;
             }
-            if (i < m) keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
         }
+        if (i < m) keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
     }
 }
 
@@ -2155,50 +2157,67 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
 
 // ---- 5c. per read: fallback chain walk (lchain.rs:162-171), chain_qrange /
 // chain_trange (178-200) and the rescue test of rescue_long_join (316-330).
+constexpr int FIN_CH = 2048;   // pprev entries staged per wave (LDS) for the chain walk
 __global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    // one wave per read; the pprev walk reads chunks of FIN_CH entries staged in
+    // LDS (coalesced) instead of one dependent HBM load per chain anchor
+    __shared__ int32_t s_pp[4][FIN_CH];
+    const int lane = lane_id(), wv = wave_id();
+    const uint32_t r = blockIdx.x * 4 + (uint32_t)wv;
     if (r >= a.n) return;
+    int32_t* spp = s_pp[wv];
     const ChainKParams P = a.P;
     ReadOut* O = a.out + r;
-    const int32_t flags0 = O->flags;
+    const int32_t flags0 = uni(O->flags);
     if (P.pass == 1 && !(flags0 & RF_RESCUED)) return;
-    const uint64_t base = a.a_off[r];
-    const int32_t A = (int32_t)(a.a_off[r + 1] - base);
-    const int32_t qlen = (int32_t)(a.rd_off[r + 1] - a.rd_off[r]);
+    const uint64_t base = uni64(a.a_off[r]);
+    const int32_t A = (int32_t)(uni64(a.a_off[r + 1]) - base);
+    const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
     if (A == 0) {
-        O->flags = flags0 & RF_EMPTY; O->n_anchors = 0; O->score = 0; O->cm = 0;
-        O->qs = O->qe = O->ts = O->te = 0; O->group = 0; O->best_i = -1; O->qlen = qlen;
+        if (lane == 0) {
+            O->flags = flags0 & RF_EMPTY; O->n_anchors = 0; O->score = 0; O->cm = 0;
+            O->qs = O->qe = O->ts = O->te = 0; O->group = 0; O->best_i = -1; O->qlen = qlen;
+        }
         return;
     }
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const uint32_t gsh = rb + qb;
     const int32_t span = P.span;
-    const int32_t A2 = (int32_t)a.cnt2[r];          // anchors in the DP (singleton filter)
-    const uint64_t sm = a.smax[r];                  // 1 + largest dropped key, 0 = none
+    const int32_t A2 = (int32_t)uni((int32_t)a.cnt2[r]);     // anchors in the DP (singleton filter)
+    const uint64_t sm = uni64(a.smax[r]);                   // 1 + largest dropped key, 0 = none
     uint64_t* K = (uint64_t*)a.keys + base;       // writable: slot A2 receives a dropped best
     const int32_t* PP = a.pp + base;
     uint32_t* CB = a.chain + base;
     int32_t best_f = span, best_i = -1;
     if (A2 > 0) {
-        const unsigned long long bk = a.rbest[r];
+        const unsigned long long bk = uni64(a.rbest[r]);
         best_f = (int32_t)((uint32_t)(bk >> 32) ^ 0x80000000u); best_i = (int32_t)(uint32_t)bk;
     }
     // "last argmax f" over all anchors: a dropped singleton (f = span) wins when
     // every kept anchor also has f == span and its key is the largest
-    const bool single = sm != 0 && (A2 == 0 || (best_f == span && sm - 1 > K[CK(A2 - 1, A)]));
-    int32_t idx, root, cm = 0;
+    const bool single = sm != 0 && (A2 == 0 || (best_f == span && sm - 1 > uni64(K[CK(A2 - 1, A)])));
+    int32_t root, cm = 0;
     if (single) {
-        K[CK(A2, A)] = sm - 1;                      // slot A2 is free (A2 < A); k_dv reads it via CB
-        CB[0] = (uint32_t)A2; cm = 1; root = A2; best_i = A2; best_f = span;
+        if (lane == 0) { K[CK(A2, A)] = sm - 1; CB[0] = (uint32_t)A2; }   // slot A2 is free (A2 < A); k_dv reads it via CB
+        cm = 1; root = A2; best_i = A2; best_f = span;
     } else {
-        idx = best_i; root = best_i;
+        // fallback chain walk (lchain.rs:162-171), wave-uniform
+        int32_t idx = best_i;
+        root = best_i;
         while (idx >= 0 && cm < A2) {
-            CB[cm] = (uint32_t)idx;
-            ++cm; root = idx;
-            idx = PP[CK(idx, A)];
+            const int32_t lo_c = idx - FIN_CH + 1 > 0 ? idx - FIN_CH + 1 : 0;
+            for (int32_t t = lo_c + lane; t <= idx; t += 64) spp[t - lo_c] = PP[CK(t, A)];
+            wave_lds_sync();
+            while (idx >= lo_c && cm < A2) {
+                if (lane == 0) CB[cm] = (uint32_t)idx;
+                ++cm; root = idx;
+                idx = uni(spp[idx - lo_c]);
+            }
+            wave_lds_sync();
         }
     }
+    if (lane != 0) return;
     const uint64_t kb = K[CK(best_i, A)], kr = K[CK(root, A)];
     const uint32_t g = (uint32_t)(kb >> gsh);
     const int32_t qe = (int32_t)(kb & qmask) + 1;
@@ -2377,7 +2396,8 @@ int launch_filter(const FilterArgs& a, int k, int n_blocks, hipStream_t st) {
     if (a.n == 0) return 0;
     hipLaunchKernelGGL(k_filter_lds, dim3(a.n), dim3(256), 0, st, a, k);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_filter, dim3(n_blocks), dim3(256), 0, st, a, k);
+    (void)n_blocks;
+    hipLaunchKernelGGL(k_filter, dim3(a.n), dim3(1024), 0, st, a, k);
     LAUNCH_CHECK();
     return 0;
 }
@@ -2435,7 +2455,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 3: hipLaunchKernelGGL(k_chain_long, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a); break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
-    default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 255) / 256), dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 3) / 4), dim3(256), 0, st, a); break;
     }
     LAUNCH_CHECK();
     return 0;
