@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--threads", type=int, default=0, help="host threads for index build (0 = auto)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    p.add_argument("--host-index", action="store_true", help="build the index on the host instead of the GPU")
     p.add_argument("--stats", default="", help="write per-read chain statistics (npz) to this path")
     p.add_argument("--streams", type=int, default=2,
                    help="contexts (HIP streams) per GPU, each mapping a contiguous share of the step's reads "
@@ -158,9 +159,12 @@ def main():
     names, lens, gbuf = simdata.genome(args.preset, args.scale, args.ref_seed, threads=thr)
     log(f"rank {rank}: reference {lens.sum() / 1e9:.3f} Gb, {len(lens)} contigs in {time.time() - t0:.1f}s")
     t0 = time.time()
-    idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr)
+    # GPU index build (byte-identical to the host build, tests/test_gpu_parity.py)
+    idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr,
+                                    device=None if args.host_index else gpu)
+    t_index = time.time() - t0
     mid = max(idx.calc_mid_occ(2e-4), 10)       # main.rs:196-197
-    log(f"rank {rank}: index built in {time.time() - t0:.1f}s, stats {idx.stats()}, mid_occ {mid}")
+    log(f"rank {rank}: index built ({'host' if args.host_index else 'GPU'}) in {t_index:.1f}s, stats {idx.stats()}, mid_occ {mid}")
 
     # ---- reads (per rank: distinct seed) -----------------------------------
     rbuf, roffs, _ = simdata.reads(gbuf, lens, args.reads, args.read_len, rank_read_seed(args.read_seed, rank))
@@ -329,6 +333,7 @@ def main():
                 "path_alg_GBps": round(path_gbs, 3) if path_gbs else None,
                 "path_frac_of_8TBps": round(path_gbs / HBM_PEAK_GBS, 6) if path_gbs else None,
                 "dp_pairs_per_s": dp_pairs_s,
+                "index_build_s": round(t_index, 3), "index_build_on": "host" if args.host_index else "gpu",
                 "index_upload_s": round(t_up, 3),
                 "reads_h2d_ms": round(t_h2d * 1e3, 3),
                 "pcie_inclusive_gbases_s": round(n_bases / (ms_per_step / 1e3 + t_h2d) / 1e9, 6) if world == 1 else None,

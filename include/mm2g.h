@@ -49,6 +49,13 @@ int mm2g_index_build_fasta(const char* path, int w, int k, int b, int flag, int 
 /* Same from in-memory sequences (names may be NULL -> no name). */
 int mm2g_index_build_seqs(uint32_t n_seq, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens,
                           int w, int k, int b, int flag, int n_threads, mm2g_index** out);
+/* The same builds on a GPU (reference sketching, bucket
+ * sort by hash and p/h construction on `device`, S packed there too); the
+ * result is identical to the host build (same .mmi bytes).  HPC (flag & 1) and
+ * even k fall back to the host build inside the call. */
+int mm2g_index_build_fasta_gpu(const char* path, int w, int k, int b, int flag, int device, int n_threads, mm2g_index** out);
+int mm2g_index_build_seqs_gpu(uint32_t n_seq, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens,
+                              int w, int k, int b, int flag, int device, int n_threads, mm2g_index** out);
 /* Index::load_from_mmi (src/index.rs:361-424) / Index::save_to_mmi (:233-307).
  * Hash entries are written in ascending key order (the reference writes
  * HashMap iteration order, which is random per process). */

@@ -49,6 +49,9 @@ SIGNATURES = {
     "mm2g_index_build_fasta": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),
     "mm2g_index_build_seqs": (C.c_int, [C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_void_p), _P64,
                                         C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),
+    "mm2g_index_build_fasta_gpu": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),
+    "mm2g_index_build_seqs_gpu": (C.c_int, [C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_void_p), _P64,
+                                            C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),
     "mm2g_index_load_mmi": (C.c_int, [C.c_char_p, C.POINTER(_VP)]),
     "mm2g_index_save_mmi": (C.c_int, [_VP, C.c_char_p]),
     "mm2g_index_free": (None, [_VP]),

@@ -74,9 +74,19 @@ class Index:
         return cls(h.value)
 
     @classmethod
+    def build_index_from_fasta_gpu(cls, path: str, w: int = 10, k: int = 15, b: int = 14, flag: int = 0, device: int = 0,
+                                   threads: int = 8) -> "Index":
+        """The same index built on a GPU (mm2g_index_build_fasta_gpu; HPC / even k build on the host)."""
+        h = C.c_void_p()
+        check(load().mm2g_index_build_fasta_gpu(path.encode(), w, k, b, flag, device, threads, C.byref(h)),
+              "build_index_from_fasta_gpu")
+        return cls(h.value)
+
+    @classmethod
     def build_from_buffer(cls, names: Optional[Sequence[str]], buf: np.ndarray, lens: np.ndarray, w: int = 10, k: int = 15,
-                          b: int = 14, flag: int = 0, threads: int = 8) -> "Index":
-        """Index from sequences concatenated in one uint8 buffer (pointers into it; no copies)."""
+                          b: int = 14, flag: int = 0, threads: int = 8, device: Optional[int] = None) -> "Index":
+        """Index from sequences concatenated in one uint8 buffer (pointers into it; no copies).
+        device = a GPU index build (mm2g_index_build_seqs_gpu) instead of the host build."""
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         lv = np.ascontiguousarray(lens, dtype=np.uint64)
         n = len(lv)
@@ -85,8 +95,12 @@ class Index:
         ptrs = (C.c_void_p * max(n, 1))(*[base + int(x) for x in starts])
         nm = (C.c_char_p * max(n, 1))(*[x.encode() for x in names]) if names is not None else None
         h = C.c_void_p()
-        check(load().mm2g_index_build_seqs(n, nm, ptrs, lv.ctypes.data_as(L._P64), w, k, b, flag, threads, C.byref(h)),
-              "build_from_buffer")
+        if device is None:
+            check(load().mm2g_index_build_seqs(n, nm, ptrs, lv.ctypes.data_as(L._P64), w, k, b, flag, threads, C.byref(h)),
+                  "build_from_buffer")
+        else:
+            check(load().mm2g_index_build_seqs_gpu(n, nm, ptrs, lv.ctypes.data_as(L._P64), w, k, b, flag, device, threads,
+                                                   C.byref(h)), "build_from_buffer_gpu")
         return cls(h.value)
 
     @classmethod

@@ -239,6 +239,38 @@ int mm2g_index_build_seqs(uint32_t n_seq, const char* const* names, const uint8_
     return 0;
 }
 
+static int build_gpu_or_host(int device, const std::vector<const uint8_t*>& seqs, const std::vector<uint64_t>& lens,
+                             const std::vector<std::string>* names, int w, int k, int b, int flag, int n_threads, mm2g_index** out) {
+    std::unique_ptr<mm2g_index> I(new mm2g_index());
+    std::string err;
+    bool unsupported = false;
+    if (!build_index_gpu(device, seqs, lens, names, w, k, b, flag, I->h, err, unsupported)) {
+        if (!unsupported) return set_err(MM2G_E_HIP, "%s", err.c_str());
+        if (!build_index(seqs, lens, names, w, k, b, flag, n_threads, I->h, err)) return set_err(MM2G_E_ARG, "%s", err.c_str());
+    }
+    *out = I.release();
+    return 0;
+}
+
+int mm2g_index_build_fasta_gpu(const char* path, int w, int k, int b, int flag, int device, int n_threads, mm2g_index** out) {
+    if (!path || !out) return set_err(MM2G_E_ARG, "null argument");
+    std::vector<FastaRecord> recs; std::string err;
+    if (!read_fasta(path, recs, false, err)) return set_err(MM2G_E_IO, "%s", err.c_str());
+    std::vector<const uint8_t*> seqs; std::vector<uint64_t> lens; std::vector<std::string> names;
+    for (auto& r : recs) { seqs.push_back((const uint8_t*)r.seq.data()); lens.push_back(r.seq.size()); names.push_back(r.name); }
+    return build_gpu_or_host(device, seqs, lens, &names, w, k, b, flag, n_threads, out);
+}
+
+int mm2g_index_build_seqs_gpu(uint32_t n_seq, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens,
+                              int w, int k, int b, int flag, int device, int n_threads, mm2g_index** out) {
+    if (!out || (n_seq && (!seqs || !lens))) return set_err(MM2G_E_ARG, "null argument");
+    std::vector<const uint8_t*> s(seqs, seqs + n_seq);
+    std::vector<uint64_t> l(lens, lens + n_seq);
+    std::vector<std::string> nm;
+    if (names) for (uint32_t i = 0; i < n_seq; ++i) nm.push_back(names[i] ? names[i] : "");
+    return build_gpu_or_host(device, s, l, names ? &nm : nullptr, w, k, b, flag, n_threads, out);
+}
+
 int mm2g_index_load_mmi(const char* path, mm2g_index** out) {
     if (!path || !out) return set_err(MM2G_E_ARG, "null argument");
     std::unique_ptr<mm2g_index> I(new mm2g_index());

@@ -43,6 +43,11 @@ struct HostIndex {
 
 bool build_index(const std::vector<const uint8_t*>& seqs, const std::vector<uint64_t>& lens, const std::vector<std::string>* names,
                  int w, int k, int b, int flag, int n_threads, HostIndex& idx, std::string& err);
+// The same index built on `device` (mm2g_ixbuild.hip).  unsupported = the GPU
+// path does not apply (HPC, even k, slot overflow): use build_index.
+bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const std::vector<uint64_t>& lens,
+                     const std::vector<std::string>* names, int w, int k, int b, int flag, HostIndex& idx, std::string& err,
+                     bool& unsupported);
 bool load_mmi(const char* path, HostIndex& idx, std::string& err);
 bool save_mmi(const HostIndex& idx, const char* path, std::string& err);
 

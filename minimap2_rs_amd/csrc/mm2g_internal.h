@@ -84,6 +84,15 @@ struct SketchArgs {
     uint32_t* mz_cnt;           // per sequence
     int32_t* overflow;
     uint64_t* prof;             // MM2G_SKETCH_PROF: per sequence 8 phase-time sums (else null)
+    // Index build (mm2g_ixbuild.hip): sequence r is a view [view_off, +view_len)
+    // into a contig with view_pre bases of that contig before it; steps before
+    // emit_from are warm-up (no emissions); view_last = the view ends its contig
+    // (final flush, sketch.rs:99).  Null view_off: sequences are rd_off ranges.
+    const uint64_t* view_off = nullptr;
+    const uint32_t* view_len = nullptr;
+    const uint32_t* view_pre = nullptr;
+    const uint32_t* emit_from = nullptr;
+    const uint8_t* view_last = nullptr;
 };
 struct FilterArgs {
     uint32_t n;

@@ -203,9 +203,18 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
     const uint32_t shift1 = 2u * (uint32_t)(k - 1);
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wv; r < a.n; r += nwaves) {
-        const uint64_t roff = uni64(a.rd_off[r]);
+        uint64_t roff;
+        int64_t L, pre = 0, efrom = 0;
+        bool flush = true;
+        if (a.view_off) {   // index chunk: a view into a contig (see SketchArgs)
+            roff = uni64(a.view_off[r]); L = (int64_t)(uint32_t)uni((int32_t)a.view_len[r]);
+            pre = (int64_t)(uint32_t)uni((int32_t)a.view_pre[r]); efrom = (int64_t)(uint32_t)uni((int32_t)a.emit_from[r]);
+            flush = uni((int32_t)a.view_last[r]) != 0;
+        } else {
+            roff = uni64(a.rd_off[r]);
+            L = (int64_t)(uni64(a.rd_off[r + 1]) - roff);
+        }
         const uint8_t* s = a.seq + roff;
-        const int64_t L = (int64_t)(uni64(a.rd_off[r + 1]) - roff);
         const uint64_t obase = uni64(a.out_base[r]), oend = uni64(a.out_end[r]);
         if (L == 0) { if (lane == 0) a.mz_cnt[r] = 0; continue; }
         uint64_t pt[6] = {0, 0, 0, 0, 0, 0}, tz = a.prof ? wall_clock64() : 0;
@@ -255,15 +264,15 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                     V |= (pk >> 16) << (8 * (d - 1));
                 }
                 const uint32_t need_bits = (k - 1 >= 32) ? 0xffffffffu : ((1u << (k - 1)) - 1u);
-                const bool slow = ps < pe && (ps < k - 1 || (V & need_bits) != need_bits);
+                const bool slow = ps < pe && (ps + pre < k - 1 || (V & need_bits) != need_bits);
                 kf = W & ((k - 1 >= 32) ? U64MAX : ((1ULL << (2 * (k - 1))) - 1));
                 kr = (rev2_64(~W) >> (64 - 2 * k)) & ~3ULL;
                 if (any(slow)) {
                     if (slow) { kf = 0; kr = 0; }
                     int64_t wsp = ps;
                     int need = slow ? k - 1 : 0;
-                    while (any(need > 0 && wsp > 0)) {
-                        if (need > 0 && wsp > 0) { --wsp; if (nt4d(s[wsp]) < 4) --need; }
+                    while (any(need > 0 && wsp > -pre)) {   // back to the contig start (views: before the view)
+                        if (need > 0 && wsp > -pre) { --wsp; if (nt4d(s[wsp]) < 4) --need; }
                     }
                     int64_t pw = slow ? wsp : ps;
                     while (any(pw < ps)) {
@@ -342,7 +351,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
             // ---- phase 2: reference step logic, count then write
             uint32_t myoff = 0, tot = 0;
             bool fast_done = false;
-#define SK_EMIT(xv, yv) do { if (WR && o < oend) { a.mz_x[o] = (xv); a.mz_y[o] = (yv); } ++o; ++n_em; } while (0)
+#define SK_EMIT(xv, yv) do { if (em_ok) { if (WR && o < oend) { a.mz_x[o] = (xv); a.mz_y[o] = (yv); } ++o; ++n_em; } } while (0)
             if (w > SK_CH) {
                 // The reference's `min` after step i is the newest minimum of slots
                 // [i-w+1, i] (DESIGN.md "Sketch").  Window = [i-w+1, ps-1] u [ps, i]:
@@ -385,7 +394,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                         need |= act && l == w + k - 1 && mxo != U64MAX;                 // A (sketch.rs:90-93)
                         const bool doB = act && xi <= mxo;                              // B (94-96)
                         const bool doC = act && !doB && mqo == ii - w;                  // C (97-105)
-                        if ((doB && l >= w + k && mxo != U64MAX) || (doC && l >= w + k - 1)) {
+                        if (((doB && l >= w + k && mxo != U64MAX) || (doC && l >= w + k - 1)) && i >= efrom) {
                             em |= 1u << t; eq[t >> 1] |= (uint32_t)mqo << (16 * (t & 1));
                         }
                         if (act) {
@@ -431,6 +440,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                 for (int t = 0; t < SK_CH; ++t) {
                     const int64_t i = ps + t;
                     const bool act = i < pe;
+                    const bool em_ok = i >= efrom;   // warm-up steps of an index view emit nothing
                     const int ii = (int)(i - hbase);
                     const uint64_t ix_x = act ? X[ii] : U64MAX;
                     const uint32_t ix_y = act ? SK_Y(ii) : 0xffffffffu;
@@ -493,7 +503,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                 const uint64_t x = X[q];
                 if (mx >= x) { mx = x; my = SK_Y(q); }
             }
-            if (mx != U64MAX) {
+            if (mx != U64MAX && flush) {
                 const uint64_t o = obase + count;
                 if (lane == 0 && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
                 ++count;

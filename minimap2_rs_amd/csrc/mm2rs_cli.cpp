@@ -18,7 +18,7 @@
 
 static void usage() {
     fprintf(stderr,
-            "Usage: mm2rs index <fasta> [-w 10] [-k 15] [-b 14] [-H] [-d out.mmi] [-t threads]\n"
+            "Usage: mm2rs index <fasta> [-w 10] [-k 15] [-b 14] [-H] [-d out.mmi] [-t threads] [--device N] [--cpu-index]\n"
             "       mm2rs align <ref.mmi|ref.fa> <reads.fa> [-w 10] [-k 15] [-H] [-f 2e-4] [-g 5000] [-r bw[,bw_long]]\n"
             "                   [-n 3] [-m 40] [-M 0.5] [-p 0.8] [-N 5] [-x map-ont|map-hifi|lr:hq|sr] [-a] [-o out]\n"
             "                   [-t threads] [--device N] [--batch-bases N] [--first-only]\n");
@@ -34,7 +34,7 @@ int main(int argc, char** argv) {
     std::string cmd = argv[1];
     std::vector<std::string> pos;
     int w = 10, k = 15, b = 14, threads = 8, device = 0;
-    bool hpc = false, first_only = false;
+    bool hpc = false, first_only = false, cpu_index = false;
     float frac = 2e-4f;
     std::string dump, out, preset, ropt;
     mm2g_map_opts mo; mm2g_map_opts_default(&mo);
@@ -62,6 +62,7 @@ int main(int argc, char** argv) {
         else if (a == "--device") device = atoi(nxt().c_str());
         else if (a == "--batch-bases") batch_bases = atoll(nxt().c_str());
         else if (a == "--first-only") first_only = true;
+        else if (a == "--cpu-index") cpu_index = true;
         else if (!a.empty() && a[0] == '-' && a.size() > 1) { fprintf(stderr, "error: unknown option %s\n", a.c_str()); usage(); return 2; }
         else pos.push_back(a);
     }
@@ -69,7 +70,10 @@ int main(int argc, char** argv) {
         if (pos.size() != 1) { usage(); return 2; }
         const int flag = hpc ? 1 : 0;
         mm2g_index* idx = nullptr;
-        if (mm2g_index_build_fasta(pos[0].c_str(), w, k, b, flag, threads, &idx) != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
+        const bool gpu = !cpu_index && mm2g_device_count() > 0;
+        const int st0 = gpu ? mm2g_index_build_fasta_gpu(pos[0].c_str(), w, k, b, flag, device, threads, &idx)
+                            : mm2g_index_build_fasta(pos[0].c_str(), w, k, b, flag, threads, &idx);
+        if (st0 != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
         uint64_t nk, tl; double ao, as; uint32_t n_seq;
         mm2g_index_stats(idx, &nk, &ao, &as, &tl);
         mm2g_index_params(idx, nullptr, nullptr, nullptr, nullptr, &n_seq);
@@ -104,7 +108,8 @@ int main(int argc, char** argv) {
     else {
         FILE* f = fopen(ref.c_str(), "rb"); char m[9] = {0};
         if (f) { size_t got = fread(m, 1, 9, f); fclose(f); if (got == 9 && memcmp(m, "MM2RSIDX\0", 9) == 0) { fprintf(stderr, "Error: MM2RSIDX indexes are out of scope; use .mmi\n"); return 1; } }
-        st = mm2g_index_build_fasta(ref.c_str(), w, k, 14, hpc ? 1 : 0, threads, &idx);
+        st = (!cpu_index && mm2g_device_count() > 0) ? mm2g_index_build_fasta_gpu(ref.c_str(), w, k, 14, hpc ? 1 : 0, device, threads, &idx)
+                                                     : mm2g_index_build_fasta(ref.c_str(), w, k, 14, hpc ? 1 : 0, threads, &idx);
     }
     if (st != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
     int32_t mid_occ;

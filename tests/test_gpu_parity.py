@@ -403,3 +403,39 @@ def test_chunked_chain_items(dev, small_world, dense_world, tmp_path, chunk):
     finally:
         del os.environ["MM2G_SEG_CHUNK"]
         dev.set_debug(True)
+
+
+def _mmi_bytes(idx, path):
+    idx.save_to_mmi(path)
+    return open(path, "rb").read()
+
+
+@pytest.mark.parametrize("chunk", [None, 4096, 300])
+def test_gpu_index_build(tmp_path, chunk):
+    """GPU index build (sketch views, pair sort, bucket distribution, packed S)
+    equals the host build byte for byte (.mmi), with stats and mid_occ, on an
+    hg38-shaped and an E. coli-shaped genome plus edge contigs: N runs across
+    view boundaries, lowercase, contigs shorter than k, empty contigs."""
+    rng = random.Random(11)
+    names, lens, gbuf = simdata.genome("hg38", 0.0006, 5)
+    seqs = [gbuf[int(o):int(o + l)].tobytes() for o, l in zip(np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)]
+    e_names, e_lens, e_buf = simdata.genome("ecoli", 0.2, 1)
+    seqs.append(e_buf.tobytes()); names.append("ecoli")
+    s = bytearray(_rand_seq(rng, 20000))
+    for st_ in (4096 - 40, 8192 - 3, 12000):
+        s[st_:st_ + 60] = b"N" * 60
+    seqs += [bytes(s), _rand_seq(rng, 9000, p_low=0.3), b"ACGTACGT", b"", _rand_seq(rng, 15, p_n=0.0), b"N" * 500 + _rand_seq(rng, 3000)]
+    names += ["nruns", "lower", "short", "empty", "k15", "leadingN"]
+    if chunk is not None:
+        os.environ["MM2G_IXCHUNK"] = str(chunk)
+    try:
+        for w, k in ((10, 15), (5, 11), (19, 19), (10, 27)):
+            ih = M.Index.build_from_seqs(names, seqs, w=w, k=k, b=14, threads=4)
+            buf = np.frombuffer(b"".join(seqs), dtype=np.uint8)
+            lv = np.array([len(x) for x in seqs], dtype=np.uint64)
+            ig = M.Index.build_from_buffer(names, buf, lv, w=w, k=k, b=14, threads=4, device=0)
+            assert ih.stats() == ig.stats(), (w, k)
+            assert ih.calc_mid_occ(2e-4) == ig.calc_mid_occ(2e-4)
+            assert _mmi_bytes(ih, str(tmp_path / "h.mmi")) == _mmi_bytes(ig, str(tmp_path / "g.mmi")), (w, k)
+    finally:
+        os.environ.pop("MM2G_IXCHUNK", None)
