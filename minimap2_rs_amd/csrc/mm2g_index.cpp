@@ -5,6 +5,7 @@
 #include "mm2g_index.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <thread>
@@ -41,6 +42,50 @@ bool read_fasta(const char* path, std::vector<FastaRecord>& out, bool first_only
             out.back().seq.append(data, pos, le - pos);
         }
         pos = e + 1;
+    }
+    return true;
+}
+
+SeqStream::~SeqStream() {
+    if (fp_) fclose(fp_);
+    free(buf_);
+}
+bool SeqStream::open(const char* path, std::string& err) {
+    fp_ = fopen(path, "rb");
+    if (!fp_) { err = std::string("cannot open ") + path; return false; }
+    return true;
+}
+bool SeqStream::getline_(std::string& s) {
+    if (has_pending_) { s.swap(pending_); has_pending_ = false; return true; }
+    const ssize_t n = ::getline(&buf_, &cap_, fp_);
+    if (n < 0) return false;
+    size_t le = (size_t)n;
+    if (le && buf_[le - 1] == '\n') --le;
+    if (le && buf_[le - 1] == '\r') --le;
+    s.assign(buf_, le);
+    return true;
+}
+bool SeqStream::next(FastaRecord& rec) {
+    std::string ln;
+    for (;;) {   // header: text before the first record is ignored (read_fasta)
+        if (!getline_(ln)) return false;
+        if (!ln.empty() && (ln[0] == '>' || ln[0] == '@')) break;
+    }
+    const bool fastq = ln[0] == '@';
+    size_t ne = 1;
+    while (ne < ln.size() && ln[ne] != ' ' && ln[ne] != '\t') ++ne;
+    rec.name = ln.substr(1, ne - 1);
+    rec.seq.clear();
+    while (getline_(ln)) {
+        if (!ln.empty() && (fastq ? ln[0] == '+' : ln[0] == '>')) {
+            if (!fastq) { pending_.swap(ln); has_pending_ = true; }
+            break;
+        }
+        rec.seq += ln;
+    }
+    if (fastq) {   // quality: as many characters as the sequence
+        size_t q = 0;
+        while (q < rec.seq.size() && getline_(ln)) q += ln.size();
     }
     return true;
 }

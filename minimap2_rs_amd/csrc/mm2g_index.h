@@ -11,6 +11,23 @@ struct FastaRecord { std::string name; std::string seq; };
 // space/tab; sequence lines concatenated with '\r' stripped.
 bool read_fasta(const char* path, std::vector<FastaRecord>& out, bool first_only, std::string& err);
 
+// Streaming reader of FASTA ('>', the read_fasta rules) and FASTQ ('@' header,
+// sequence lines up to '+', quality skipped by length) records, one at a time
+// (the CLI's double-buffered align pipeline).
+class SeqStream {
+  public:
+    ~SeqStream();
+    bool open(const char* path, std::string& err);
+    bool next(FastaRecord& rec);          // false at end of input
+  private:
+    bool getline_(std::string& s);        // without '\n' / trailing '\r'
+    FILE* fp_ = nullptr;
+    char* buf_ = nullptr;
+    size_t cap_ = 0;
+    std::string pending_;
+    bool has_pending_ = false;
+};
+
 struct HostMinimizer { uint64_t key_span, rid_pos_strand; };
 // sketch_sequence (src/sketch.rs:29-100) on the host, incl. the HPC branch
 // (index build with -H).  Returns false on the reference's assert conditions.

@@ -1,16 +1,27 @@
 // mm2rs — command line of the MI355X path, flag-compatible with the
 // reference CLI (src/main.rs:11-233):
 //   mm2rs index <ref.fa> [-w 10] [-k 15] [-b 14] [-H] [-d out.mmi]
-//   mm2rs align <ref.mmi|ref.fa> <reads.fa> [-w] [-k] [-H] [-f] [-g] [-r bw[,bw_long]]
+//   mm2rs align <ref.mmi|ref.fa> <reads.fa|fq> [-w] [-k] [-H] [-f] [-g] [-r bw[,bw_long]]
 //               [-n] [-m] [-M] [-p] [-N] [-x preset] [-a] [-o out]
+//   mm2rs anchors <ref> <reads.fa> [-w] [-k] [-H]       (main.rs:160-171)
+//   mm2rs chain <ref> <reads.fa> [-w] [-k] [-r 5000] [-H] (main.rs:172-186)
 // Extra flags: -t threads (host index build), --device N, --batch-bases N,
-// --first-only (map only the first record, exactly as the reference does).
-// Unlike the reference, align maps every record of <reads.fa>; the output is
+// --streams N (contexts in the align pipeline), --first-only (map only the
+// first record, exactly as the reference does), --cpu-index.
+// Unlike the reference, align maps every record of <reads> (FASTA or FASTQ),
+// streaming: a reader fills batches, N contexts (HIP streams, one shared
+// device index) map them concurrently -- batch k+1's upload and sketch overlap
+// batch k's chaining -- and a writer emits PAF in input order.  The output is
 // the per-read concatenation of what the reference prints for each read alone.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <condition_variable>
+#include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mm2g.h"
@@ -39,6 +50,7 @@ int main(int argc, char** argv) {
     std::string dump, out, preset, ropt;
     mm2g_map_opts mo; mm2g_map_opts_default(&mo);
     long long batch_bases = 256LL << 20;
+    int n_streams = 2;
     for (int i = 2; i < argc; ++i) {
         std::string a = argv[i];
         auto nxt = [&]() -> std::string { if (i + 1 >= argc) { usage(); exit(2); } return std::string(argv[++i]); };
@@ -61,6 +73,7 @@ int main(int argc, char** argv) {
         else if (a == "-t") threads = atoi(nxt().c_str());
         else if (a == "--device") device = atoi(nxt().c_str());
         else if (a == "--batch-bases") batch_bases = atoll(nxt().c_str());
+        else if (a == "--streams") n_streams = std::max(1, atoi(nxt().c_str()));
         else if (a == "--first-only") first_only = true;
         else if (a == "--cpu-index") cpu_index = true;
         else if (!a.empty() && a[0] == '-' && a.size() > 1) { fprintf(stderr, "error: unknown option %s\n", a.c_str()); usage(); return 2; }
@@ -86,13 +99,19 @@ int main(int argc, char** argv) {
         mm2g_index_free(idx);
         return 0;
     }
-    if (cmd != "align") { usage(); return 2; }
+    if (cmd != "align" && cmd != "anchors" && cmd != "chain") { usage(); return 2; }
+    const bool dbg_cmd = cmd != "align";
+    if (dbg_cmd) { preset.clear(); }
     if (pos.size() != 2) { usage(); return 2; }
     // apply_preset (main.rs:125-133)
     if (preset == "map-ont") { k = 15; w = 10; }
     else if (preset == "map-hifi" || preset == "lr:hq") { k = 19; w = 10; }
     else if (preset == "sr") { k = 21; w = 11; }
     mo.w = w; mo.k = k;
+    if (cmd == "chain") {   // Chain: default_chain_params(k) with bw = -r (default 5000), chain_dp (no rescue)
+        mo.bw = ropt.empty() ? 5000 : atoi(ropt.c_str());
+        ropt.clear();
+    }
     if (!ropt.empty()) {   // main.rs:202-207: "-r bw[,bw_long]", unparsable parts ignored
         size_t c = ropt.find(',');
         std::string a0 = ropt.substr(0, c);
@@ -119,37 +138,155 @@ int main(int argc, char** argv) {
     if (mm2g_ctx_create(device, &ctx) != 0 || mm2g_ctx_upload_index(ctx, idx, mid_occ) != 0) {
         fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1;
     }
-    std::vector<mm2g::FastaRecord> recs; std::string err;
-    if (!mm2g::read_fasta(pos[1].c_str(), recs, first_only, err)) { fprintf(stderr, "Error: %s\n", err.c_str()); return 1; }
+    if (dbg_cmd) {   // anchors / chain of the first read (read_fasta_first, main.rs:92-103)
+        mm2g::SeqStream in; std::string err;
+        mm2g::FastaRecord rec;
+        if (!in.open(pos[1].c_str(), err)) { fprintf(stderr, "Error: %s\n", err.c_str()); return 1; }
+        if (!in.next(rec)) rec = mm2g::FastaRecord{"*", std::string()};
+        mm2g_ctx_set_debug(ctx, 1);   // full sorted anchors and f / pprev
+        if (cmd == "chain") mo.bw_long = mo.bw;   // a rescue pass with the same parameters = chain_dp
+        uint64_t offs[2] = {0, rec.seq.size()};
+        mm2g_read_result res;
+        if (mm2g_batch_set_reads(ctx, (const uint8_t*)rec.seq.data(), offs, 1) != 0 || mm2g_batch_map(ctx, &mo) != 0 ||
+            mm2g_batch_results(ctx, &res, 1) != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
+        const int64_t A = mm2g_debug_anchors(ctx, 0, nullptr, 0);
+        std::vector<uint64_t> xy((size_t)std::max<int64_t>(A, 1) * 2);
+        if (A > 0) mm2g_debug_anchors(ctx, 0, xy.data(), A);
+        if (cmd == "anchors") {
+            printf("anchors: %lld\n", (long long)A);
+            for (int64_t i = 0; i < A && i < 10; ++i) printf("x=0x%016llx y=0x%016llx\n", (unsigned long long)xy[2 * i], (unsigned long long)xy[2 * i + 1]);
+        } else {
+            // fallback chain (lchain.rs:162-171): last argmax f, pprev walk
+            std::vector<int32_t> f((size_t)std::max<int64_t>(A, 1)), pp((size_t)std::max<int64_t>(A, 1));
+            if (A > 0) mm2g_debug_dp(ctx, 0, f.data(), pp.data(), A);
+            std::vector<int64_t> ch;
+            if (A > 0) {
+                int64_t bi = 0;
+                for (int64_t i = 1; i < A; ++i) if (f[i] >= f[bi]) bi = i;
+                for (int64_t i = bi; i >= 0; i = pp[i]) ch.push_back(i);
+            }
+            printf("best_chain_len: %zu\n", ch.size());
+            if (!ch.empty()) {
+                const int64_t st = ch.back(), en = ch.front();
+                printf("start: x=0x%016llx y=0x%016llx\n", (unsigned long long)xy[2 * st], (unsigned long long)xy[2 * st + 1]);
+                printf("end:   x=0x%016llx y=0x%016llx\n", (unsigned long long)xy[2 * en], (unsigned long long)xy[2 * en + 1]);
+            }
+        }
+        mm2g_ctx_destroy(ctx);
+        mm2g_index_free(idx);
+        return 0;
+    }
+    // ---- streaming align: reader -> N mapping contexts -> in-order writer
+    std::vector<mm2g_ctx*> ctxs{ctx};
+    for (int i = 1; i < n_streams; ++i) {
+        mm2g_ctx* c2 = nullptr;
+        if (mm2g_ctx_create(device, &c2) != 0 || mm2g_ctx_share_index(c2, ctx, mid_occ) != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
+        ctxs.push_back(c2);
+    }
+    mm2g::SeqStream in; std::string err;
+    if (!in.open(pos[1].c_str(), err)) { fprintf(stderr, "Error: %s\n", err.c_str()); return 1; }
     FILE* fo = stdout;
     if (!out.empty() && out != "-") { fo = fopen(out.c_str(), "w"); if (!fo) { fprintf(stderr, "Error: cannot create %s\n", out.c_str()); return 1; } }
+    struct Batch {
+        size_t no = 0;
+        std::vector<std::string> names;
+        std::string cat;
+        std::vector<uint64_t> offs{0};
+        std::vector<mm2g_read_result> res;
+        bool ok = false;
+    };
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Batch*> todo;                 // FIFO of batches to map
+    std::map<size_t, Batch*> done;            // mapped, by batch number
+    bool eof = false, failed = false;
+    size_t n_batches = 0;
+    const size_t max_inflight = 2 * ctxs.size() + 1;
+    size_t inflight = 0;
+    auto worker = [&](mm2g_ctx* c) {
+        for (;;) {
+            Batch* B;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !todo.empty() || eof || failed; });
+                if (todo.empty()) return;
+                B = todo.front(); todo.erase(todo.begin());
+            }
+            const uint32_t n = (uint32_t)B->names.size();
+            B->res.resize(n);
+            B->ok = mm2g_batch_set_reads(c, (const uint8_t*)B->cat.data(), B->offs.data(), n) == 0 && mm2g_batch_map(c, &mo) == 0 &&
+                    mm2g_batch_results(c, B->res.data(), n) == 0;
+            if (!B->ok) fprintf(stderr, "Error: %s\n", mm2g_last_error());
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                done[B->no] = B;
+                if (!B->ok) failed = true;
+            }
+            cv.notify_all();
+        }
+    };
     std::vector<char> pafbuf;
-    for (size_t r0 = 0; r0 < recs.size();) {
-        size_t r1 = r0; long long bases = 0;
-        while (r1 < recs.size() && (r1 == r0 || bases + (long long)recs[r1].seq.size() <= batch_bases)) { bases += (long long)recs[r1].seq.size(); ++r1; }
-        std::vector<uint64_t> offs(r1 - r0 + 1, 0);
-        std::string cat; cat.reserve((size_t)bases);
-        std::vector<const char*> names;
-        for (size_t i = r0; i < r1; ++i) { cat += recs[i].seq; offs[i - r0 + 1] = cat.size(); names.push_back(recs[i].name.c_str()); }
-        const uint32_t n = (uint32_t)(r1 - r0);
-        std::vector<mm2g_read_result> res(n);
-        if (mm2g_batch_set_reads(ctx, (const uint8_t*)cat.data(), offs.data(), n) != 0 || mm2g_batch_map(ctx, &mo) != 0 ||
-            mm2g_batch_results(ctx, res.data(), n) != 0) {
-            fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1;
+    auto writer = [&]() {
+        for (size_t next = 0;; ++next) {
+            Batch* B;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return done.count(next) || (eof && next >= n_batches) || failed; });
+                if (!done.count(next)) return;
+                B = done[next]; done.erase(next);
+            }
+            if (B->ok) {
+                const uint32_t n = (uint32_t)B->names.size();
+                std::vector<const char*> nm(n);
+                for (uint32_t i = 0; i < n; ++i) {
+                    nm[i] = B->names[i].c_str();
+                    if (B->res[i].flags & MM2G_R_EMPTY) fprintf(stderr, "warning: read %s is empty (the reference asserts on it, src/sketch.rs:40); skipped\n", nm[i]);
+                    if (B->res[i].flags & MM2G_R_PANIC) fprintf(stderr, "warning: read %s: the reference panics here (index out of bounds: rid 2147483647, DESIGN.md Q19); no PAF line\n", nm[i]);
+                }
+                const int64_t need = mm2g_format_paf(idx, B->res.data(), nm.data(), n, nullptr, 0);
+                pafbuf.resize((size_t)std::max<int64_t>(need, 0) + 512 * (size_t)n + 1);
+                const int64_t got = mm2g_format_paf(idx, B->res.data(), nm.data(), n, pafbuf.data(), (int64_t)pafbuf.size());
+                if (got < 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); std::lock_guard<std::mutex> lk(mu); failed = true; }
+                else fwrite(pafbuf.data(), 1, (size_t)got, fo);
+            }
+            delete B;
+            { std::lock_guard<std::mutex> lk(mu); --inflight; }
+            cv.notify_all();
         }
-        for (uint32_t i = 0; i < n; ++i) {
-            if (res[i].flags & MM2G_R_EMPTY) fprintf(stderr, "warning: read %s is empty (the reference asserts on it, src/sketch.rs:40); skipped\n", names[i]);
-            if (res[i].flags & MM2G_R_PANIC) fprintf(stderr, "warning: read %s: the reference panics here (index out of bounds: rid 2147483647, DESIGN.md Q19); no PAF line\n", names[i]);
+    };
+    std::vector<std::thread> th;
+    for (mm2g_ctx* c : ctxs) th.emplace_back(worker, c);
+    std::thread wt(writer);
+    {   // reader: batches of up to --batch-bases bases (at least one read)
+        mm2g::FastaRecord rec;
+        Batch* B = nullptr;
+        size_t n_read = 0;
+        auto push = [&](Batch* b) {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return inflight < max_inflight || failed; });
+            b->no = n_batches++; ++inflight;
+            todo.push_back(b);
+            cv.notify_all();
+        };
+        while (!(first_only && n_read >= 1) && in.next(rec)) {
+            ++n_read;
+            if (B && !B->names.empty() && (long long)(B->cat.size() + rec.seq.size()) > batch_bases) { push(B); B = nullptr; }
+            if (!B) B = new Batch();
+            B->names.push_back(rec.name);
+            B->cat += rec.seq;
+            B->offs.push_back(B->cat.size());
+            { std::lock_guard<std::mutex> lk(mu); if (failed) break; }
         }
-        int64_t need = mm2g_format_paf(idx, res.data(), names.data(), n, nullptr, 0);
-        pafbuf.resize((size_t)need + 512 * n + 1);
-        int64_t got = mm2g_format_paf(idx, res.data(), names.data(), n, pafbuf.data(), (int64_t)pafbuf.size());
-        if (got < 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
-        fwrite(pafbuf.data(), 1, (size_t)got, fo);
-        r0 = r1;
+        if (B) push(B);
+        { std::lock_guard<std::mutex> lk(mu); eof = true; }
+        cv.notify_all();
     }
+    for (auto& t : th) t.join();
+    { std::lock_guard<std::mutex> lk(mu); eof = true; }
+    cv.notify_all();
+    wt.join();
     if (fo != stdout) fclose(fo);
-    mm2g_ctx_destroy(ctx);
+    for (mm2g_ctx* c : ctxs) mm2g_ctx_destroy(c);
     mm2g_index_free(idx);
-    return 0;
+    return failed ? 1 : 0;
 }

@@ -439,3 +439,47 @@ def test_gpu_index_build(tmp_path, chunk):
             assert _mmi_bytes(ih, str(tmp_path / "h.mmi")) == _mmi_bytes(ig, str(tmp_path / "g.mmi")), (w, k)
     finally:
         os.environ.pop("MM2G_IXCHUNK", None)
+
+
+def test_cli_streaming_fastq(small_world, tmp_path):
+    """`mm2rs align` streams: many small batches over 3 contexts (out-of-order
+    completion, in-order output) and FASTQ input give the oracle CLI's lines."""
+    import subprocess
+    ref, reads, rnames, rseqs = small_world
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mm2rs = os.path.join(root, "minimap2_rs_amd", "build", "mm2rs")
+    cpu = os.path.join(root, "oracle", "build", "mm2rs-cpu")
+    want = subprocess.run([cpu, "align", ref, reads], check=True, capture_output=True, text=True).stdout
+    got = subprocess.run([mm2rs, "align", ref, reads, "--streams", "3", "--batch-bases", "20000"], check=True,
+                         capture_output=True, text=True).stdout
+    assert got == want and want.count("\n") > 50
+    fq = str(tmp_path / "reads.fq")
+    with open(fq, "w") as fh:
+        for n, s in zip(rnames, rseqs):
+            fh.write(f"@{n} extra\n{s.decode()}\n+\n{'I' * len(s)}\n")
+    got = subprocess.run([mm2rs, "align", ref, fq, "--batch-bases", "50000"], check=True, capture_output=True, text=True).stdout
+    assert got == want
+
+
+def test_cli_anchors_chain(small_world, tmp_path):
+    """`mm2rs anchors` / `mm2rs chain` (main.rs:160-186) on the first read, against
+    the oracle's build_anchors_filtered and chain_dp (bw from -r, no rescue)."""
+    import subprocess
+    ref, reads, rnames, rseqs = small_world
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mm2rs = os.path.join(root, "minimap2_rs_amd", "build", "mm2rs")
+    oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+    mid = max(oi.mid_occ(2e-4), 10)
+    a, _ = oi.anchors(rseqs[0], 10, 15, mid)
+    want = f"anchors: {len(a)}\n" + "".join(f"x=0x{int(x):016x} y=0x{int(y):016x}\n" for x, y in a[:10])
+    got = subprocess.run([mm2rs, "anchors", ref, reads], check=True, capture_output=True, text=True).stdout
+    assert got == want
+    for bw in (5000, 500):
+        _, _, chain, _, _ = O.chain_dp(a, 15, max_gap=5000, bw=bw)
+        want = f"best_chain_len: {len(chain)}\n"
+        if len(chain):
+            s, e = a[chain[0]], a[chain[-1]]
+            want += f"start: x=0x{int(s[0]):016x} y=0x{int(s[1]):016x}\nend:   x=0x{int(e[0]):016x} y=0x{int(e[1]):016x}\n"
+        args = [mm2rs, "chain", ref, reads] + ([] if bw == 5000 else ["-r", str(bw)])
+        got = subprocess.run(args, check=True, capture_output=True, text=True).stdout
+        assert got == want, bw
