@@ -635,6 +635,8 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
     ca.seg_chunk = (uint32_t)SEG_CHUNK;
+    ca.giant_min = 1024;
+    if (const char* e = getenv("MM2G_GIANT_MIN")) ca.giant_min = std::max(2, atoi(e));   // tests
     if (const char* e = getenv("MM2G_SEG_CHUNK")) ca.seg_chunk = std::max(64u, (uint32_t)atoi(e) & ~63u);   // tests
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) {
@@ -665,6 +667,10 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         }
         ca.lseg_prof = env_on("MM2G_LSEG_PROF") ? 1u : 0u;
         for (int stg = 0; stg < 5; ++stg) {
+            if (stg == 2 && ca.lazy && !env_on("MM2G_NO_GIANT")) {   // giant segments as a Jacobi fixed point (production)
+                ProfScope ps(c, pass ? "chain_giant_rescue" : "chain_giant");
+                LCHK(launch_chain_stage(7, ca, 256, c->stream));
+            }
             ProfScope ps(c, names[pass][stg]);
             LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));
         }

@@ -1378,6 +1378,7 @@ DEVI void scan_lb(int32_t& a, int32_t& b) {
 #undef LB_STEP
 }
 
+constexpr uint32_t LSEG_DONE = 0xffffffffu;   // lseg[].w: handled by k_chain_giant
 constexpr int TINY = CHAIN_TINY;  // segments up to this many anchors: one lane, registers
 constexpr int MED = CHAIN_MED;    // up to this many: one lane, state machine over HBM; longer: whole wave
 
@@ -1929,6 +1930,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
     for (uint32_t t = blockIdx.x * DP_NW + wv; t < nl; t += nwaves) {
         const uint32_t q = (uint32_t)uni((int32_t)a.lseg_order[t]);
         const uint4 L = a.lseg[q];
+        if (uni((int32_t)L.w) == (int32_t)LSEG_DONE) continue;   // k_chain_giant did it
         const uint32_t r = (uint32_t)uni((int32_t)L.x);
         const int32_t s = uni((int32_t)L.y), e = uni((int32_t)L.z);
         if (t < 256) __builtin_amdgcn_s_setprio(2);
@@ -2162,6 +2164,248 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
             atomicAdd(&a.out[r].n_noniso, (uint32_t)(e - s - 1));
             atomicAdd(&a.out[r].n_steps, n_steps);
         }
+    }
+}
+
+// ---- 5b'. giant segments (production only): chain_dp_all (lchain.rs:73-90)
+// as a policy-iteration fixed point.  When no window holds more than max_skip
+// mark sources (valid j with pprev[j] >= lo), no n_skip break can happen and
+// the reference's loop is the plain running maximum in visiting order:
+//   f[i] = max(span, max_{j in [lo_i, i-1], valid} f[j] + sc(i, j)),
+//   pprev[i] = the first visited (largest) j reaching it (when > span).
+// Only j < i appear, so the recurrence has one solution.  Plain value
+// iteration needs (longest chain) rounds; policy iteration -- evaluate the
+// current predecessor forest by pointer doubling, then re-pick predecessors --
+// needs a handful even for chains thousands of anchors deep, each round
+// parallel over anchors instead of one dependent 64-lane step per anchor.
+// A segment that does not settle in GIANT_IT rounds or violates the mark
+// bound is left to k_chain_long.
+constexpr int GIANT_MAX = 4096;   // anchors per segment, at most (4 per thread)
+constexpr int GIANT_B = 30;       // LDS per anchor: key 8 B, f/val/pprev/ptr/children 5 x 4 B, lo 2 B
+// segment capacity left beside the pen LUT in 160 KB of LDS (1 KB for statics)
+__host__ __device__ inline int giant_cap(int lut_n) {
+    const int c = (160 * 1024 - 1024 - (((lut_n * 2) + 15) & ~15)) / GIANT_B;
+    return (c < GIANT_MAX ? c : GIANT_MAX) & ~15;
+}
+constexpr int GIANT_IT = 32;
+constexpr int GIANT_PINS = 32;    // exactly evaluated anchors per segment before giving up
+constexpr int GIANT_MKW = 160;    // mark bitmap words (window <= max_iter 5000)
+__global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ uint32_t s_flag;
+    __shared__ unsigned long long s_best;
+    __shared__ uint32_t s_mk[GIANT_MKW];
+    __shared__ uint32_t s_red[16];
+    const ChainKParams P = a.P;
+    int16_t* lut = (int16_t*)smem;
+    const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
+    uint64_t* gk = (uint64_t*)(smem + lut_bytes);
+    const int gcap = giant_cap(P.lut_n);
+    int32_t* f0 = (int32_t*)(gk + gcap);
+    int32_t* f1 = f0 + gcap;
+    int32_t* gp = f1 + gcap;
+    int32_t* gptr = gp + gcap;
+    int32_t* gch = gptr + gcap;
+    uint16_t* glo = (uint16_t*)(gch + gcap);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < P.lut_n; i += 1024) lut[i] = a.lut[i];
+    __syncthreads();
+    const uint32_t qb = a.kl.qb, rb = a.kl.rb;
+    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
+    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    const uint32_t nl = min(*a.lseg_n, a.lseg_cap);
+    for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
+        const uint4 L = a.lseg[q];
+        const int32_t s = (int32_t)L.y, e = (int32_t)L.z, len = e - s;
+        if (len < (int32_t)a.giant_min || len > gcap) continue;
+        const uint32_t r = L.x;
+        const uint64_t base = a.a_off[r];
+        const uint64_t* K = a.keys + base;
+        for (int t = tid; t < len; t += 1024) { gk[t] = K[s + t]; f0[t] = span; }
+        __syncthreads();
+        // window start (lchain.rs:75-77): first j with p_i <= p_j + max_dist_x, and max_iter
+        for (int t = tid; t < len; t += 1024) {
+            const int32_t pi = (int32_t)((gk[t] >> qb) & rmask);
+            int32_t lo = 0, hi = t;            // first j in [0, t] with p_j >= p_i - maxdx
+            while (lo < hi) { const int32_t mid = (lo + hi) >> 1; if (pi > (int32_t)((uint32_t)((gk[mid] >> qb) & rmask) + (uint32_t)maxdx)) lo = mid + 1; else hi = mid; }
+            const int32_t l2 = lo > t - P.max_iter ? lo : t - P.max_iter;
+            glo[t] = (uint16_t)min(t - l2, 65535);
+        }
+        __syncthreads();
+        auto sc_of = [&](uint64_t ki, uint64_t kj, bool& ok) -> int32_t {   // comput_sc (lchain.rs:17-34)
+            const int32_t dq = (int32_t)(ki & qmask) - (int32_t)(kj & qmask);
+            const int32_t dr = (int32_t)((ki >> qb) & rmask) - (int32_t)((kj >> qb) & rmask);
+            const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+            ok = dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
+            const int32_t dg = dr < dq ? dr : dq;
+            return (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
+        };
+        // Rounds: Jacobi to convergence, then the mark-bound check.  The first
+        // anchor that fails it gets the reference loop exactly (one thread,
+        // marks in an LDS bitmap, its predecessors being exact already) and is
+        // pinned; the next round re-converges the anchors after it.
+        for (int t = tid; t < len; t += 1024) gp[t] = -1;
+        int32_t* fo = f0; int32_t* val = f1;
+        int dbl = 0;
+        while ((1 << dbl) < len) ++dbl;
+        bool ok_seg = false;
+        for (int round = 0; round < GIANT_PINS; ++round) {
+            // Policy iteration: evaluate the current predecessor forest exactly
+            // (pointer doubling, ceil(log2 len) rounds), then let every anchor
+            // re-pick its best predecessor (reference order, strict >) under
+            // those values.  Values never decrease; when no anchor's value
+            // changes they are the DP's fixed point and gp is its argmax.
+            bool conv = false;
+            for (int it = 0; it < GIANT_IT && !conv; ++it) {
+                for (int t = tid; t < len; t += 1024) {
+                    const int32_t p = gp[t];
+                    if ((glo[t] & 0x8000u) || p < 0) { val[t] = (glo[t] & 0x8000u) ? fo[t] : span; gptr[t] = -1; }
+                    else { bool ok; val[t] = sc_of(gk[t], gk[p], ok); gptr[t] = p; }
+                }
+                __syncthreads();
+                for (int d = 0; d < dbl; ++d) {
+                    int32_t nv[4], np[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int t = tid + k * 1024;
+                        if (t < len) {
+                            const int32_t p = gptr[t];
+                            nv[k] = p >= 0 ? val[t] + val[p] : val[t];
+                            np[k] = p >= 0 ? gptr[p] : -1;
+                        }
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int t = tid + k * 1024;
+                        if (t < len) { val[t] = nv[k]; gptr[t] = np[k]; }
+                    }
+                    __syncthreads();
+                }
+                if (tid == 0) s_flag = 0;
+                for (int t = tid; t < len; t += 1024) fo[t] = val[t];
+                __syncthreads();
+                uint32_t ch = 0;
+                for (int t = tid; t < len; t += 1024) {
+                    const uint32_t lw = glo[t];
+                    if (lw & 0x8000u) continue;          // pinned: exact already
+                    const uint64_t ki = gk[t];
+                    const int32_t lo = t - (int32_t)lw;
+                    int32_t mf = span, mj = -1;
+                    for (int32_t j = t - 1; j >= lo; --j) {
+                        bool ok;
+                        const int32_t sv = sc_of(ki, gk[j], ok) + fo[j];
+                        if (ok && sv > mf) { mf = sv; mj = j; }
+                    }
+                    gp[t] = mj;
+                    ch |= mf != fo[t] ? 1u : 0u;
+                }
+                if (ch) atomicOr(&s_flag, 1u);
+                __syncthreads();
+                conv = s_flag == 0;
+                __syncthreads();
+            }
+            if (!conv) {                         // k_chain_long runs it
+                if (a.lseg_prof && tid == 0) printf("[giant] len %d round %d: noconv\n", len, round);
+                break;
+            }
+            // Children lists of the converged forest: j is marked for i (t[j]
+            // == i) iff a valid c in (j, i) has pprev[c] == j.  gptr = child
+            // counts, val = list ends, gch = the lists.
+            for (int t = tid; t < len; t += 1024) gptr[t] = 0;
+            __syncthreads();
+            for (int t = tid; t < len; t += 1024) if (gp[t] >= 0) atomicAdd((uint32_t*)&gptr[gp[t]], 1u);
+            __syncthreads();
+            {
+                uint32_t c4[4], sum = 0, tot;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { const int t = tid * 4 + k; c4[k] = t < len ? (uint32_t)gptr[t] : 0u; sum += c4[k]; }
+                uint32_t ex = block_excl_sum(sum, tot, s_red);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { const int t = tid * 4 + k; if (t < len) val[t] = (int32_t)ex; ex += c4[k]; }
+            }
+            __syncthreads();
+            for (int t = tid; t < len; t += 1024) if (gp[t] >= 0) gch[atomicAdd((uint32_t*)&val[gp[t]], 1u)] = t;
+            // No break is possible where a window holds <= max_skip mark
+            // sources.  Elsewhere run the reference loop on the converged
+            // values: the first anchor where it disagrees is pinned below.
+            if (tid == 0) s_flag = 0x7fffffffu;
+            __syncthreads();
+            for (int t = tid; t < len; t += 1024) {
+                const uint32_t lw = glo[t];
+                if (lw & 0x8000u) continue;
+                const uint64_t ki = gk[t];
+                const int32_t lo = t - (int32_t)lw;
+                int32_t nmk = 0;
+                for (int32_t j = t - 1; j >= lo && nmk <= P.max_skip; --j) {
+                    bool ok;
+                    (void)sc_of(ki, gk[j], ok);
+                    nmk += (ok && gp[j] >= lo) ? 1 : 0;
+                }
+                if (nmk <= P.max_skip) continue;
+                int32_t mf = span, mj = -1, n_skip = 0;
+                for (int32_t j = t - 1; j >= lo; --j) {
+                    bool ok;
+                    const int32_t sv = sc_of(ki, gk[j], ok) + fo[j];
+                    if (!ok) continue;
+                    if (sv > mf) { mf = sv; mj = j; if (n_skip > 0) --n_skip; continue; }
+                    const int32_t ce = val[j];
+                    bool mk = false;
+                    for (int32_t c = ce - gptr[j]; c < ce && !mk; ++c) {
+                        const int32_t cj = gch[c];
+                        if (cj < t) { bool okc; (void)sc_of(ki, gk[cj], okc); mk = okc; }
+                    }
+                    if (mk && ++n_skip > P.max_skip) break;
+                }
+                if (mf != fo[t] || mj != gp[t]) atomicMin(&s_flag, (uint32_t)t);
+            }
+            __syncthreads();
+            const uint32_t tf = s_flag;
+            if (tf == 0x7fffffffu) {
+                if (a.lseg_prof && tid == 0) printf("[giant] len %d: settled after %d pins\n", len, round);
+                ok_seg = true;
+                break;
+            }
+            if (tid == 0) {   // the reference loop (lchain.rs:78-87) for anchor tf
+                const int32_t t = (int32_t)tf, lo = t - (int32_t)glo[t];
+                const int32_t nw = (t - lo + 31) >> 5;
+                for (int32_t w = 0; w < nw; ++w) s_mk[w] = 0;   // marks t[j] == i, j in [lo, t)
+                const uint64_t ki = gk[t];
+                int32_t mf = span, mj = -1, n_skip = 0;
+                for (int32_t j = t - 1; j >= lo; --j) {
+                    bool ok;
+                    const int32_t sv = sc_of(ki, gk[j], ok) + fo[j];
+                    if (!ok) continue;
+                    if (sv > mf) { mf = sv; mj = j; if (n_skip > 0) --n_skip; }
+                    else if ((s_mk[(j - lo) >> 5] >> ((j - lo) & 31)) & 1u) { if (++n_skip > P.max_skip) break; }
+                    const int32_t pj = gp[j];
+                    if (pj >= lo) s_mk[(pj - lo) >> 5] |= 1u << ((pj - lo) & 31);
+                }
+                fo[t] = mf; gp[t] = mj; glo[t] = (uint16_t)(glo[t] | 0x8000u);
+            }
+            __syncthreads();
+        }
+        if (a.lseg_prof && tid == 0) printf("[giant] len %d: %s\n", len, ok_seg ? "done" : "fallback");
+        if (!ok_seg) continue;
+        if (tid == 0) s_best = 0;
+        __syncthreads();
+        uint64_t pairs = 0;
+        for (int t = tid; t < len; t += 1024) { glo[t] &= 0x7fffu; pairs += glo[t]; }
+        int32_t* F = a.f + base; int32_t* PP = a.pp + base;
+        int32_t bf = INT_MIN, bi = -1;
+        for (int t = tid; t < len; t += 1024) {
+            F[s + t] = fo[t];
+            PP[s + t] = gp[t] >= 0 ? s + gp[t] : -1;
+            best_merge(bf, bi, fo[t], s + t);
+        }
+        if (bi >= 0) atomicMax(&s_best, best_key(bf, bi));
+        atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)pairs);
+        __syncthreads();
+        if (tid == 0) {
+            atomicMax(a.rbest + r, s_best);
+            a.lseg[q].w = LSEG_DONE;
+        }
+        __syncthreads();
     }
 }
 
@@ -2439,6 +2683,7 @@ static size_t chain_lds(int lut_n) {
     return (size_t)(((lut_n * 2) + 15) & ~15) + (size_t)DP_NW * (RING_WORDS * 4 + RK * 8 + RK * 8);
 }
 static size_t lut_lds(int lut_n) { return (size_t)(((lut_n * 2) + 15) & ~15); }
+static size_t giant_lds(int lut_n) { return lut_lds(lut_n) + (size_t)giant_cap(lut_n) * GIANT_B; }
 static size_t seg_lds(int lut_n) { return lut_lds(lut_n) + (size_t)DP_NW * (KRING * 8 + 3 * TQ * 5 + MEDB * 8); }
 int chain_max_blocks(int lut_n, int which) {
     int dev = 0, ncu = 0, per = 0;
@@ -2465,6 +2710,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 3: hipLaunchKernelGGL(k_chain_long, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a); break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
+    case 7: hipLaunchKernelGGL(k_chain_giant, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 3) / 4), dim3(256), 0, st, a); break;
     }
     LAUNCH_CHECK();

@@ -483,3 +483,17 @@ def test_cli_anchors_chain(small_world, tmp_path):
         args = [mm2rs, "chain", ref, reads] + ([] if bw == 5000 else ["-r", str(bw)])
         got = subprocess.run(args, check=True, capture_output=True, text=True).stdout
         assert got == want, bw
+
+
+@pytest.mark.parametrize("giant_min", [16, 200])
+def test_giant_segments_jacobi(dev, small_world, dense_world, giant_min):
+    """Long segments through k_chain_giant (policy iteration to the fixed point
+    of the no-break DP, the reference loop verified wherever a window holds
+    more than max_skip mark sources, k_chain_long when it does not settle):
+    every result field equals the debug run's (exact sequential DP), and PAF
+    equals the oracle's."""
+    os.environ["MM2G_GIANT_MIN"] = str(giant_min)
+    try:
+        _filter_transparent(dev, small_world, dense_world)
+    finally:
+        del os.environ["MM2G_GIANT_MIN"]
