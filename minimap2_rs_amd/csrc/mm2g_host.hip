@@ -635,8 +635,13 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
     ca.seg_chunk = (uint32_t)SEG_CHUNK;
-    ca.giant_min = 1024;
-    if (const char* e = getenv("MM2G_GIANT_MIN")) ca.giant_min = std::max(2, atoi(e));   // tests
+    // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
+    // settle in a few policy-iteration rounds; pass 0's long segments are real
+    // chains whose windows carry many mark sources, where k_chain_long is
+    // faster (measured: DESIGN.md section 7), so pass 0 leaves them to it.
+    const char* genv = getenv("MM2G_GIANT_MIN");   // tests: both passes
+    const uint32_t giant_min[2] = {genv ? (uint32_t)std::max(2, atoi(genv)) : 0xffffffffu,
+                                   genv ? (uint32_t)std::max(2, atoi(genv)) : 128u};
     if (const char* e = getenv("MM2G_SEG_CHUNK")) ca.seg_chunk = std::max(64u, (uint32_t)atoi(e) & ~63u);   // tests
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) {
@@ -667,7 +672,8 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         }
         ca.lseg_prof = env_on("MM2G_LSEG_PROF") ? 1u : 0u;
         for (int stg = 0; stg < 5; ++stg) {
-            if (stg == 2 && ca.lazy && !env_on("MM2G_NO_GIANT")) {   // giant segments as a Jacobi fixed point (production)
+            ca.giant_min = giant_min[pass];
+            if (stg == 2 && ca.lazy && ca.giant_min != 0xffffffffu && !env_on("MM2G_NO_GIANT")) {   // production only
                 ProfScope ps(c, pass ? "chain_giant_rescue" : "chain_giant");
                 LCHK(launch_chain_stage(7, ca, 256, c->stream));
             }

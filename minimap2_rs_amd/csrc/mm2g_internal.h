@@ -168,7 +168,7 @@ struct ChainArgs {
     uint32_t lazy;           // k_chain_long: skip deep windows no predecessor of which can beat max_f (not in debug mode)
     uint32_t* item_off;      // k_seg_items: first work item (chunk) of order[t]; [n] = total
     uint32_t seg_chunk;      // anchors per work item (multiple of 64; SEG_CHUNK)
-    uint32_t giant_min;      // long segments of at least this many anchors try k_chain_giant first (1024)
+    uint32_t giant_min;      // long segments of at least this many anchors try k_chain_giant first (rescue: 128)
 };
 struct DvArgs {
     uint32_t n;

@@ -1,0 +1,4 @@
+set -e
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
