@@ -163,8 +163,10 @@ def main():
     idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr,
                                     device=None if args.host_index else gpu)
     t_index = time.time() - t0
-    mid = max(idx.calc_mid_occ(2e-4), 10)       # main.rs:196-197
-    log(f"rank {rank}: index built ({'host' if args.host_index else 'GPU'}) in {t_index:.1f}s, stats {idx.stats()}, mid_occ {mid}")
+    t0 = time.time()
+    mid_host = idx.calc_mid_occ(2e-4)            # the reference's sort of all counts (index.rs:124-141)
+    t_mid_host = time.time() - t0
+    log(f"rank {rank}: index built ({'host' if args.host_index else 'GPU'}) in {t_index:.1f}s, stats {idx.stats()}")
 
     # ---- reads (per rank: distinct seed) -----------------------------------
     rbuf, roffs, _ = simdata.reads(gbuf, lens, args.reads, args.read_len, rank_read_seed(args.read_seed, rank))
@@ -174,10 +176,19 @@ def main():
     S = max(1, args.streams)
     devs = [M.Device(gpu) for _ in range(S)]
     t0 = time.time()
-    devs[0].upload_index(idx, mid)
+    devs[0].upload_index(idx, 10)
+    t_up = time.time() - t0
+    # mid_occ from the device table's count histogram, checked against the host's
+    t0 = time.time()
+    mid_dev = devs[0].index_mid_occ(2e-4)
+    t_mid_dev = time.time() - t0
+    if mid_dev != mid_host:
+        raise SystemExit(f"bench.py: device mid_occ {mid_dev} != host {mid_host}")
+    mid = max(mid_dev, 10)                       # main.rs:196-197
+    devs[0].set_mid_occ(mid)
     for d in devs[1:]:
         d.share_index(devs[0], mid)
-    t_up = time.time() - t0
+    log(f"rank {rank}: mid_occ {mid} (device {t_mid_dev * 1e3:.1f} ms, host sort {t_mid_host * 1e3:.0f} ms)")
     # contiguous shares of the batch, one per context; reads resident in HBM before timing
     cuts = share_cuts(args.reads, S)
     shards = []
@@ -335,6 +346,7 @@ def main():
                 "dp_pairs_per_s": dp_pairs_s,
                 "index_build_s": round(t_index, 3), "index_build_on": "host" if args.host_index else "gpu",
                 "index_upload_s": round(t_up, 3),
+                "mid_occ_device_ms": round(t_mid_dev * 1e3, 2), "mid_occ_host_sort_ms": round(t_mid_host * 1e3, 1),
                 "reads_h2d_ms": round(t_h2d * 1e3, 3),
                 "pcie_inclusive_gbases_s": round(n_bases / (ms_per_step / 1e3 + t_h2d) / 1e9, 6) if world == 1 else None,
                 "parity_vs_oracle": parity,

@@ -84,6 +84,12 @@ int mm2g_ctx_upload_index(mm2g_ctx* ctx, const mm2g_index* idx, int32_t mid_occ)
  * several contexts — one per host thread, each with its own stream and batch
  * buffers — map concurrently against one index in HBM. */
 int mm2g_ctx_share_index(mm2g_ctx* dst, const mm2g_ctx* src, int32_t mid_occ);
+/* Index::calc_mid_occ (src/index.rs:124-141) computed on the uploaded device
+ * table by a count histogram; equals
+ * mm2g_index_calc_mid_occ on the same index.  INT32_MAX when empty. */
+int mm2g_ctx_index_mid_occ(mm2g_ctx* ctx, float frac, int32_t* out);
+/* Replace the mid_occ given at upload/share (main.rs:196-197 clamp is the caller's). */
+int mm2g_ctx_set_mid_occ(mm2g_ctx* ctx, int32_t mid_occ);
 
 /* Mapping options: `mm2rs align` flags (src/main.rs:55-89) and the chain
  * parameters they drive (default_chain_params, src/main.rs:105-123). */

@@ -78,6 +78,8 @@ SIGNATURES = {
     "mm2g_prof_reset": (C.c_int, [_VP]),
     "mm2g_debug_chain_stats": (C.c_int64, [_VP, C.POINTER(C.c_uint32), C.c_uint32]),
     "mm2g_ctx_share_index": (C.c_int, [_VP, _VP, C.c_int32]),
+    "mm2g_ctx_index_mid_occ": (C.c_int, [_VP, C.c_float, _PI32]),
+    "mm2g_ctx_set_mid_occ": (C.c_int, [_VP, C.c_int32]),
     "mm2g_batch_counters": (C.c_int, [_VP, _P64, C.c_int]),
 }
 

@@ -189,6 +189,16 @@ class Device:
         check(load().mm2g_ctx_share_index(self._h, other._h, mid_occ), "share_index")
         self.index = other.index
 
+    def index_mid_occ(self, frac: float) -> int:
+        """``Index::calc_mid_occ`` (index.rs:124-141) on the uploaded device
+        table (count histogram); equals :meth:`Index.calc_mid_occ`."""
+        out = C.c_int32()
+        check(load().mm2g_ctx_index_mid_occ(self._h, frac, C.byref(out)), "index_mid_occ")
+        return out.value
+
+    def set_mid_occ(self, mid_occ: int) -> None:
+        check(load().mm2g_ctx_set_mid_occ(self._h, mid_occ), "set_mid_occ")
+
     def set_reads(self, seqs: Sequence[bytes]) -> None:
         offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
         if seqs:

@@ -407,6 +407,60 @@ int mm2g_ctx_share_index(mm2g_ctx* dst, const mm2g_ctx* src, int32_t mid_occ) {
     return 0;
 }
 
+// Index::calc_mid_occ (src/index.rs:124-141) from the uploaded device table
+// (SURVEY.md §8f row 2): a histogram of per-key occurrence counts instead of the
+// reference's sort of all of them; counts at or above the last bin are gathered
+// and sorted only if the quantile lands among them.
+int mm2g_ctx_index_mid_occ(mm2g_ctx* c, float frac, int32_t* out) {
+    if (!c || !out) return set_err(MM2G_E_ARG, "null argument");
+    if (!c->have_index) return set_err(MM2G_E_STATE, "no index uploaded");
+    HIPCHK(hipSetDevice(c->device));
+    uint32_t nbins = 4096;
+    if (const char* e = getenv("MM2G_MIDHIST_BINS")) nbins = (uint32_t)std::max(2, std::min(16384, atoi(e)));   // tests
+    const uint64_t cap = 1ULL << c->log2cap;
+    const IxEntry* tab = (const IxEntry*)c->dix->tab.p;
+    DevBuf dh, dn, dv;
+    unsigned long long* hist; uint32_t* n_ovf;
+    ENSURE(dh, unsigned long long, nbins, hist);
+    ENSURE(dn, uint32_t, 1, n_ovf);
+    HIPCHK(hipMemsetAsync(hist, 0, (size_t)nbins * 8, c->stream));
+    HIPCHK(hipMemsetAsync(n_ovf, 0, 4, c->stream));
+    LCHK(launch_mid_hist(tab, cap, nbins, hist, nullptr, 0, n_ovf, c->stream));
+    std::vector<unsigned long long> h(nbins);
+    uint32_t no = 0;
+    HIPCHK(hipMemcpyAsync(h.data(), hist, (size_t)nbins * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&no, n_ovf, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    uint64_t n = no;
+    for (auto v : h) n += v;
+    if (n == 0) { *out = INT32_MAX; return 0; }
+    const double f = (1.0 - (double)frac) * (double)n;
+    uint64_t i = f <= 0.0 ? 0 : (uint64_t)f;
+    if (i > n - 1) i = n - 1;
+    uint64_t run = 0;
+    for (uint32_t v = 0; v < nbins; ++v) {
+        if (i < run + h[v]) { *out = (int32_t)v + 1; return 0; }
+        run += h[v];
+    }
+    uint32_t* ovf;
+    ENSURE(dv, uint32_t, no, ovf);
+    HIPCHK(hipMemsetAsync(hist, 0, (size_t)nbins * 8, c->stream));
+    HIPCHK(hipMemsetAsync(n_ovf, 0, 4, c->stream));
+    LCHK(launch_mid_hist(tab, cap, nbins, hist, ovf, no, n_ovf, c->stream));
+    std::vector<uint32_t> ov(no);
+    if (no) HIPCHK(hipMemcpyAsync(ov.data(), ovf, (size_t)no * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::nth_element(ov.begin(), ov.begin() + (i - run), ov.end());
+    *out = (int32_t)ov[i - run] + 1;
+    return 0;
+}
+
+int mm2g_ctx_set_mid_occ(mm2g_ctx* c, int32_t mid_occ) {
+    if (!c) return set_err(MM2G_E_ARG, "null argument");
+    c->mid_occ = mid_occ;
+    return 0;
+}
+
 // ------------------------------------------------------------------ batch
 void mm2g_map_opts_default(mm2g_map_opts* o) {
     o->w = 10; o->k = 15; o->max_gap = 5000; o->bw = 500; o->bw_long = 20000;

@@ -11,6 +11,11 @@
 #include <thread>
 #include <atomic>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 namespace mm2g {
 
 // ------------------------------------------------------------------ FASTA
@@ -331,24 +336,48 @@ int32_t HostIndex::calc_mid_occ(float frac) const {
     return (int32_t)c[i] + 1;
 }
 
+static int load_threads() {
+    if (const char* e = getenv("MM2G_LOAD_THREADS")) return std::max(1, atoi(e));
+    return (int)std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+}
+
+// The device table's input: per key (minier, first position, count) and the
+// positions, buckets in order.  Per-bucket prefix sums, then threads fill
+// disjoint slices.
 void HostIndex::flatten(std::vector<uint64_t>& keys, std::vector<uint32_t>& offs, std::vector<uint32_t>& ns, std::vector<uint64_t>& pos) const {
-    keys.clear(); offs.clear(); ns.clear(); pos.clear();
-    size_t nk = 0, np = 0;
-    for (const auto& bk : B) { nk += bk.h.size(); for (const auto& e : bk.h) np += (e.first & 1) ? 1 : (size_t)(e.second & 0xffffffffULL); }
-    keys.reserve(nk); offs.reserve(nk); ns.reserve(nk); pos.reserve(np);
-    for (size_t t = 0; t < B.size(); ++t) {
-        const HostBucket& bk = B[t];
-        for (const auto& e : bk.h) {
-            keys.push_back(((e.first >> 1) << b) | (uint64_t)t);
-            offs.push_back((uint32_t)pos.size());
-            if (e.first & 1) { ns.push_back(1); pos.push_back(e.second); }
-            else {
-                const size_t o = (size_t)(e.second >> 32), c = (size_t)(e.second & 0xffffffffULL);
-                ns.push_back((uint32_t)c);
-                for (size_t i = 0; i < c; ++i) pos.push_back(bk.p[o + i]);
+    const size_t nb = B.size();
+    std::vector<size_t> ko(nb + 1, 0), po(nb + 1, 0);
+    for (size_t t = 0; t < nb; ++t) {
+        size_t np = 0;
+        for (const auto& e : B[t].h) np += (e.first & 1) ? 1 : (size_t)(e.second & 0xffffffffULL);
+        ko[t + 1] = ko[t] + B[t].h.size();
+        po[t + 1] = po[t] + np;
+    }
+    keys.resize(ko[nb]); offs.resize(ko[nb]); ns.resize(ko[nb]); pos.resize(po[nb]);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t t; (t = next.fetch_add(1)) < nb;) {
+            const HostBucket& bk = B[t];
+            size_t kq = ko[t], pq = po[t];
+            for (const auto& e : bk.h) {
+                keys[kq] = ((e.first >> 1) << b) | (uint64_t)t;
+                offs[kq] = (uint32_t)pq;
+                if (e.first & 1) { ns[kq] = 1; pos[pq++] = e.second; }
+                else {
+                    const size_t o = (size_t)(e.second >> 32), c = (size_t)(e.second & 0xffffffffULL);
+                    ns[kq] = (uint32_t)c;
+                    memcpy(pos.data() + pq, bk.p.data() + o, c * 8);
+                    pq += c;
+                }
+                ++kq;
             }
         }
-    }
+    };
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)load_threads(), nb));
+    std::vector<std::thread> th;
+    for (int i = 1; i < nt; ++i) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
 }
 
 // ------------------------------------------------------------------ MMI v2
@@ -383,13 +412,28 @@ bool save_mmi(const HostIndex& idx, const char* path, std::string& err) {
     return ok;
 }
 
+// load_from_mmi (src/index.rs:361-424).  The reference reads word by word;
+// here the file is mapped, a sequential walk records where each bucket starts
+// (two words per bucket), and threads then copy, sort and de-duplicate the
+// buckets' tables independently.
 bool load_mmi(const char* path, HostIndex& idx, std::string& err) {
-    FILE* f = fopen(path, "rb");
-    if (!f) { err = std::string("cannot open ") + path; return false; }
-    std::vector<char> iobuf(1 << 22);
-    setvbuf(f, iobuf.data(), _IOFBF, iobuf.size());
-    auto rd = [&](void* p, size_t n) { return fread(p, 1, n, f) == n; };
-    auto fail = [&](const char* m) { err = m; fclose(f); return false; };
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) { err = std::string("cannot open ") + path; return false; }
+    struct stat st;
+    if (fstat(fd, &st) != 0) { close(fd); err = std::string("cannot stat ") + path; return false; }
+    const size_t fsz = (size_t)st.st_size;
+    const uint8_t* m = nullptr;
+    if (fsz) {
+        void* mp = mmap(nullptr, fsz, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (mp == MAP_FAILED) { close(fd); err = std::string("cannot map ") + path; return false; }
+        m = (const uint8_t*)mp;
+        madvise(mp, fsz, MADV_WILLNEED);
+    }
+    close(fd);
+    struct Unmap { const uint8_t* m; size_t n; ~Unmap() { if (m) munmap((void*)m, n); } } um{m, fsz};
+    size_t cur = 0;
+    auto rd = [&](void* p, size_t n) { if (fsz - cur < n) return false; memcpy(p, m + cur, n); cur += n; return true; };
+    auto fail = [&](const char* msg) { err = msg; return false; };
     char magic[4];
     if (!rd(magic, 4) || memcmp(magic, "MMI\x02", 4) != 0) return fail("invalid MMI magic");
     uint32_t hdr[5];
@@ -409,20 +453,38 @@ bool load_mmi(const char* path, HostIndex& idx, std::string& err) {
         idx.seq.push_back(std::move(s));
     }
     const size_t nb = (size_t)1 << idx.b;
-    idx.B.assign(nb, HostBucket());
+    std::vector<size_t> at(nb);                    // file offset of bucket i's `n`
     for (size_t i = 0; i < nb; ++i) {
-        HostBucket& bk = idx.B[i];
-        uint32_t n;
+        at[i] = cur;
+        uint32_t n, sz;
         if (!rd(&n, 4)) return fail("truncated MMI bucket");
-        bk.p.resize(n);
-        if (n && !rd(bk.p.data(), 8 * (size_t)n)) return fail("truncated MMI positions");
-        uint32_t sz;
+        if (fsz - cur < 8 * (size_t)n) return fail("truncated MMI positions");
+        cur += 8 * (size_t)n;
         if (!rd(&sz, 4)) return fail("truncated MMI bucket size");
-        if (sz > 0) {
+        if ((fsz - cur) / 16 < (size_t)sz) return fail("truncated MMI hash table");
+        cur += 16 * (size_t)sz;
+    }
+    const size_t words = (size_t)((sum + 7) / 8);
+    if ((fsz - cur) / 4 < words) return fail("truncated MMI packed sequence");
+    idx.S.resize(words);
+    if (words) memcpy(idx.S.data(), m + cur, 4 * words);
+    idx.B.assign(nb, HostBucket());
+    std::atomic<size_t> next{0};
+    std::atomic<bool> bad{false};
+    auto work = [&]() {
+        for (size_t i; (i = next.fetch_add(1)) < nb && !bad.load(std::memory_order_relaxed);) {
+            HostBucket& bk = idx.B[i];
+            const uint8_t* q = m + at[i];
+            uint32_t n, sz;
+            memcpy(&n, q, 4); q += 4;
+            bk.p.resize(n);
+            if (n) memcpy(bk.p.data(), q, 8 * (size_t)n);
+            q += 8 * (size_t)n;
+            memcpy(&sz, q, 4); q += 4;
+            if (!sz) continue;
             bk.has_h = true;
             bk.h.resize(sz);
-            for (uint32_t j = 0; j < sz; ++j)
-                if (!rd(&bk.h[j].first, 8) || !rd(&bk.h[j].second, 8)) return fail("truncated MMI hash table");
+            memcpy((void*)bk.h.data(), q, 16 * (size_t)sz);
             std::stable_sort(bk.h.begin(), bk.h.end(), [](const std::pair<uint64_t, uint64_t>& x, const std::pair<uint64_t, uint64_t>& y) { return x.first < y.first; });
             // HashMap::insert semantics: a later duplicate key overwrites an earlier one
             size_t o = 0;
@@ -432,13 +494,15 @@ bool load_mmi(const char* path, HostIndex& idx, std::string& err) {
             }
             bk.h.resize(o);
             for (const auto& e : bk.h)
-                if (!(e.first & 1) && (e.second >> 32) + (e.second & 0xffffffffULL) > bk.p.size()) return fail("MMI multi entry out of range");
+                if (!(e.first & 1) && (e.second >> 32) + (e.second & 0xffffffffULL) > bk.p.size()) bad = true;
         }
-    }
-    const size_t words = (size_t)((sum + 7) / 8);
-    idx.S.assign(words, 0u);
-    if (words && !rd(idx.S.data(), 4 * words)) return fail("truncated MMI packed sequence");
-    fclose(f);
+    };
+    const int nt = (int)std::min<size_t>((size_t)load_threads(), nb);
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    if (bad) return fail("MMI multi entry out of range");
     return true;
 }
 

@@ -198,4 +198,6 @@ int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStr
 int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st);
 int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, hipStream_t st);
+int launch_mid_hist(const mm2g::IxEntry* tab, uint64_t cap, uint32_t nbins, unsigned long long* hist, uint32_t* ovf, uint32_t ovf_cap,
+                    uint32_t* ovf_n, hipStream_t st);
 int launch_ix_build(const uint64_t* keys, const uint32_t* offs, const uint32_t* ns, uint64_t nk, mm2g::IxEntry* tab, uint32_t log2cap, hipStream_t st);

@@ -2636,6 +2636,36 @@ __global__ void k_ix_build(const uint64_t* keys, const uint32_t* offs, const uin
     }
 }
 
+// calc_mid_occ (src/index.rs:124-141) on the device table: a histogram of the
+// per-key occurrence counts (1 for a Single) below `nbins`, plus the counts at
+// or above it (`ovf`, gathered only when the quantile falls there).  Singletons
+// dominate, so count == 1 is tallied per wave by ballot.
+__global__ __launch_bounds__(256) void k_mid_hist(const IxEntry* tab, uint64_t cap, uint32_t nbins, unsigned long long* hist,
+                                                  uint32_t* ovf, uint32_t ovf_cap, uint32_t* ovf_n) {
+    extern __shared__ uint32_t sh[];
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) sh[i] = 0;
+    __syncthreads();
+    uint32_t ones = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < cap; b0 += stride) {   // block-uniform trips
+        const uint64_t t = b0 + threadIdx.x;
+        bool one = false;
+        if (t < cap && tab[t].key != U64MAX) {
+            const uint32_t n = tab[t].n;
+            one = n == 1;
+            if (n < nbins) { if (!one) atomicAdd(&sh[n], 1u); }
+            else if (ovf) { const uint32_t q = atomicAdd(ovf_n, 1u); if (q < ovf_cap) ovf[q] = n; }
+            else atomicAdd(ovf_n, 1u);
+        }
+        const uint64_t m = ballot(one);
+        if (lane_id() == 0) ones += (uint32_t)__popcll(m);
+    }
+    if (lane_id() == 0 && ones && nbins > 1) atomicAdd(&sh[1], ones);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x)
+        if (sh[i]) atomicAdd(hist + i, (unsigned long long)sh[i]);
+}
+
 // ---------------------------------------------------------------- launchers
 #define LAUNCH_CHECK() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 
@@ -2730,6 +2760,16 @@ int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, in
 int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, hipStream_t st) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_mz_base, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, base, end);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_mid_hist(const IxEntry* tab, uint64_t cap, uint32_t nbins, unsigned long long* hist, uint32_t* ovf, uint32_t ovf_cap,
+                    uint32_t* ovf_n, hipStream_t st) {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+    const uint64_t want = (cap + 255) / 256;
+    const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ncu * 8));
+    hipLaunchKernelGGL(k_mid_hist, dim3(blocks), dim3(256), nbins * 4, st, tab, cap, nbins, hist, ovf, ovf_cap, ovf_n);
     LAUNCH_CHECK();
     return 0;
 }

@@ -131,13 +131,15 @@ int main(int argc, char** argv) {
                                                      : mm2g_index_build_fasta(ref.c_str(), w, k, 14, hpc ? 1 : 0, threads, &idx);
     }
     if (st != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
-    int32_t mid_occ;
-    mm2g_index_calc_mid_occ(idx, frac, &mid_occ);
-    if (mid_occ < 10) mid_occ = 10;                        // main.rs:197
+    // calc_mid_occ (main.rs:196-197) on the device table once it is uploaded
+    int32_t mid_occ = 10;
     mm2g_ctx* ctx = nullptr;
-    if (mm2g_ctx_create(device, &ctx) != 0 || mm2g_ctx_upload_index(ctx, idx, mid_occ) != 0) {
+    if (mm2g_ctx_create(device, &ctx) != 0 || mm2g_ctx_upload_index(ctx, idx, mid_occ) != 0 ||
+        mm2g_ctx_index_mid_occ(ctx, frac, &mid_occ) != 0) {
         fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1;
     }
+    if (mid_occ < 10) mid_occ = 10;                        // main.rs:197
+    mm2g_ctx_set_mid_occ(ctx, mid_occ);
     if (dbg_cmd) {   // anchors / chain of the first read (read_fasta_first, main.rs:92-103)
         mm2g::SeqStream in; std::string err;
         mm2g::FastaRecord rec;

@@ -131,3 +131,60 @@ def test_host_index_params(world, tmp_path, w, k, flag):
     oi.save_mmi(p2)
     assert open(p1, "rb").read() == open(p2, "rb").read()
     assert idx.calc_mid_occ(2e-4) == oi.mid_occ(2e-4)
+
+
+def _mmi_rewrite(src: bytes, fn) -> bytes:
+    """Re-emit an .mmi (index.rs:233-307 layout) with each bucket's hash
+    table passed through fn(list of (key, val)) -> list."""
+    import struct
+    o = 4
+    w, k, b, n_seq, flag = struct.unpack_from("<5I", src, o); o += 20
+    for _ in range(n_seq):
+        nl = src[o]; o += 1 + nl + 4
+    out = bytearray(src[:o])
+    for _ in range(1 << b):
+        (n,) = struct.unpack_from("<I", src, o)
+        out += src[o:o + 4 + 8 * n]; o += 4 + 8 * n
+        (sz,) = struct.unpack_from("<I", src, o); o += 4
+        ents = [struct.unpack_from("<QQ", src, o + 16 * j) for j in range(sz)]
+        o += 16 * sz
+        ents = fn(ents)
+        out += struct.pack("<I", len(ents))
+        for e in ents:
+            out += struct.pack("<QQ", *e)
+    out += src[o:]
+    return bytes(out)
+
+
+def test_mmi_load_mapped_parallel(world, tmp_path, monkeypatch):
+    """load_from_mmi (index.rs:361-424) via the mapped, bucket-parallel loader:
+    HashMap iteration order in the file does not matter, a later duplicate key
+    overwrites an earlier one (HashMap::insert), any thread count gives the
+    same index, and every truncation is an MM2G_E_IO error."""
+    idx = M.Index.build_index_from_fasta(world["ref_path"], world["w"], world["k"], world["b"], 0, 2)
+    p = str(tmp_path / "a.mmi")
+    idx.save_to_mmi(p)
+    raw = open(p, "rb").read()
+    rev = tmp_path / "rev.mmi"
+    rev.write_bytes(_mmi_rewrite(raw, lambda e: e[::-1]))
+    # duplicate: the first entry of each table again, with a bogus value first
+    dup = tmp_path / "dup.mmi"
+    dup.write_bytes(_mmi_rewrite(raw, lambda e: ([(e[0][0], 1 | 0)] + e) if e and (e[0][0] & 1) else e))
+    want = [idx.get(g["key"]) for g in world["gets"]]
+    for path in (p, str(rev), str(dup)):
+        for thr in ("1", "5"):
+            monkeypatch.setenv("MM2G_LOAD_THREADS", thr)
+            back = M.Index.load_from_mmi(path)
+            assert tuple(back.stats()) == tuple(idx.stats())
+            assert [back.get(g["key"]) for g in world["gets"]] == want
+            for fr, mo in world["calc_mid_occ"].items():
+                assert back.calc_mid_occ(float(fr)) == mo
+            q = str(tmp_path / "re.mmi")
+            back.save_to_mmi(q)
+            assert open(q, "rb").read() == raw
+    monkeypatch.delenv("MM2G_LOAD_THREADS")
+    cut = tmp_path / "cut.mmi"
+    for n in (3, 20, 30, len(raw) // 3, len(raw) // 2, len(raw) - 1):
+        cut.write_bytes(raw[:n])
+        with pytest.raises(RuntimeError):
+            M.Index.load_from_mmi(str(cut))

@@ -497,3 +497,18 @@ def test_giant_segments_jacobi(dev, small_world, dense_world, giant_min):
         _filter_transparent(dev, small_world, dense_world)
     finally:
         del os.environ["MM2G_GIANT_MIN"]
+
+
+@pytest.mark.parametrize("bins", [None, "2", "3", "64"])
+def test_device_mid_occ(dev, small_world, dense_world, monkeypatch, bins):
+    """calc_mid_occ (index.rs:124-141) from the device table's count histogram
+    equals the host's sort of all counts, at quantiles inside the histogram and
+    in its overflow (few bins force the gathered-overflow path)."""
+    if bins:
+        monkeypatch.setenv("MM2G_MIDHIST_BINS", bins)
+    for ref in (small_world[0], dense_world[0]):
+        idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+        dev.upload_index(idx, 10)
+        for fr in (0.0, 2e-4, 1e-3, 0.01, 0.1, 0.5, 0.9, 1.0, 1.5, -0.25):
+            assert dev.index_mid_occ(fr) == idx.calc_mid_occ(fr), (ref, fr)
+    dev.set_mid_occ(10)
