@@ -817,7 +817,7 @@ constexpr uint32_t SEG_TINY = 16;        // segments up to this length: ranked b
 constexpr uint32_t SEG_RANK = 2048;      // up to this: block-wide rank count; beyond: radix
 constexpr int BIG_MAX = 128;             // larger segments listed per read (more: radix over the read)
 constexpr int GOFF_LDS = 256;            // group offsets staged in LDS when 2 * n_seq + 2 fits
-constexpr int SORT_LDS = 150 * 1024;     // dynamic LDS of k_sort_read (one workgroup per CU)
+constexpr int SORT_LDS = 157 * 1024;     // dynamic LDS of k_sort_read (one workgroup per CU; 2.4 KB static)
 
 // 8 independent loads per thread, then fn(i, x) for each (i < n): hides HBM
 // latency in the block-wide passes of k_sort_read
