@@ -75,6 +75,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
+    DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
     DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
@@ -727,9 +728,22 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         ca.lseg_prof = env_on("MM2G_LSEG_PROF") ? 1u : 0u;
         for (int stg = 0; stg < 5; ++stg) {
             ca.giant_min = giant_min[pass];
-            if (stg == 2 && ca.lazy && ca.giant_min != 0xffffffffu && !env_on("MM2G_NO_GIANT")) {   // production only
+            // production only; the pin bitmap and the lo field bound the window (max_iter <= 5120)
+            if (stg == 2 && ca.lazy && ca.giant_min != 0xffffffffu && ca.P.max_iter <= 5120 && !env_on("MM2G_NO_GIANT")) {
                 ProfScope ps(c, pass ? "chain_giant_rescue" : "chain_giant");
+                if (const char* e = getenv("MM2G_GIANT_LCAP")) ca.giant_lcap = (uint32_t)std::max(16, atoi(e)) & ~15u;   // tests
                 LCHK(launch_chain_stage(7, ca, 256, c->stream));
+                // longer segments from a per-workgroup HBM slice (100 kb reads' rescue)
+                uint32_t gmax = 65536;
+                if (const char* e = getenv("MM2G_GIANT_GMAX")) gmax = (uint32_t)std::max(0, atoi(e)) & ~15u;
+                if (gmax) {
+                    const int gblocks = 128;
+                    unsigned char* scr;
+                    ENSURE(c->giant_scr, unsigned char, (size_t)gblocks * gmax * 38, scr);
+                    ca.giant_scr = scr;
+                    ca.giant_gmax = gmax;
+                    LCHK(launch_chain_stage(8, ca, gblocks, c->stream));
+                }
             }
             ProfScope ps(c, names[pass][stg]);
             LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));

@@ -169,6 +169,9 @@ struct ChainArgs {
     uint32_t* item_off;      // k_seg_items: first work item (chunk) of order[t]; [n] = total
     uint32_t seg_chunk;      // anchors per work item (multiple of 64; SEG_CHUNK)
     uint32_t giant_min;      // long segments of at least this many anchors try k_chain_giant first (rescue: 128)
+    uint32_t giant_lcap;     // tests: cap of the LDS variant below its LDS capacity (0 = none)
+    uint32_t giant_gmax;     // global variant: anchors per workgroup scratch slice (0 = off)
+    void* giant_scr;         // global variant scratch: grid x giant_gmax x 38 B
 };
 struct DvArgs {
     uint32_t n;

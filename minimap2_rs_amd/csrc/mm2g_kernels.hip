@@ -2187,9 +2187,14 @@ __host__ __device__ inline int giant_cap(int lut_n) {
     const int c = (160 * 1024 - 1024 - (((lut_n * 2) + 15) & ~15)) / GIANT_B;
     return (c < GIANT_MAX ? c : GIANT_MAX) & ~15;
 }
+constexpr int GIANT_GB = 38;      // HBM scratch per anchor (global variant): + ping-pong val/ptr 2 x 4 B
 constexpr int GIANT_IT = 32;
 constexpr int GIANT_PINS = 32;    // exactly evaluated anchors per segment before giving up
 constexpr int GIANT_MKW = 160;    // mark bitmap words (window <= max_iter 5000)
+// G = false: the segment lives in LDS (len <= giant_cap).  G = true: longer
+// segments (the 100 kb rescue's) in a per-workgroup HBM/L2 scratch slice of
+// a.giant_gmax anchors; same algorithm, pointer doubling by ping-pong.
+template <bool G>
 __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ uint32_t s_flag;
@@ -2199,14 +2204,18 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
     const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
-    uint64_t* gk = (uint64_t*)(smem + lut_bytes);
-    const int gcap = giant_cap(P.lut_n);
-    int32_t* f0 = (int32_t*)(gk + gcap);
-    int32_t* f1 = f0 + gcap;
-    int32_t* gp = f1 + gcap;
-    int32_t* gptr = gp + gcap;
-    int32_t* gch = gptr + gcap;
-    uint16_t* glo = (uint16_t*)(gch + gcap);
+    const int gcap = a.giant_lcap ? min(giant_cap(P.lut_n), (int)a.giant_lcap) : giant_cap(P.lut_n);
+    const int cap = G ? (int)a.giant_gmax : gcap;
+    unsigned char* arr = G ? (unsigned char*)a.giant_scr + (size_t)blockIdx.x * (size_t)cap * GIANT_GB : smem + lut_bytes;
+    uint64_t* gk = (uint64_t*)arr;
+    int32_t* f0 = (int32_t*)(gk + cap);
+    int32_t* f1 = f0 + cap;
+    int32_t* gp = f1 + cap;
+    int32_t* gptr = gp + cap;
+    int32_t* gch = gptr + cap;
+    uint16_t* glo = (uint16_t*)(gch + cap);
+    int32_t* val2 = (int32_t*)(glo + cap);      // G only
+    int32_t* gptr2 = val2 + cap;
     const int tid = threadIdx.x;
     for (int i = tid; i < P.lut_n; i += 1024) lut[i] = a.lut[i];
     __syncthreads();
@@ -2217,7 +2226,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
     for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
         const uint4 L = a.lseg[q];
         const int32_t s = (int32_t)L.y, e = (int32_t)L.z, len = e - s;
-        if (len < (int32_t)a.giant_min || len > gcap) continue;
+        if (G ? (len <= gcap || len > cap) : (len < (int32_t)a.giant_min || len > gcap)) continue;
         const uint32_t r = L.x;
         const uint64_t base = a.a_off[r];
         const uint64_t* K = a.keys + base;
@@ -2263,27 +2272,43 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                     else { bool ok; val[t] = sc_of(gk[t], gk[p], ok); gptr[t] = p; }
                 }
                 __syncthreads();
-                for (int d = 0; d < dbl; ++d) {
-                    int32_t nv[4], np[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int t = tid + k * 1024;
-                        if (t < len) {
-                            const int32_t p = gptr[t];
-                            nv[k] = p >= 0 ? val[t] + val[p] : val[t];
-                            np[k] = p >= 0 ? gptr[p] : -1;
+                const int32_t* vres = val;
+                if constexpr (G) {
+                    int32_t *v0 = val, *p0 = gptr, *v1 = val2, *p1 = gptr2;
+                    for (int d = 0; d < dbl; ++d) {
+                        for (int t = tid; t < len; t += 1024) {
+                            const int32_t p = p0[t];
+                            v1[t] = p >= 0 ? v0[t] + v0[p] : v0[t];
+                            p1[t] = p >= 0 ? p0[p] : -1;
                         }
+                        __syncthreads();
+                        int32_t* tv = v0; v0 = v1; v1 = tv;
+                        int32_t* tp = p0; p0 = p1; p1 = tp;
                     }
-                    __syncthreads();
+                    vres = v0;
+                } else {
+                    for (int d = 0; d < dbl; ++d) {
+                        int32_t nv[4], np[4];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int t = tid + k * 1024;
-                        if (t < len) { val[t] = nv[k]; gptr[t] = np[k]; }
+                        for (int k = 0; k < 4; ++k) {
+                            const int t = tid + k * 1024;
+                            if (t < len) {
+                                const int32_t p = gptr[t];
+                                nv[k] = p >= 0 ? val[t] + val[p] : val[t];
+                                np[k] = p >= 0 ? gptr[p] : -1;
+                            }
+                        }
+                        __syncthreads();
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int t = tid + k * 1024;
+                            if (t < len) { val[t] = nv[k]; gptr[t] = np[k]; }
+                        }
+                        __syncthreads();
                     }
-                    __syncthreads();
                 }
                 if (tid == 0) s_flag = 0;
-                for (int t = tid; t < len; t += 1024) fo[t] = val[t];
+                for (int t = tid; t < len; t += 1024) fo[t] = vres[t];
                 __syncthreads();
                 uint32_t ch = 0;
                 for (int t = tid; t < len; t += 1024) {
@@ -2316,13 +2341,14 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
             __syncthreads();
             for (int t = tid; t < len; t += 1024) if (gp[t] >= 0) atomicAdd((uint32_t*)&gptr[gp[t]], 1u);
             __syncthreads();
-            {
+            for (int c0 = 0, carry = 0; c0 < len; c0 += 4096) {   // exclusive scan, 4096 per pass
                 uint32_t c4[4], sum = 0, tot;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) { const int t = tid * 4 + k; c4[k] = t < len ? (uint32_t)gptr[t] : 0u; sum += c4[k]; }
-                uint32_t ex = block_excl_sum(sum, tot, s_red);
+                for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; c4[k] = t < len ? (uint32_t)gptr[t] : 0u; sum += c4[k]; }
+                uint32_t ex = block_excl_sum(sum, tot, s_red) + (uint32_t)carry;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) { const int t = tid * 4 + k; if (t < len) val[t] = (int32_t)ex; ex += c4[k]; }
+                for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; if (t < len) val[t] = (int32_t)ex; ex += c4[k]; }
+                carry += (int)tot;
             }
             __syncthreads();
             for (int t = tid; t < len; t += 1024) if (gp[t] >= 0) gch[atomicAdd((uint32_t*)&val[gp[t]], 1u)] = t;
@@ -2740,7 +2766,8 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 3: hipLaunchKernelGGL(k_chain_long, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a); break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
-    case 7: hipLaunchKernelGGL(k_chain_giant, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
+    case 7: hipLaunchKernelGGL(k_chain_giant<false>, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
+    case 8: hipLaunchKernelGGL(k_chain_giant<true>, dim3(blocks), dim3(1024), lut_lds(a.P.lut_n), st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 3) / 4), dim3(256), 0, st, a); break;
     }
     LAUNCH_CHECK();

@@ -485,18 +485,18 @@ def test_cli_anchors_chain(small_world, tmp_path):
         assert got == want, bw
 
 
-@pytest.mark.parametrize("giant_min", [16, 200])
-def test_giant_segments_jacobi(dev, small_world, dense_world, giant_min):
+@pytest.mark.parametrize("giant_min,lcap", [(16, None), (200, None), (16, "64")])
+def test_giant_segments_jacobi(dev, small_world, dense_world, monkeypatch, giant_min, lcap):
     """Long segments through k_chain_giant (policy iteration to the fixed point
     of the no-break DP, the reference loop verified wherever a window holds
     more than max_skip mark sources, k_chain_long when it does not settle):
     every result field equals the debug run's (exact sequential DP), and PAF
-    equals the oracle's."""
-    os.environ["MM2G_GIANT_MIN"] = str(giant_min)
-    try:
-        _filter_transparent(dev, small_world, dense_world)
-    finally:
-        del os.environ["MM2G_GIANT_MIN"]
+    equals the oracle's.  lcap 64 sends every segment over 64 anchors to the
+    HBM-scratch variant (k_chain_giant<true>)."""
+    monkeypatch.setenv("MM2G_GIANT_MIN", str(giant_min))
+    if lcap:
+        monkeypatch.setenv("MM2G_GIANT_LCAP", lcap)
+    _filter_transparent(dev, small_world, dense_world)
 
 
 @pytest.mark.parametrize("bins", [None, "2", "3", "64"])
