@@ -737,7 +737,8 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
                 uint32_t gmax = 65536;
                 if (const char* e = getenv("MM2G_GIANT_GMAX")) gmax = (uint32_t)std::max(0, atoi(e)) & ~15u;
                 if (gmax) {
-                    const int gblocks = 128;
+                    int gblocks = 256;
+                    if (const char* e = getenv("MM2G_GIANT_GBLOCKS")) gblocks = std::max(1, atoi(e));
                     unsigned char* scr;
                     ENSURE(c->giant_scr, unsigned char, (size_t)gblocks * gmax * 38, scr);
                     ca.giant_scr = scr;

@@ -1954,6 +1954,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
         uint64_t sk = 0;
         int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
         bool try_simple = true;
+        int32_t next_try = 0, backoff = 16;     // after a failed simple attempt: retry at next_try (backoff 16..128)
         uint64_t nk = (s + lane < e) ? K[s + lane] : 0;
         for (int32_t i0 = s; i0 < e; i0 += 64) {
             const uint64_t ak = nk;
@@ -2003,7 +2004,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 // first visited (largest j) among equal ones.  No prefix scans, no
                 // marks.  Tried while it keeps succeeding (and every 16th anchor).
                 bool done = false;
-                if (a.lazy && (try_simple || (i & 15) == 0)) {
+                if (a.lazy && (try_simple || i >= next_try)) {
                     int32_t bv = INT_MIN, bj = -1;
                     uint32_t nmk = 0;
                     for (int32_t jtop = i - 1; jtop >= lo && nmk <= (uint32_t)P.max_skip; jtop -= 64) {
@@ -2038,6 +2039,8 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     done = nmk <= (uint32_t)P.max_skip;
                     if (done && bv > span) { max_f = bv; max_j = bj; }
                     try_simple = done;
+                    if (done) backoff = 16;
+                    else { next_try = i + backoff; backoff = backoff < 128 ? 2 * backoff : 128; }
                 }
                 if (!done)
                 for (int32_t jtop = i - 1; jtop >= lo; jtop -= 64) {
@@ -2217,12 +2220,20 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
     int32_t* val2 = (int32_t*)(glo + cap);      // G only
     int32_t* gptr2 = val2 + cap;
     const int tid = threadIdx.x;
+    const uint32_t nl = min(*a.lseg_n, a.lseg_cap);
+    if constexpr (G) {   // most workgroups have no segment over the LDS capacity: leave before the LUT load
+        bool mine = false;
+        for (uint32_t q = blockIdx.x; q < nl && !mine; q += gridDim.x) {
+            const int32_t len = (int32_t)a.lseg[q].z - (int32_t)a.lseg[q].y;
+            mine = len > gcap && len <= cap;
+        }
+        if (!mine) return;
+    }
     for (int i = tid; i < P.lut_n; i += 1024) lut[i] = a.lut[i];
     __syncthreads();
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
-    const uint32_t nl = min(*a.lseg_n, a.lseg_cap);
     for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
         const uint4 L = a.lseg[q];
         const int32_t s = (int32_t)L.y, e = (int32_t)L.z, len = e - s;
