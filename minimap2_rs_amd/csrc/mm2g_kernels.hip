@@ -2241,6 +2241,8 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
         const uint32_t r = L.x;
         const uint64_t base = a.a_off[r];
         const uint64_t* K = a.keys + base;
+        const uint64_t g_t0 = a.lseg_prof ? wall_clock64() : 0;
+        int g_its = 0;
         for (int t = tid; t < len; t += 1024) { gk[t] = K[s + t]; f0[t] = span; }
         __syncthreads();
         // window start (lchain.rs:75-77): first j with p_i <= p_j + max_dist_x, and max_iter
@@ -2319,7 +2321,19 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                     }
                 }
                 if (tid == 0) s_flag = 0;
-                for (int t = tid; t < len; t += 1024) fo[t] = vres[t];
+                // Values that moved in this evaluation, as a prefix count (gch is free
+                // until the children lists).  An anchor none of whose predecessors
+                // moved keeps its argmax, and its own value already equals that
+                // maximum: the improvement skips it (after the first iteration).
+                for (int c0 = 0, carry = 0; c0 < len; c0 += 4096) {
+                    uint32_t c4[4], sum = 0, tot;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; c4[k] = (t < len && vres[t] != fo[t]) ? 1u : 0u; sum += c4[k]; }
+                    uint32_t ex = block_excl_sum(sum, tot, s_red) + (uint32_t)carry;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; if (t < len) { gch[t] = (int32_t)ex; fo[t] = vres[t]; } ex += c4[k]; }
+                    carry += (int)tot;
+                }
                 __syncthreads();
                 uint32_t ch = 0;
                 for (int t = tid; t < len; t += 1024) {
@@ -2327,6 +2341,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                     if (lw & 0x8000u) continue;          // pinned: exact already
                     const uint64_t ki = gk[t];
                     const int32_t lo = t - (int32_t)lw;
+                    if (it > 0 && gch[t] == gch[lo]) continue;
                     int32_t mf = span, mj = -1;
                     for (int32_t j = t - 1; j >= lo; --j) {
                         bool ok;
@@ -2339,6 +2354,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                 if (ch) atomicOr(&s_flag, 1u);
                 __syncthreads();
                 conv = s_flag == 0;
+                ++g_its;
                 __syncthreads();
             }
             if (!conv) {                         // k_chain_long runs it
@@ -2422,7 +2438,9 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
             }
             __syncthreads();
         }
-        if (a.lseg_prof && tid == 0) printf("[giant] len %d: %s\n", len, ok_seg ? "done" : "fallback");
+        if (a.lseg_prof && tid == 0)
+            printf("[giant%s] len %d: %s, %d iterations, %.0f us\n", G ? "-hbm" : "", len, ok_seg ? "done" : "fallback", g_its,
+                   (double)(wall_clock64() - g_t0) / 100.0);
         if (!ok_seg) continue;
         if (tid == 0) s_best = 0;
         __syncthreads();
