@@ -691,12 +691,15 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     ca.item_off = item_off;
     ca.seg_chunk = (uint32_t)SEG_CHUNK;
     // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
-    // settle in a few policy-iteration rounds; pass 0's long segments are real
-    // chains whose windows carry many mark sources, where k_chain_long is
-    // faster (measured: DESIGN.md section 7), so pass 0 leaves them to it.
+    // settle in a few no-break policy-iteration rounds.  Pass 0's long segments
+    // are real chains whose windows carry many mark sources: k_chain_long is
+    // faster on the usual few-hundred-anchor ones.
     const char* genv = getenv("MM2G_GIANT_MIN");   // tests: both passes
-    const uint32_t giant_min[2] = {genv ? (uint32_t)std::max(2, atoi(genv)) : 0xffffffffu,
-                                   genv ? (uint32_t)std::max(2, atoi(genv)) : 128u};
+    // Pass 0's exact mode is off by default: measured 15x (C3) and 6x (C5)
+    // slower than k_chain_long on real chains.
+    uint32_t giant_min[2] = {genv ? (uint32_t)std::max(2, atoi(genv)) : 0xffffffffu,
+                             genv ? (uint32_t)std::max(2, atoi(genv)) : 128u};
+    if (const char* e = getenv("MM2G_GIANT_MIN0")) giant_min[0] = (uint32_t)std::max(2, atoi(e));   // A/B
     if (const char* e = getenv("MM2G_SEG_CHUNK")) ca.seg_chunk = std::max(64u, (uint32_t)atoi(e) & ~63u);   // tests
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) {
@@ -728,6 +731,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
         ca.lseg_prof = env_on("MM2G_LSEG_PROF") ? 1u : 0u;
         for (int stg = 0; stg < 5; ++stg) {
             ca.giant_min = giant_min[pass];
+            ca.giant_exact = pass == 0 ? 1u : 0u;
             // production only; the pin bitmap and the lo field bound the window (max_iter <= 5120)
             if (stg == 2 && ca.lazy && ca.giant_min != 0xffffffffu && ca.P.max_iter <= 5120 && !env_on("MM2G_NO_GIANT")) {
                 ProfScope ps(c, pass ? "chain_giant_rescue" : "chain_giant");
@@ -740,7 +744,7 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
                     int gblocks = 256;
                     if (const char* e = getenv("MM2G_GIANT_GBLOCKS")) gblocks = std::max(1, atoi(e));
                     unsigned char* scr;
-                    ENSURE(c->giant_scr, unsigned char, (size_t)gblocks * gmax * 38, scr);
+                    ENSURE(c->giant_scr, unsigned char, (size_t)gblocks * gmax * 42, scr);
                     ca.giant_scr = scr;
                     ca.giant_gmax = gmax;
                     LCHK(launch_chain_stage(8, ca, gblocks, c->stream));

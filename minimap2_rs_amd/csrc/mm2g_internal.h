@@ -171,7 +171,8 @@ struct ChainArgs {
     uint32_t giant_min;      // long segments of at least this many anchors try k_chain_giant first (rescue: 128)
     uint32_t giant_lcap;     // tests: cap of the LDS variant below its LDS capacity (0 = none)
     uint32_t giant_gmax;     // global variant: anchors per workgroup scratch slice (0 = off)
-    void* giant_scr;         // global variant scratch: grid x giant_gmax x 38 B
+    void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
+    uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
 };
 struct DvArgs {
     uint32_t n;

@@ -2184,13 +2184,13 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
 // A segment that does not settle in GIANT_IT rounds or violates the mark
 // bound is left to k_chain_long.
 constexpr int GIANT_MAX = 4096;   // anchors per segment, at most (4 per thread)
-constexpr int GIANT_B = 30;       // LDS per anchor: key 8 B, f/val/pprev/ptr/children 5 x 4 B, lo 2 B
+constexpr int GIANT_B = 34;       // LDS per anchor: key 8 B, f/val/pprev/ptr/children/next-pprev 6 x 4 B, lo 2 B
 // segment capacity left beside the pen LUT in 160 KB of LDS (1 KB for statics)
 __host__ __device__ inline int giant_cap(int lut_n) {
     const int c = (160 * 1024 - 1024 - (((lut_n * 2) + 15) & ~15)) / GIANT_B;
     return (c < GIANT_MAX ? c : GIANT_MAX) & ~15;
 }
-constexpr int GIANT_GB = 38;      // HBM scratch per anchor (global variant): + ping-pong val/ptr 2 x 4 B
+constexpr int GIANT_GB = 42;      // HBM scratch per anchor (global variant): + ping-pong val/ptr 2 x 4 B
 constexpr int GIANT_IT = 32;
 constexpr int GIANT_PINS = 32;    // exactly evaluated anchors per segment before giving up
 constexpr int GIANT_MKW = 160;    // mark bitmap words (window <= max_iter 5000)
@@ -2216,7 +2216,8 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
     int32_t* gp = f1 + cap;
     int32_t* gptr = gp + cap;
     int32_t* gch = gptr + cap;
-    uint16_t* glo = (uint16_t*)(gch + cap);
+    int32_t* gnp = gch + cap;                   // exact mode: the next policy
+    uint16_t* glo = (uint16_t*)(gnp + cap);
     int32_t* val2 = (int32_t*)(glo + cap);      // G only
     int32_t* gptr2 = val2 + cap;
     const int tid = threadIdx.x;
@@ -2225,7 +2226,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
         bool mine = false;
         for (uint32_t q = blockIdx.x; q < nl && !mine; q += gridDim.x) {
             const int32_t len = (int32_t)a.lseg[q].z - (int32_t)a.lseg[q].y;
-            mine = len > gcap && len <= cap;
+            mine = len > gcap && len <= cap && len >= (int32_t)a.giant_min;
         }
         if (!mine) return;
     }
@@ -2237,7 +2238,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
     for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
         const uint4 L = a.lseg[q];
         const int32_t s = (int32_t)L.y, e = (int32_t)L.z, len = e - s;
-        if (G ? (len <= gcap || len > cap) : (len < (int32_t)a.giant_min || len > gcap)) continue;
+        if (len < (int32_t)a.giant_min || (G ? (len <= gcap || len > cap) : len > gcap)) continue;
         const uint32_t r = L.x;
         const uint64_t base = a.a_off[r];
         const uint64_t* K = a.keys + base;
@@ -2270,7 +2271,122 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
         int32_t* fo = f0; int32_t* val = f1;
         int dbl = 0;
         while ((1 << dbl) < len) ++dbl;
+        // f of the forest gp (pinned anchors keep fo): pointer doubling; returns
+        // the array holding the values (fo itself is not written)
+        auto eval_forest = [&]() -> const int32_t* {
+            for (int t = tid; t < len; t += 1024) {
+                const int32_t p = gp[t];
+                if ((glo[t] & 0x8000u) || p < 0) { val[t] = (glo[t] & 0x8000u) ? fo[t] : span; gptr[t] = -1; }
+                else { bool ok; val[t] = sc_of(gk[t], gk[p], ok); gptr[t] = p; }
+            }
+            __syncthreads();
+            const int32_t* vres = val;
+            if constexpr (G) {
+                int32_t *v0 = val, *p0 = gptr, *v1 = val2, *p1 = gptr2;
+                for (int d = 0; d < dbl; ++d) {
+                    for (int t = tid; t < len; t += 1024) {
+                        const int32_t p = p0[t];
+                        v1[t] = p >= 0 ? v0[t] + v0[p] : v0[t];
+                        p1[t] = p >= 0 ? p0[p] : -1;
+                    }
+                    __syncthreads();
+                    int32_t* tv = v0; v0 = v1; v1 = tv;
+                    int32_t* tp = p0; p0 = p1; p1 = tp;
+                }
+                vres = v0;
+            } else {
+                for (int d = 0; d < dbl; ++d) {
+                    int32_t nv[4], np[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int t = tid + k * 1024;
+                        if (t < len) {
+                            const int32_t p = gptr[t];
+                            nv[k] = p >= 0 ? val[t] + val[p] : val[t];
+                            np[k] = p >= 0 ? gptr[p] : -1;
+                        }
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int t = tid + k * 1024;
+                        if (t < len) { val[t] = nv[k]; gptr[t] = np[k]; }
+                    }
+                    __syncthreads();
+                }
+            }
+            return vres;
+        };
+        // Children lists of the forest gp: j is marked for i (t[j] == i) iff a
+        // valid c in (j, i) has pprev[c] == j.  gptr = child counts, val = list
+        // ends, gch = the lists.  Ends without a barrier.
+        auto build_children = [&]() {
+            for (int t = tid; t < len; t += 1024) gptr[t] = 0;
+            __syncthreads();
+            for (int t = tid; t < len; t += 1024) if (gp[t] >= 0) atomicAdd((uint32_t*)&gptr[gp[t]], 1u);
+            __syncthreads();
+            for (int c0 = 0, carry = 0; c0 < len; c0 += 4096) {   // exclusive scan, 4096 per pass
+                uint32_t c4[4], sum = 0, tot;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; c4[k] = t < len ? (uint32_t)gptr[t] : 0u; sum += c4[k]; }
+                uint32_t ex = block_excl_sum(sum, tot, s_red) + (uint32_t)carry;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; if (t < len) val[t] = (int32_t)ex; ex += c4[k]; }
+                carry += (int)tot;
+            }
+            __syncthreads();
+            for (int t = tid; t < len; t += 1024) if (gp[t] >= 0) gch[atomicAdd((uint32_t*)&val[gp[t]], 1u)] = t;
+        };
+        // marked(j) for anchor t with key ki
+        auto marked = [&](int32_t j, int32_t t, uint64_t ki) -> bool {
+            const int32_t ce = val[j];
+            for (int32_t c = ce - gptr[j]; c < ce; ++c) {
+                const int32_t cj = gch[c];
+                if (cj < t) { bool okc; (void)sc_of(ki, gk[cj], okc); if (okc) return true; }
+            }
+            return false;
+        };
         bool ok_seg = false;
+        if (a.giant_exact) {
+            // Pass 0 (real chains, marks everywhere): policy iteration on the
+            // reference loop itself (lchain.rs:78-87, n_skip and break, marks from
+            // the current forest's children).  Each anchor depends only on
+            // earlier ones, so a forest that the loop reproduces everywhere, with
+            // its evaluated values, is the reference's solution.
+            bool conv = false;
+            for (int it = 0; it < GIANT_IT && !conv; ++it) {
+                build_children();
+                if (tid == 0) s_flag = 0;
+                __syncthreads();
+                uint32_t ch = 0;
+                for (int t = tid; t < len; t += 1024) {
+                    const uint64_t ki = gk[t];
+                    const int32_t lo = t - (int32_t)glo[t];
+                    int32_t mf = span, mj = -1, n_skip = 0;
+                    for (int32_t j = t - 1; j >= lo; --j) {
+                        bool ok;
+                        const int32_t sv = sc_of(ki, gk[j], ok) + fo[j];
+                        if (!ok) continue;
+                        if (sv > mf) { mf = sv; mj = j; if (n_skip > 0) --n_skip; continue; }
+                        if (marked(j, t, ki) && ++n_skip > P.max_skip) break;
+                    }
+                    gnp[t] = mj;
+                    ch |= (mf != fo[t] || mj != gp[t]) ? 1u : 0u;
+                }
+                if (ch) atomicOr(&s_flag, 1u);
+                __syncthreads();
+                conv = s_flag == 0;
+                ++g_its;
+                if (!conv) {
+                    for (int t = tid; t < len; t += 1024) gp[t] = gnp[t];
+                    __syncthreads();
+                    const int32_t* vres = eval_forest();
+                    for (int t = tid; t < len; t += 1024) fo[t] = vres[t];
+                }
+                __syncthreads();
+            }
+            ok_seg = conv;
+        } else
         for (int round = 0; round < GIANT_PINS; ++round) {
             // Policy iteration: evaluate the current predecessor forest exactly
             // (pointer doubling, ceil(log2 len) rounds), then let every anchor
@@ -2279,47 +2395,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
             // changes they are the DP's fixed point and gp is its argmax.
             bool conv = false;
             for (int it = 0; it < GIANT_IT && !conv; ++it) {
-                for (int t = tid; t < len; t += 1024) {
-                    const int32_t p = gp[t];
-                    if ((glo[t] & 0x8000u) || p < 0) { val[t] = (glo[t] & 0x8000u) ? fo[t] : span; gptr[t] = -1; }
-                    else { bool ok; val[t] = sc_of(gk[t], gk[p], ok); gptr[t] = p; }
-                }
-                __syncthreads();
-                const int32_t* vres = val;
-                if constexpr (G) {
-                    int32_t *v0 = val, *p0 = gptr, *v1 = val2, *p1 = gptr2;
-                    for (int d = 0; d < dbl; ++d) {
-                        for (int t = tid; t < len; t += 1024) {
-                            const int32_t p = p0[t];
-                            v1[t] = p >= 0 ? v0[t] + v0[p] : v0[t];
-                            p1[t] = p >= 0 ? p0[p] : -1;
-                        }
-                        __syncthreads();
-                        int32_t* tv = v0; v0 = v1; v1 = tv;
-                        int32_t* tp = p0; p0 = p1; p1 = tp;
-                    }
-                    vres = v0;
-                } else {
-                    for (int d = 0; d < dbl; ++d) {
-                        int32_t nv[4], np[4];
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int t = tid + k * 1024;
-                            if (t < len) {
-                                const int32_t p = gptr[t];
-                                nv[k] = p >= 0 ? val[t] + val[p] : val[t];
-                                np[k] = p >= 0 ? gptr[p] : -1;
-                            }
-                        }
-                        __syncthreads();
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int t = tid + k * 1024;
-                            if (t < len) { val[t] = nv[k]; gptr[t] = np[k]; }
-                        }
-                        __syncthreads();
-                    }
-                }
+                const int32_t* vres = eval_forest();
                 if (tid == 0) s_flag = 0;
                 // Values that moved in this evaluation, as a prefix count (gch is free
                 // until the children lists).  An anchor none of whose predecessors
@@ -2364,21 +2440,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
             // Children lists of the converged forest: j is marked for i (t[j]
             // == i) iff a valid c in (j, i) has pprev[c] == j.  gptr = child
             // counts, val = list ends, gch = the lists.
-            for (int t = tid; t < len; t += 1024) gptr[t] = 0;
-            __syncthreads();
-            for (int t = tid; t < len; t += 1024) if (gp[t] >= 0) atomicAdd((uint32_t*)&gptr[gp[t]], 1u);
-            __syncthreads();
-            for (int c0 = 0, carry = 0; c0 < len; c0 += 4096) {   // exclusive scan, 4096 per pass
-                uint32_t c4[4], sum = 0, tot;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; c4[k] = t < len ? (uint32_t)gptr[t] : 0u; sum += c4[k]; }
-                uint32_t ex = block_excl_sum(sum, tot, s_red) + (uint32_t)carry;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; if (t < len) val[t] = (int32_t)ex; ex += c4[k]; }
-                carry += (int)tot;
-            }
-            __syncthreads();
-            for (int t = tid; t < len; t += 1024) if (gp[t] >= 0) gch[atomicAdd((uint32_t*)&val[gp[t]], 1u)] = t;
+            build_children();
             // No break is possible where a window holds <= max_skip mark
             // sources.  Elsewhere run the reference loop on the converged
             // values: the first anchor where it disagrees is pinned below.
@@ -2402,13 +2464,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                     const int32_t sv = sc_of(ki, gk[j], ok) + fo[j];
                     if (!ok) continue;
                     if (sv > mf) { mf = sv; mj = j; if (n_skip > 0) --n_skip; continue; }
-                    const int32_t ce = val[j];
-                    bool mk = false;
-                    for (int32_t c = ce - gptr[j]; c < ce && !mk; ++c) {
-                        const int32_t cj = gch[c];
-                        if (cj < t) { bool okc; (void)sc_of(ki, gk[cj], okc); mk = okc; }
-                    }
-                    if (mk && ++n_skip > P.max_skip) break;
+                    if (marked(j, t, ki) && ++n_skip > P.max_skip) break;
                 }
                 if (mf != fo[t] || mj != gp[t]) atomicMin(&s_flag, (uint32_t)t);
             }
