@@ -75,6 +75,7 @@ struct mm2g_ctx {
     DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
     DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
     DevBuf tab_off, tab_key, tab_cnt;
+    DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
     DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
     DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
     uint64_t* h_small = nullptr;          // pinned, 16 u64
@@ -609,9 +610,11 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     uint32_t *mz_n, *mz_poff, *a_cnt; uint64_t* a_off;
     ENSURE(c->mz_n, uint32_t, mcap, mz_n); ENSURE(c->mz_poff, uint32_t, mcap, mz_poff);
     ENSURE(c->a_cnt, uint32_t, n + 1, a_cnt); ENSURE(c->a_off, uint64_t, n + 1, a_off);
+    uint32_t* a_part;
+    ENSURE(c->a_part, uint32_t, (size_t)n * (SEED_PARTS - 1), a_part);
     SeedArgs sa{n, (const uint64_t*)c->rd_off.p, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, (const uint32_t*)c->mz_y.p, keep,
                 (const IxEntry*)c->dix->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->dix->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k,
-                0, c->dix->ix_pos.cap / 8, mcap, out};
+                0, c->dix->ix_pos.cap / 8, mcap, out, a_part};
     {
         ProfScope ps(c, "seed_count");
         LCHK(launch_seed_count(sa, grid_for(n), c->stream));

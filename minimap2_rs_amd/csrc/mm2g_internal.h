@@ -115,7 +115,11 @@ struct SeedArgs {
     KeyLayout kl; int span;
     uint64_t cap_keys, cap_pos, cap_mz;   // bounds for the MM2G_CHECKED build
     ReadOut* out;                         // m_kept
+    uint32_t* a_part;                     // per read, SEED_PARTS-1 entries: anchors before part k (k = 1..)
 };
+// seed_write splits each read's minimizers into this many contiguous parts
+// (whole 64-minimizer chunks), one wave each; seed_count records where they start
+constexpr int SEED_PARTS = 4;
 // per-read anchor sort + singleton filter (k_sort_small / k_sort_read)
 constexpr int32_t SEG_CHUNK = 4096;     // anchors per work item of the streaming chain kernels
 constexpr uint32_t SEG_THREAD = 1024;   // cell segments up to this length: one thread per anchor (default seg_small)

@@ -651,8 +651,15 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
         const uint64_t mb = uni64(a.mz_base[r]);
         const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
+        const uint32_t nch = (m + 63) >> 6;
         uint32_t acc = 0, kept = 0;
+        int kn = 1;                        // next seed_write part boundary
         for (uint32_t b0 = 0; b0 < m; b0 += 64) {
+            while (kn < SEED_PARTS && (b0 >> 6) == (nch * (uint32_t)kn) / SEED_PARTS) {
+                const uint32_t sofar = wave_sum(acc);
+                if (lane == 0) a.a_part[(uint64_t)r * (SEED_PARTS - 1) + kn - 1] = sofar;
+                ++kn;
+            }
             const uint32_t i = b0 + lane;
             const bool act = i < m;
             bool done = !(act && a.keep[mb + i]);
@@ -673,6 +680,7 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
         }
         acc = wave_sum(acc);
         kept = wave_sum(kept);
+        for (; kn < SEED_PARTS; ++kn) if (lane == 0) a.a_part[(uint64_t)r * (SEED_PARTS - 1) + kn - 1] = acc;
         if (lane == 0) { a.a_cnt[r] = acc; a.out[r].m_kept = (int32_t)kept; }
     }
 }
@@ -696,14 +704,21 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
     const int lane = lane_id(), wv = wave_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
     constexpr int U = 4;   // output batches whose position gathers are in flight together
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wv; r < a.n; r += nwaves) {
+    // one wave per (read, part): parts are contiguous runs of whole 64-minimizer
+    // chunks, starting at the anchor counts seed_count recorded
+    for (uint32_t wp = blockIdx.x * (blockDim.x >> 6) + wv; wp < a.n * (uint32_t)SEED_PARTS; wp += nwaves) {
+        const uint32_t r = wp / SEED_PARTS, part = wp % SEED_PARTS;
         const uint64_t mb = uni64(a.mz_base[r]);
         const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
+        const uint32_t nch = (m + 63) >> 6;
+        const uint32_t cb = (nch * part) / SEED_PARTS, ce = (nch * (part + 1)) / SEED_PARTS;
+        if (cb >= ce) continue;
         const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
         const uint64_t obase = uni64(a.a_off[r]);
         uint64_t* out = a.keys;
-        uint64_t run = 0;
-        for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+        uint64_t run = part ? (uint64_t)(uint32_t)uni((int32_t)a.a_part[(uint64_t)r * (SEED_PARTS - 1) + part - 1]) : 0;
+        const uint32_t cend = ce * 64 < m ? ce * 64 : m;
+        for (uint32_t c0 = cb * 64; c0 < cend; c0 += 64) {
             const uint32_t i = c0 + lane;
             const bool vi = i < m;
             const uint32_t n = vi ? a.mz_n[CK(mb + i, a.cap_mz)] : 0;
@@ -2802,7 +2817,10 @@ int launch_seed_count(const SeedArgs& a, int n_blocks, hipStream_t st) {
     return 0;
 }
 int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
-    hipLaunchKernelGGL(k_seed_write, dim3(n_blocks), dim3(256), 0, st, a);
+    (void)n_blocks;
+    const uint64_t parts = (uint64_t)a.n * SEED_PARTS;
+    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>((parts + 3) / 4, 16384));
+    hipLaunchKernelGGL(k_seed_write, dim3(blocks), dim3(256), 0, st, a);
     LAUNCH_CHECK();
     return 0;
 }
