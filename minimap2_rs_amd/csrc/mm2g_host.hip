@@ -184,19 +184,21 @@ static void dump_sketch_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
     (void)hipFree(d);
     double ph[5] = {0, 0, 0, 0, 0}, L = 0;
     uint32_t m = 0;
-    uint64_t t_hi = 0;
+    uint64_t t_hi = 0, tiles = 0, slow = 0;
     for (uint32_t r = 0; r < n; ++r) {
         const uint64_t* p = &h[(size_t)r * 8];
         if (!p[5]) continue;
         ++m;
+        tiles += p[7] >> 32; slow += p[7] & 0xffffffffULL;
         for (int k = 0; k < 5; ++k) ph[k] += (double)p[k];
         L += (double)p[5];
         t_hi = std::max(t_hi, p[6]);
     }
     if (!m) return;
     double tot = ph[0] + ph[1] + ph[2] + ph[3] + ph[4];
-    fprintf(stderr, "[sketch_prof] reads=%u len=%.0f us/read: stage=%.1f warmup=%.1f phase1=%.1f phase2=%.1f tail=%.1f total=%.1f\n",
-            m, L / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100, tot / m / 100);
+    fprintf(stderr, "[sketch_prof] reads=%u len=%.0f us/read: stage=%.1f warmup=%.1f phase1=%.1f phase2=%.1f tail=%.1f total=%.1f; exact-path tiles %.1f%%\n",
+            m, L / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100, tot / m / 100,
+            tiles ? 100.0 * (double)slow / (double)tiles : 0.0);
 }
 
 static inline uint32_t bit_width(uint64_t x) { uint32_t b = 0; while (x) { ++b; x >>= 1; } return b; }

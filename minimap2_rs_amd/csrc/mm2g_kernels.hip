@@ -225,6 +225,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
             if (t < w) { X[t] = U64MAX; LZ[t] = 0; }
         }
         uint64_t count = 0;
+        uint32_t n_tiles = 0, n_slow = 0;      // MM2G_SKETCH_PROF: tiles, tiles on the exact (2-pass) step path
         int32_t l_carry = 0;
         // bases of this lane's chunk, prefetched one tile ahead; lanes 0-3 also
         // keep the previous tile's last 32 bases (codes | reversed validity << 16)
@@ -423,7 +424,9 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                     fast_done = true;
                 }
             }
+            ++n_tiles;
             if (!fast_done) {
+              ++n_slow;
               myoff = 0; tot = 0;
               for (int pass = 0; pass < 2; ++pass) {
                 const bool WR = pass == 1;
@@ -518,6 +521,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
             for (int q = 0; q < 5; ++q) a.prof[(uint64_t)r * 8 + q] = pt[q];
             a.prof[(uint64_t)r * 8 + 5] = (uint64_t)L;
             a.prof[(uint64_t)r * 8 + 6] = wall_clock64();
+            a.prof[(uint64_t)r * 8 + 7] = ((uint64_t)n_tiles << 32) | n_slow;
         }
 #undef SK_PT
 #undef SK_Y
