@@ -2097,8 +2097,17 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     const bool mk = ok && ppj >= lo;
                     const int32_t tb = jtop - ppj;                 // target lane
                     const bool mk_in = mk && tb < 64;
-                    const uint64_t tbit = mk_in ? (1ULL << (tb & 63)) : 0ULL;
-                    const uint64_t M = ((uint64_t)wave_or32((uint32_t)(tbit >> 32)) << 32) | wave_or32((uint32_t)tbit);
+                    // along a chain pprev[j] is usually j-1 (target lane l+1): then the
+                    // mask is the marking lanes shifted by one, without the OR-reduction
+                    const uint64_t mkM = ballot(mk_in);
+                    uint64_t M = 0;
+                    if (mkM) {
+                        if (ballot(mk_in && tb != lane + 1) == 0) M = mkM << 1;
+                        else {
+                            const uint64_t tbit = mk_in ? (1ULL << (tb & 63)) : 0ULL;
+                            M = ((uint64_t)wave_or32((uint32_t)(tbit >> 32)) << 32) | wave_or32((uint32_t)tbit);
+                        }
+                    }
                     // strict new maximum in processing order
                     const int32_t v = ok ? sv : INT_MIN;
                     const int32_t excl = shr1_dpp(scan_max(v), INT_MIN);
