@@ -151,9 +151,16 @@ constexpr int SK_TS = 64 * SK_CH;
 
 // per-wave LDS: X[NB] (x = hash<<8 | span, MAX = no info), LZ[NB] (l | z<<15);
 // y = pos<<1 | z is implicit.  Bases stay in registers (8 per lane).
-__host__ __device__ inline size_t sketch_wave_lds(int w) {
+// Lane l works on slots [w + 8l, w + 8l + 8): a stride of 8 slots (16 LDS banks
+// for X) would put all 64 lanes on 4 banks.  One pad slot per 8 spreads them.
+#define SKP(i) ((i) + ((i) >> 3))
+__host__ __device__ inline size_t sketch_wave_slots(int w) {
     const size_t nb = (size_t)SK_TS + (size_t)w;
-    return ((nb * 8 + nb * 2) + 15) & ~(size_t)15;
+    return nb + (nb >> 3) + 1;
+}
+__host__ __device__ inline size_t sketch_wave_lds(int w) {
+    const size_t pnb = sketch_wave_slots(w);
+    return ((pnb * 8 + pnb * 2) + 15) & ~(size_t)15;
 }
 
 // reverse the order of the 32 2-bit groups of x
@@ -194,10 +201,9 @@ template <bool K32>
 __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int w = a.w, k = a.k;
-    const int NB = SK_TS + w;                        // history (w) + tile
     const int wv = wave_id(), lane = lane_id();
     uint64_t* X = (uint64_t*)(smem + sketch_wave_lds(w) * wv);
-    uint16_t* LZ = (uint16_t*)(X + NB);
+    uint16_t* LZ = (uint16_t*)(X + sketch_wave_slots(w));
     const int CAP = w + k;
     const uint64_t mask = (k >= 32) ? U64MAX : ((1ULL << (2 * k)) - 1);
     const uint32_t shift1 = 2u * (uint32_t)(k - 1);
@@ -222,7 +228,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
         // history slots = positions [-w, -1]: MAX
         for (int t0 = 0; t0 < w; t0 += 64) {
             const int t = t0 + lane;
-            if (t < w) { X[t] = U64MAX; LZ[t] = 0; }
+            if (t < w) { X[SKP(t)] = U64MAX; LZ[SKP(t)] = 0; }
         }
         uint64_t count = 0;
         uint32_t n_tiles = 0, n_slow = 0;      // MM2G_SKETCH_PROF: tiles, tiles on the exact (2-pass) step path
@@ -307,7 +313,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                             fl = 2;
                         }
                     }
-                    X[ix] = x; LZ[ix] = (uint16_t)(fl | (z << 15));
+                    X[SKP(ix)] = x; LZ[SKP(ix)] = (uint16_t)(fl | (z << 15));
                     if (fl == 0) { rs = true; lc = 0; } else if (fl == 2) { lc = lc + 1 < CAP ? lc + 1 : CAP; }
                 }
             }
@@ -332,11 +338,11 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                 const int64_t p = ps + t;
                 if (p < pe) {
                     const int ix = (int)(p - hbase);
-                    const uint16_t v = LZ[ix];
+                    const uint16_t v = LZ[SKP(ix)];
                     const uint16_t fl = v & 3u;
                     if (fl == 0) lv = 0; else if (fl == 2) lv = lv + 1 < CAP ? lv + 1 : CAP;
-                    LZ[ix] = (uint16_t)((v & 0x8000u) | (uint16_t)lv);
-                    if (!(fl == 2 && lv >= k)) X[ix] = U64MAX;
+                    LZ[SKP(ix)] = (uint16_t)((v & 0x8000u) | (uint16_t)lv);
+                    if (!(fl == 2 && lv >= k)) X[SKP(ix)] = U64MAX;
                 }
             }
             {
@@ -346,7 +352,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
             }
             wave_lds_sync();
             SK_PT(2);
-#define SK_Y(q) ((((uint32_t)(hbase + (q))) << 1) | (uint32_t)(LZ[(q)] >> 15))
+#define SK_Y(q) ((((uint32_t)(hbase + (q))) << 1) | (uint32_t)(LZ[SKP((q))] >> 15))
             uint32_t code16n, valid8n;
             codes8(nbytes, code16n, valid8n);
             // ---- phase 2: reference step logic, count then write
@@ -366,13 +372,13 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                     uint64_t cx = U64MAX; uint32_t cp = 0xffffffffu;
                     const int q0 = (int)(ps - hbase);
                     for (int d = 1; d < w - SK_CH; ++d) {          // slot q0 - d (newest first)
-                        const uint64_t x = X[q0 - d];
+                        const uint64_t x = X[SKP(q0 - d)];
                         if (cp == 0xffffffffu || x < cx) { cx = x; cp = (uint32_t)(q0 - d); } else if (x == cx) cp |= 0x10000u;
                     }
 #pragma unroll
                     for (int t = 0; t <= SK_CH; ++t) {
                         const int d = w - SK_CH + t;                 // j = ps - w + (SK_CH - t)
-                        const uint64_t x = X[q0 - d];
+                        const uint64_t x = X[SKP(q0 - d)];
                         if (cp == 0xffffffffu || x < cx) { cx = x; cp = (uint32_t)(q0 - d); } else if (x == cx) cp |= 0x10000u;
                         sx[SK_CH - t] = cx; sp[SK_CH - t] = cp;
                     }
@@ -390,8 +396,8 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                         const int64_t i = ps + t;
                         const bool act = i < pe;
                         const int ii = (int)(i - hbase);
-                        const uint64_t xi = act ? X[ii] : U64MAX;
-                        const int32_t l = act ? (int32_t)(LZ[ii] & 0x7fffu) : 0;
+                        const uint64_t xi = act ? X[SKP(ii)] : U64MAX;
+                        const int32_t l = act ? (int32_t)(LZ[SKP(ii)] & 0x7fffu) : 0;
                         need |= act && l == w + k - 1 && mxo != U64MAX;                 // A (sketch.rs:90-93)
                         const bool doB = act && xi <= mxo;                              // B (94-96)
                         const bool doC = act && !doB && mqo == ii - w;                  // C (97-105)
@@ -417,7 +423,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                     for (int t = 0; t < SK_CH; ++t) {
                         if ((em >> t) & 1u) {
                             const int q = (int)((eq[t >> 1] >> (16 * (t & 1))) & 0xffffu);
-                            if (o < oend) { a.mz_x[o] = X[q]; a.mz_y[o] = SK_Y(q); }
+                            if (o < oend) { a.mz_x[o] = X[SKP(q)]; a.mz_y[o] = SK_Y(q); }
                             ++o;
                         }
                     }
@@ -437,7 +443,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                 for (int d = 0; d < w; ++d) {
                     const int64_t p = ps - w + d;
                     const int q = (int)(p - hbase);
-                    const uint64_t x = X[q];
+                    const uint64_t x = X[SKP(q)];
                     if (mx >= x) { mx = x; my = SK_Y(q); mp = p; }
                 }
                 for (int t = 0; t < SK_CH; ++t) {
@@ -445,14 +451,14 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                     const bool act = i < pe;
                     const bool em_ok = i >= efrom;   // warm-up steps of an index view emit nothing
                     const int ii = (int)(i - hbase);
-                    const uint64_t ix_x = act ? X[ii] : U64MAX;
+                    const uint64_t ix_x = act ? X[SKP(ii)] : U64MAX;
                     const uint32_t ix_y = act ? SK_Y(ii) : 0xffffffffu;
-                    const int32_t l = act ? (int32_t)(LZ[ii] & 0x7fffu) : 0;
+                    const int32_t l = act ? (int32_t)(LZ[SKP(ii)] & 0x7fffu) : 0;
                     const bool doA = act && l == w + k - 1 && mx != U64MAX;
                     if (any(doA)) {
                         for (int d = 1; d < w; ++d) {
                             const int q = ii - w + d;
-                            if (doA && X[q] == mx && SK_Y(q) != my) SK_EMIT(X[q], SK_Y(q));
+                            if (doA && X[SKP(q)] == mx && SK_Y(q) != my) SK_EMIT(X[SKP(q)], SK_Y(q));
                         }
                     }
                     const bool doB = act && ix_x <= mx;
@@ -463,7 +469,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                         uint64_t nx = U64MAX; uint32_t ny = 0; int64_t np = mp;
                         for (int d = 1; d <= w; ++d) {
                             const int q = ii - w + d;
-                            const uint64_t x = X[q];
+                            const uint64_t x = X[SKP(q)];
                             if (nx >= x) { nx = x; ny = SK_Y(q); np = i - w + d; }
                         }
                         if (doC) { mx = nx; my = ny; mp = np; }
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                         if (any(doT)) {
                             for (int d = 1; d <= w; ++d) {
                                 const int q = ii - w + d;
-                                if (doT && mx == X[q] && my != SK_Y(q)) SK_EMIT(X[q], SK_Y(q));
+                                if (doT && mx == X[SKP(q)] && my != SK_Y(q)) SK_EMIT(X[SKP(q)], SK_Y(q));
                             }
                         }
                     }
@@ -491,7 +497,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                 // source [TS, TS+w) and destination [0, w) never overlap (w < 256 <= TS)
                 for (int b0 = 0; b0 < w; b0 += 64) {
                     const int t = b0 + ln;
-                    if (t < w) { X[t] = X[SK_TS + t]; LZ[t] = LZ[SK_TS + t]; }
+                    if (t < w) { X[SKP(t)] = X[SKP(SK_TS + t)]; LZ[SKP(t)] = LZ[SKP(SK_TS + t)]; }
                 }
             }
             wave_lds_sync();
@@ -503,7 +509,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
             uint64_t mx = U64MAX; uint32_t my = 0;
             for (int d = 0; d < w; ++d) {
                 const int q = (int)(L - w + d - hbase);
-                const uint64_t x = X[q];
+                const uint64_t x = X[SKP(q)];
                 if (mx >= x) { mx = x; my = SK_Y(q); }
             }
             if (mx != U64MAX && flush) {
