@@ -664,29 +664,49 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
         const uint32_t nch = (m + 63) >> 6;
         uint32_t acc = 0, kept = 0;
         int kn = 1;                        // next seed_write part boundary
-        for (uint32_t b0 = 0; b0 < m; b0 += 64) {
-            while (kn < SEED_PARTS && (b0 >> 6) == (nch * (uint32_t)kn) / SEED_PARTS) {
-                const uint32_t sofar = wave_sum(acc);
-                if (lane == 0) a.a_part[(uint64_t)r * (SEED_PARTS - 1) + kn - 1] = sofar;
-                ++kn;
+        // SC_U chunks of 64 minimizers at a time: their table probes are
+        // independent, so SC_U loads per lane are in flight together
+        constexpr int SC_U = 4;
+        for (uint32_t b0 = 0; b0 < m; b0 += 64 * SC_U) {
+            uint64_t h[SC_U];
+            uint32_t sl[SC_U], n[SC_U], off[SC_U];
+            bool done[SC_U];
+#pragma unroll
+            for (int u = 0; u < SC_U; ++u) {
+                const uint32_t i = b0 + (uint32_t)u * 64 + lane;
+                const bool act = i < m;
+                done[u] = !(act && a.keep[mb + i]);
+                kept += done[u] ? 0u : 1u;
+                h[u] = act ? (a.mz_x[mb + i] >> 8) : 0;
+                sl[u] = ix_slot(h[u], a.log2cap); n[u] = 0; off[u] = 0;
             }
-            const uint32_t i = b0 + lane;
-            const bool act = i < m;
-            bool done = !(act && a.keep[mb + i]);
-            kept += done ? 0u : 1u;
-            const uint64_t h = act ? (a.mz_x[mb + i] >> 8) : 0;
-            uint32_t sl = ix_slot(h, a.log2cap), n = 0, off = 0;
-            while (any(!done)) {
-                if (!done) {
-                    const IxEntry e = a.tab[sl];
-                    if (e.key == h) { off = e.off; n = e.n; done = true; }
-                    else if (e.key == U64MAX) done = true;
-                    else sl = (sl + 1) & cmask;
+            while (any(!(done[0] && done[1] && done[2] && done[3]))) {
+                IxEntry e[SC_U];
+#pragma unroll
+                for (int u = 0; u < SC_U; ++u) if (!done[u]) e[u] = a.tab[sl[u]];
+#pragma unroll
+                for (int u = 0; u < SC_U; ++u) {
+                    if (done[u]) continue;
+                    if (e[u].key == h[u]) { off[u] = e[u].off; n[u] = e[u].n; done[u] = true; }
+                    else if (e[u].key == U64MAX) done[u] = true;
+                    else sl[u] = (sl[u] + 1) & cmask;
                 }
             }
-            if (n > 1 && (int64_t)n > (int64_t)a.mid_occ) n = 0;   // Multi with len > mid_occ: skip
-            if (act) { a.mz_n[mb + i] = n; a.mz_poff[mb + i] = off; }
-            acc += n;
+#pragma unroll
+            for (int u = 0; u < SC_U; ++u) {
+                const uint32_t c = (b0 >> 6) + (uint32_t)u;
+                if (c >= nch) break;
+                while (kn < SEED_PARTS && c == (nch * (uint32_t)kn) / SEED_PARTS) {
+                    const uint32_t sofar = wave_sum(acc);
+                    if (lane == 0) a.a_part[(uint64_t)r * (SEED_PARTS - 1) + kn - 1] = sofar;
+                    ++kn;
+                }
+                const uint32_t i = b0 + (uint32_t)u * 64 + lane;
+                uint32_t nn = n[u];
+                if (nn > 1 && (int64_t)nn > (int64_t)a.mid_occ) nn = 0;   // Multi with len > mid_occ: skip
+                if (i < m) { a.mz_n[mb + i] = nn; a.mz_poff[mb + i] = off[u]; }
+                acc += nn;
+            }
         }
         acc = wave_sum(acc);
         kept = wave_sum(kept);
