@@ -733,7 +733,7 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
     __shared__ uint32_t s_inc[4][64], s_poff[4][64], s_y[4][64];
     const int lane = lane_id(), wv = wave_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
-    constexpr int U = 4;   // output batches whose position gathers are in flight together
+    constexpr int U = 8;   // output batches whose position gathers are in flight together
     // one wave per (read, part): parts are contiguous runs of whole 64-minimizer
     // chunks, starting at the anchor counts seed_count recorded
     for (uint32_t wp = blockIdx.x * (blockDim.x >> 6) + wv; wp < a.n * (uint32_t)SEED_PARTS; wp += nwaves) {
@@ -2731,18 +2731,28 @@ __global__ __launch_bounds__(64) void k_dv(DvArgs a) {
     }
     uint32_t st = b;
     while (st > 0 && uni(mpos(st - 1)) == first) --st;
-    // greedy match (paf.rs:179-186): the next j with P[j] == C[kk], 64 candidates per ballot
+    // greedy match (paf.rs:179-186): the next j with P[j] == C[kk].  A window of
+    // 64 positions after j sits in registers; successive targets are matched in
+    // it by ballot (each after the previous match) until one is not there, and
+    // then the window moves past its end.
     uint32_t j = st, en = st;
     int32_t kk = 1, n_match = 1, kb = 1;
     int32_t cv = (kb + lane < cm) ? fwdq(kb + lane) : 0;
     while (kk < cm && j + 1 < m) {
-        if (kk - kb >= 64) { kb = kk; cv = (kb + lane < cm) ? fwdq(kb + lane) : 0; }
-        const int32_t target = rdl(cv, kk - kb);
         const uint32_t c0 = j + 1;
         const uint32_t jl = c0 + (uint32_t)lane;
-        const uint64_t hit = ballot(jl < m && mpos(jl) == target);
-        if (hit) { j = c0 + (uint32_t)ctz64(hit); ++n_match; en = j; ++kk; }
-        else j = (c0 + 63 < m - 1) ? c0 + 63 : m - 1;
+        const int32_t pv = jl < m ? mpos(jl) : 0;
+        uint64_t avail = ballot(jl < m);
+        while (kk < cm) {
+            if (kk - kb >= 64) { kb = kk; cv = (kb + lane < cm) ? fwdq(kb + lane) : 0; }
+            const int32_t target = rdl(cv, kk - kb);
+            const uint64_t hit = ballot(pv == target) & avail;
+            if (!hit) break;
+            const int L = ctz64(hit);
+            j = c0 + (uint32_t)L; ++n_match; en = j; ++kk;
+            avail &= L == 63 ? 0ULL : ~((2ULL << L) - 1ULL);
+        }
+        if (kk < cm) j = (c0 + 63 < m - 1) ? c0 + 63 : m - 1;   // C[kk] is not in this window
     }
     if (lane == 0) {
         ReadOut* O = a.out + r;
