@@ -17,7 +17,9 @@
  *     context are serialised on its HIP stream; distinct contexts (and
  *     devices) run concurrently — that is how reads shard over GPUs.
  *   - Argument checks mirror the reference asserts: 0 < w < 256,
- *     0 < k <= 28, non-empty sequence (src/sketch.rs:40-42).
+ *     0 < k <= 28, non-empty sequence (src/sketch.rs:30-32).
+ *   - Nothing on the mapping path reads the environment: tuning and test
+ *     switches are explicit per-context knobs (mm2g_ctx_set_knob).
  */
 #ifndef MM2G_H
 #define MM2G_H
@@ -120,7 +122,7 @@ typedef struct {
     int32_t ts, te;       /* chain_trange                                      */
     int32_t rid;          /* target id (0x7fffffff for a Q19 chain)            */
     int32_t rev;          /* strand '-'                                        */
-    int32_t n_match;      /* paf.rs:414-421 greedy match                       */
+    int32_t n_match;      /* paf.rs:178-186 greedy match                       */
     int32_t dv_st, dv_en; /* minimizer-index range of the match                */
     int32_t m_dv;         /* #minimizers of the dv sketch (idx.w, idx.k)       */
     int64_t sum_k;        /* sum of their spans                                */
@@ -128,14 +130,49 @@ typedef struct {
     float dv;             /* filled by the host (glibc powf)                   */
 } mm2g_read_result;
 
-/* Upload a batch of reads (ASCII, concatenated; offs has n_reads+1 entries). */
+/* ---------------------------------------------------------------- reads
+ * nt4 read batch: the input format of query reads on the device.  Reads cross
+ * PCIe and sit in HBM as nt4 codes (src/nt4.rs:2-10: A/a 0, C/c 1, G/g 2,
+ * T/t 3, anything else 4) packed 2 bits per base:
+ *   base i of read r: bits 2*(i%32) of words[pk_off[r] + i/32]  (code & 3;
+ *                     an ambiguous base stores 0)
+ *   a read with an ambiguous base (code 4) also has a bitmap:
+ *                     bit i%64 of words[amb_off[r] + i/64] = base i is ambiguous;
+ *                     amb_off[r] = UINT64_MAX for a read without one. */
+typedef struct {
+    uint32_t n_reads;
+    const uint64_t* lens;      /* bases per read                               */
+    const uint64_t* pk_off;    /* word offset of each read's codes             */
+    const uint64_t* amb_off;   /* word offset of its bitmap, or UINT64_MAX     */
+    const uint64_t* words;
+    uint64_t n_words;
+} mm2g_nt4_batch;
+/* Words mm2g_nt4_pack may need for these reads (codes plus worst-case bitmaps). */
+uint64_t mm2g_nt4_words_bound(const uint64_t* offs, uint32_t n_reads);
+/* Pack ASCII reads (seq[offs[r] .. offs[r+1])) into the nt4 format on
+ * n_threads host threads; fills pk_off/amb_off (n_reads each).  Returns the
+ * words written or a negative status.  The reference applies nt4 base by base
+ * inside sketch_sequence (src/sketch.rs:62). */
+int64_t mm2g_nt4_pack(const uint8_t* seq, const uint64_t* offs, uint32_t n_reads, uint64_t* pk_off, uint64_t* amb_off,
+                      uint64_t* words, uint64_t cap_words, int n_threads);
+
+/* Stage a batch of ASCII reads (concatenated; offs has n_reads+1 entries):
+ * packed to nt4 on host threads into pinned memory (double-buffered per
+ * context) and copied to HBM asynchronously on the context stream.  Returns
+ * before the copy ends; the caller may reuse its buffers at once.  A batch
+ * whose results were not collected is dropped. */
 int mm2g_batch_set_reads(mm2g_ctx* ctx, const uint8_t* seq, const uint64_t* offs, uint32_t n_reads);
-/* Run sketch -> filter -> lookup -> anchors -> sort -> chain DP (+rescue) ->
- * chain epilogue -> dv counts on the device for the resident batch; the
- * results stay on the device until mm2g_batch_results.  Equivalent to the
+/* The same for reads the caller already packed (copied into pinned staging). */
+int mm2g_batch_set_reads_nt4(mm2g_ctx* ctx, const mm2g_nt4_batch* batch);
+/* Queue sketch -> filter -> lookup -> anchors -> sort -> chain DP (+rescue) ->
+ * chain epilogue -> dv counts for the resident batch on the context stream and
+ * return without waiting (no host synchronisation inside).  Equivalent to the
  * Align flow (src/main.rs:189-230) applied to every read. */
 int mm2g_batch_map(mm2g_ctx* ctx, const mm2g_map_opts* opts);
-/* Copy per-read results to the host and finish dv (paf.rs:156-199). */
+/* Wait for the batch, copy per-read results to the caller and finish dv
+ * (paf.rs:189-199).  Batch workspaces are sized from the previous batches; if
+ * one was too small (the device flags it) it is grown and the batch mapped
+ * again here, transparently. */
 int mm2g_batch_results(mm2g_ctx* ctx, mm2g_read_result* out, uint32_t n_reads);
 /* Format PAF lines (write_paf, src/paf.rs:224-236) for n results; names
  * are the read names. Returns bytes written (or negative status); lines
@@ -150,6 +187,46 @@ int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, cons
  * of read r at [out_off[r], out_off[r+1]).  Pass NULL buffers to size. */
 int mm2g_batch_sketch(mm2g_ctx* ctx, int w, int k, uint32_t rid, uint64_t* out_off, uint64_t* out_ks, uint64_t* out_rps,
                       uint64_t cap);
+/* build_anchors_filtered(idx, mv, qlen, mid_occ) (src/seeds.rs:42-60) for every
+ * read of the resident batch, with the query minimizers collected and filtered
+ * as the Align flow does (collect_query_minimizers with opts->w/k, seeds.rs:7-11;
+ * filter_query_minimizers(10, 0.01), seeds.rs:13-36; main.rs:194-195) and the
+ * context's mid_occ.  Read r's anchors, sorted by (x, y) (seeds.rs:58), are the
+ * Anchor {x, y} pairs xy[2*a_off[r] ..] up to xy[2*a_off[r+1]]; a_off has
+ * n_reads+1 entries.  Returns the number of anchors; xy = NULL only sizes. */
+int64_t mm2g_seed_batch(mm2g_ctx* ctx, const mm2g_map_opts* opts, uint64_t* a_off, uint64_t* xy, uint64_t cap);
+
+/* ChainParams (src/lchain.rs:36-52). */
+typedef struct {
+    int32_t max_dist_x, max_dist_y, bw, max_chain_iter, min_chain_score, min_cnt;
+    float chn_pen_gap, chn_pen_skip;
+    int32_t max_chain_skip, max_drop, bw_long, rmq_rescue_size;
+    float rmq_rescue_ratio;
+} mm2g_chain_params;
+/* default_chain_params(k) (src/main.rs:105-123). */
+void mm2g_chain_params_default(mm2g_chain_params* p, int k);
+/* One read's chain: chain_dp_all's chains[0]/scores[0] (src/lchain.rs:59-176;
+ * the fallback chain under min_cnt >= 2), after rescue_long_join
+ * when requested (:321-330), with chain_qrange/chain_trange (:178-200). */
+typedef struct {
+    int32_t flags;        /* MM2G_R_MAPPED, MM2G_R_RESCUED, MM2G_R_PANIC (Q19 rid) */
+    int32_t n_anchors, score, cm;
+    int32_t qs, qe, ts, te;
+    int32_t rid, rev;     /* of the chain's last anchor; 0x7fffffff/1 for Q19 */
+} mm2g_chain_result;
+/* chain_dp_all(&anchors, &p) (src/lchain.rs:59) on the device for n_reads
+ * caller-owned anchor sets: read r's anchors are xy[2*(a_off[r]-a_off[0]) ..]
+ * ({x, y} pairs sorted by (x, y) as build_anchors_filtered returns them; one
+ * span for all), qlen[r] its query length.  rescue != 0 also runs
+ * rescue_long_join(anchors, chains, scores, p, qlen) (:321-330).  Optional
+ * outputs (NULL to skip), indexed like the anchors: f and pprev of the final
+ * DP pass (lchain.rs:67-91), and chain = the anchor indices of chains[0]
+ * (ascending, res[r].cm of them, relative to the read's first anchor).
+ * Unsupported (MM2G_E_UNSUP): chn_pen_skip != 0, min_cnt < 2, unsorted or
+ * mixed-span anchors. */
+int mm2g_chain_batch(mm2g_ctx* ctx, const mm2g_chain_params* p, uint32_t n_reads, const uint64_t* a_off, const uint64_t* xy,
+                     const int32_t* qlen, int rescue, mm2g_chain_result* res, int32_t* f, int32_t* pprev, uint32_t* chain);
+
 /* After mm2g_batch_map with debug enabled: the sorted anchors of read r
  * (build_anchors_filtered, src/seeds.rs:42-60) as (x, y) pairs, and the DP
  * arrays f/pprev of the final chain_dp_all pass (src/lchain.rs:59-91).
@@ -165,6 +242,43 @@ int64_t mm2g_debug_keep(mm2g_ctx* ctx, uint32_t r, uint8_t* keep, int64_t cap);
  * longest segment | #long segments << 16 (pass 0)] of the chain kernel
  * (6 values per read).  Returns the batch size. */
 int64_t mm2g_debug_chain_stats(mm2g_ctx* ctx, uint32_t* out6, uint32_t n);
+
+/* ---------------------------------------------------------------- knobs
+ * Tuning and test switches of one context (defaults in brackets).  The
+ * production path reads no environment variable; tests and A/B runs set these. */
+enum {
+    MM2G_KNOB_SORT_SMALL = 1,    /* reads with <= this many anchors: LDS bitonic sort, max 4096 [4096]        */
+    MM2G_KNOB_SEG_SMALL = 2,     /* sort cell segments ranked one thread per anchor up to this length [1024]  */
+    MM2G_KNOB_SEG_CHUNK = 3,     /* anchors per chain work item (multiple of 64) [4096]                       */
+    MM2G_KNOB_GIANT_MIN = 4,     /* rescue-pass segments of >= this many anchors try k_chain_giant [128]      */
+    MM2G_KNOB_GIANT_MIN0 = 5,    /* the same for pass 0 (exact mode); <= 0 = off [0]                          */
+    MM2G_KNOB_GIANT_LCAP = 6,    /* tests: cap of the LDS giant variant; 0 = its LDS capacity [0]             */
+    MM2G_KNOB_GIANT_GMAX = 7,    /* anchors per workgroup slice of the HBM giant variant; 0 = off [65536]     */
+    MM2G_KNOB_GIANT_GBLOCKS = 8, /* workgroups of the HBM giant variant [256]                                 */
+    MM2G_KNOB_FILTER = 9,        /* the sort's singleton filter [1]                                           */
+    MM2G_KNOB_LAZY = 10,         /* k_chain_long skips windows that cannot beat max_f [1]                     */
+    MM2G_KNOB_PRUNE = 11,        /* pass-0 segment pruning by the best-f lower bound [1]                      */
+    MM2G_KNOB_GIANT = 12,        /* the giant-segment kernels [1]                                             */
+    MM2G_KNOB_SKETCH_PROF = 13,  /* phase profile of k_sketch to stderr [0]                                   */
+    MM2G_KNOB_SORT_PROF = 14,    /* phase profile of k_sort_read to stderr [0]                                */
+    MM2G_KNOB_LSEG_PROF = 15,    /* slowest long segments to stderr [0]                                       */
+    MM2G_KNOB_MIDHIST_BINS = 16, /* bins of the device mid_occ histogram, 2..16384 [4096]                     */
+    MM2G_KNOB_SYNC_EACH = 17,    /* synchronise after every stage and report faults [0]                       */
+    MM2G_KNOB_HOST_THREADS = 18, /* host threads packing reads to nt4 [min(8, cores)]                         */
+    MM2G_KNOB_WS_MIN = 19,       /* tests: a batch's first map starts with minimizer slots, filter-table and
+                                    anchor workspaces of this many entries, forcing the re-map; 0 = off [0]   */
+    MM2G_KNOB_COUNT = 20
+};
+int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
+int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);
+/* Process-wide switches of the index build and .mmi load. */
+enum {
+    MM2G_IKNOB_IXCHUNK = 1,      /* GPU index build: bases per sketch view [65536]                            */
+    MM2G_IKNOB_IXPROF = 2,       /* GPU index build: phase times to stderr [0]                                */
+    MM2G_IKNOB_LOAD_THREADS = 3, /* .mmi load threads; 0 = min(32, cores) [0]                                 */
+    MM2G_IKNOB_COUNT = 4
+};
+int mm2g_set_index_knob(int knob, int64_t value);
 
 /* Per-kernel device time (HIP events on the context stream) accumulated over
  * mm2g_batch_map calls since the last reset: names[i], ms[i], calls[i]. */

@@ -37,6 +37,30 @@ class ReadResult(C.Structure):
 
 assert C.sizeof(ReadResult) == 72
 
+
+class Nt4Batch(C.Structure):
+    _fields_ = [("n_reads", C.c_uint32), ("lens", C.POINTER(C.c_uint64)), ("pk_off", C.POINTER(C.c_uint64)),
+                ("amb_off", C.POINTER(C.c_uint64)), ("words", C.POINTER(C.c_uint64)), ("n_words", C.c_uint64)]
+
+
+class ChainParams(C.Structure):
+    _fields_ = [("max_dist_x", C.c_int32), ("max_dist_y", C.c_int32), ("bw", C.c_int32), ("max_chain_iter", C.c_int32),
+                ("min_chain_score", C.c_int32), ("min_cnt", C.c_int32), ("chn_pen_gap", C.c_float), ("chn_pen_skip", C.c_float),
+                ("max_chain_skip", C.c_int32), ("max_drop", C.c_int32), ("bw_long", C.c_int32), ("rmq_rescue_size", C.c_int32),
+                ("rmq_rescue_ratio", C.c_float)]
+
+
+class ChainResult(C.Structure):
+    _fields_ = [("flags", C.c_int32), ("n_anchors", C.c_int32), ("score", C.c_int32), ("cm", C.c_int32), ("qs", C.c_int32),
+                ("qe", C.c_int32), ("ts", C.c_int32), ("te", C.c_int32), ("rid", C.c_int32), ("rev", C.c_int32)]
+
+
+# knobs (include/mm2g.h)
+KNOBS = {"sort_small": 1, "seg_small": 2, "seg_chunk": 3, "giant_min": 4, "giant_min0": 5, "giant_lcap": 6, "giant_gmax": 7,
+         "giant_gblocks": 8, "filter": 9, "lazy": 10, "prune": 11, "giant": 12, "sketch_prof": 13, "sort_prof": 14,
+         "lseg_prof": 15, "midhist_bins": 16, "sync_each": 17, "host_threads": 18, "ws_min": 19}
+INDEX_KNOBS = {"ixchunk": 1, "ixprof": 2, "load_threads": 3}
+
 _VP = C.c_void_p
 _P64 = C.POINTER(C.c_uint64)
 _PI32 = C.POINTER(C.c_int32)
@@ -81,6 +105,16 @@ SIGNATURES = {
     "mm2g_ctx_index_mid_occ": (C.c_int, [_VP, C.c_float, _PI32]),
     "mm2g_ctx_set_mid_occ": (C.c_int, [_VP, C.c_int32]),
     "mm2g_batch_counters": (C.c_int, [_VP, _P64, C.c_int]),
+    "mm2g_nt4_words_bound": (C.c_uint64, [_P64, C.c_uint32]),
+    "mm2g_nt4_pack": (C.c_int64, [C.c_void_p, _P64, C.c_uint32, _P64, _P64, _P64, C.c_uint64, C.c_int]),
+    "mm2g_batch_set_reads_nt4": (C.c_int, [_VP, C.POINTER(Nt4Batch)]),
+    "mm2g_seed_batch": (C.c_int64, [_VP, C.POINTER(MapOpts), _P64, _P64, C.c_uint64]),
+    "mm2g_chain_params_default": (None, [C.POINTER(ChainParams), C.c_int]),
+    "mm2g_chain_batch": (C.c_int, [_VP, C.POINTER(ChainParams), C.c_uint32, _P64, _P64, _PI32, C.c_int, C.POINTER(ChainResult),
+                                   _PI32, _PI32, C.POINTER(C.c_uint32)]),
+    "mm2g_ctx_set_knob": (C.c_int, [_VP, C.c_int, C.c_int64]),
+    "mm2g_ctx_get_knob": (C.c_int64, [_VP, C.c_int]),
+    "mm2g_set_index_knob": (C.c_int, [C.c_int, C.c_int64]),
 }
 
 _lib = None

@@ -11,8 +11,11 @@ reference (file:line)                      here
 ``Index::get`` (index.rs:143)              :meth:`Index.get`
 ``Index::calc_mid_occ`` (index.rs:124)     :meth:`Index.calc_mid_occ`
 ``Index::stats`` (index.rs:111)            :meth:`Index.stats`
-``build_anchors_filtered`` (seeds.rs:42)   :meth:`Device.map` + :meth:`Device.debug_anchors`
-``chain_dp_all`` (lchain.rs:59)            :meth:`Device.map` + :meth:`Device.debug_dp`
+``nt4`` (nt4.rs:2-10) on a read batch      :func:`nt4_pack`, :meth:`Device.set_reads_nt4`
+``build_anchors_filtered`` (seeds.rs:42)   :meth:`Device.seed_batch`
+``chain_dp_all`` (lchain.rs:59)            :meth:`Device.chain_batch`
+``rescue_long_join`` (lchain.rs:321)       :meth:`Device.chain_batch` (``rescue=True``)
+``default_chain_params`` (main.rs:105)     :func:`chain_params`
 ``write_paf`` (paf.rs:224)                 :meth:`Device.paf`
 Align flow (main.rs:189-230)               :func:`align`
 =========================================  ==========================================
@@ -29,7 +32,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib as L
-from ._lib import MapOpts, ReadResult, check, load
+from ._lib import ChainParams, ChainResult, MapOpts, Nt4Batch, ReadResult, check, load
 
 
 @dataclass
@@ -45,6 +48,34 @@ def map_opts(**kw) -> MapOpts:
     for k, v in kw.items():
         setattr(o, k, v)
     return o
+
+
+def chain_params(k: int = 15, **kw) -> ChainParams:
+    """``default_chain_params(k)`` (main.rs:105-123) with keyword overrides."""
+    p = ChainParams()
+    load().mm2g_chain_params_default(C.byref(p), k)
+    for name, v in kw.items():
+        setattr(p, name, v)
+    return p
+
+
+def set_index_knob(name: str, value: int) -> None:
+    """Process-wide switch of the index build / .mmi load (``mm2g_set_index_knob``)."""
+    check(load().mm2g_set_index_knob(L.INDEX_KNOBS[name], int(value)), "set_index_knob")
+
+
+def nt4_pack(seq: np.ndarray, offs: np.ndarray, threads: int = 4):
+    """ASCII reads -> the device nt4 format (include/mm2g.h): (pk_off, amb_off, words)."""
+    seq = np.ascontiguousarray(seq, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    n = len(offs) - 1
+    cap = int(load().mm2g_nt4_words_bound(offs.ctypes.data_as(L._P64), n))
+    pk = np.zeros(max(n, 1), np.uint64)
+    amb = np.zeros(max(n, 1), np.uint64)
+    words = np.zeros(max(cap, 1), np.uint64)
+    nw = check(load().mm2g_nt4_pack(seq.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(L._P64), n, pk.ctypes.data_as(L._P64),
+                                    amb.ctypes.data_as(L._P64), words.ctypes.data_as(L._P64), cap, threads), "nt4_pack")
+    return pk[:n], amb[:n], words[:nw]
 
 
 class Index:
@@ -212,6 +243,61 @@ class Device:
         n = len(offs) - 1
         check(load().mm2g_batch_set_reads(self._h, seq.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(L._P64), n), "set_reads")
         self.n_reads = n
+
+    def set_reads_nt4(self, lens: np.ndarray, pk_off: np.ndarray, amb_off: np.ndarray, words: np.ndarray) -> None:
+        """Stage reads the caller packed (:func:`nt4_pack`)."""
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        pk_off = np.ascontiguousarray(pk_off, dtype=np.uint64)
+        amb_off = np.ascontiguousarray(amb_off, dtype=np.uint64)
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        b = Nt4Batch(len(lens), lens.ctypes.data_as(L._P64), pk_off.ctypes.data_as(L._P64), amb_off.ctypes.data_as(L._P64),
+                     words.ctypes.data_as(L._P64), len(words))
+        check(load().mm2g_batch_set_reads_nt4(self._h, C.byref(b)), "set_reads_nt4")
+        self.n_reads = len(lens)
+
+    def set_knob(self, name: str, value: int) -> None:
+        check(load().mm2g_ctx_set_knob(self._h, L.KNOBS[name], int(value)), "set_knob")
+
+    def get_knob(self, name: str) -> int:
+        return check(load().mm2g_ctx_get_knob(self._h, L.KNOBS[name]), "get_knob")
+
+    def seed_batch(self, opts: Optional[MapOpts] = None) -> List[np.ndarray]:
+        """``build_anchors_filtered`` for every resident read: list of (A, 2) uint64 (x, y) arrays."""
+        o = opts if opts is not None else map_opts()
+        n = self.n_reads
+        off = np.zeros(n + 1, dtype=np.uint64)
+        A = check(load().mm2g_seed_batch(self._h, C.byref(o), off.ctypes.data_as(L._P64), None, 0), "seed_batch")
+        xy = np.zeros(2 * max(A, 1), dtype=np.uint64)
+        check(load().mm2g_seed_batch(self._h, C.byref(o), off.ctypes.data_as(L._P64), xy.ctypes.data_as(L._P64), A), "seed_batch")
+        xy = xy[: 2 * A].reshape(A, 2)
+        return [xy[int(off[r]):int(off[r + 1])] for r in range(n)]
+
+    def chain_batch(self, anchors: Sequence[np.ndarray], qlens: Sequence[int], params: Optional[ChainParams] = None,
+                    rescue: bool = True, want_dp: bool = False):
+        """``chain_dp_all`` (+ ``rescue_long_join``) on caller anchors, one (A, 2) (x, y) array per read.
+        Returns (results, chains[, f, pprev]) with per-read numpy arrays."""
+        p = params if params is not None else chain_params()
+        n = len(anchors)
+        cnt = np.array([len(a) for a in anchors], dtype=np.uint64)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(cnt)
+        A = int(off[-1])
+        xy = np.ascontiguousarray(np.concatenate([np.asarray(a, np.uint64).reshape(-1, 2) for a in anchors]) if A else
+                                  np.zeros((1, 2), np.uint64), dtype=np.uint64)
+        ql = np.ascontiguousarray(qlens, dtype=np.int32)
+        res = (ChainResult * max(n, 1))()
+        ch = np.zeros(max(A, 1), np.uint32)
+        f = np.zeros(max(A, 1), np.int32) if want_dp else None
+        pp = np.zeros(max(A, 1), np.int32) if want_dp else None
+        check(load().mm2g_chain_batch(self._h, C.byref(p), n, off.ctypes.data_as(L._P64), xy.ctypes.data_as(L._P64),
+                                      ql.ctypes.data_as(L._PI32), 1 if rescue else 0, res,
+                                      f.ctypes.data_as(L._PI32) if want_dp else None, pp.ctypes.data_as(L._PI32) if want_dp else None,
+                                      ch.ctypes.data_as(C.POINTER(C.c_uint32))), "chain_batch")
+        chains = [ch[int(off[r]):int(off[r]) + res[r].cm].astype(np.int64) for r in range(n)]
+        out = [res[r] for r in range(n)]
+        if want_dp:
+            return out, chains, [f[int(off[r]):int(off[r + 1])] for r in range(n)], [pp[int(off[r]):int(off[r + 1])] for r in range(n)]
+        return out, chains
 
     def sketch_sequences(self, seqs: Sequence[bytes], w: int, k: int, rid: int = 0) -> List[np.ndarray]:
         """``sketch_sequence`` for each sequence; returns (m, 2) uint64 arrays of (key_span, rid_pos_strand)."""

@@ -1,9 +1,11 @@
 // Host orchestration of the MI355X path and the C ABI declared in
 // include/mm2g.h.  One mm2g_ctx = one device + one HIP stream + the device
 // index + batch workspaces sized for 288 GB of HBM3E (buffers grow on demand,
-// never shrink).  The batch pipeline is a fixed sequence of kernel launches
-// with two small device->host reads (minimizer overflow/table size, anchor
-// total) used to size the workspaces.
+// never shrink).  A batch is: host nt4 packing into pinned staging + async H2D
+// (mm2g_batch_set_reads), a fixed sequence of kernel launches with no host
+// synchronisation (mm2g_batch_map), and one wait for the results
+// (mm2g_batch_results).  Workspaces are sized from earlier batches; the
+// device flags one that was too small and the batch is mapped again.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,11 +16,13 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mm2g.h"
 #include "mm2g_index.h"
 #include "mm2g_internal.h"
+#include "mm2g_reads.h"
 
 using namespace mm2g;
 
@@ -56,9 +60,34 @@ static int ensure(DevBuf& b, size_t n, T** out) {
 
 struct ProfSlot { std::string name; double ms = 0; int64_t calls = 0; };
 
+// pinned host staging of one read batch (header + nt4 words), double-buffered
+struct Stage { uint64_t* p = nullptr; uint64_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; };
+// minimizer slots of one sketch of the batch
+struct SketchBufs {
+    DevBuf base, end, x, y, cnt, need;
+    bool exact = false;    // slots sized by the true counts (after an overflow)
+    uint64_t cap = 0;      // minimizer slots allocated
+};
+
+static int64_t knob_default(int k) {
+    switch (k) {
+    case MM2G_KNOB_SORT_SMALL: return 4096;
+    case MM2G_KNOB_SEG_SMALL: return SEG_THREAD;
+    case MM2G_KNOB_SEG_CHUNK: return SEG_CHUNK;
+    case MM2G_KNOB_GIANT_MIN: return 128;
+    case MM2G_KNOB_GIANT_GMAX: return 65536;
+    case MM2G_KNOB_GIANT_GBLOCKS: return 256;
+    case MM2G_KNOB_FILTER: case MM2G_KNOB_LAZY: case MM2G_KNOB_PRUNE: case MM2G_KNOB_GIANT: return 1;
+    case MM2G_KNOB_MIDHIST_BINS: return 4096;
+    case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    default: return 0;
+    }
+}
+
 struct mm2g_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    int64_t knob[MM2G_KNOB_COUNT] = {};
     // index (device copy shared by every context it was shared with, same device)
     const HostIndex* hidx = nullptr;
     struct DevIndex { DevBuf tab, ix_pos, goff; uint32_t cells = 0; };
@@ -66,25 +95,32 @@ struct mm2g_ctx {
     uint32_t log2cap = 0;
     int32_t mid_occ = 10;
     bool have_index = false;
-    // batch
+    // batch: reads (device: rd_off[n+1] | pk_off[n] | amb_off[n] | nt4 words)
     uint32_t n_reads = 0;
     uint64_t total_bases = 0;
     uint32_t max_read_len = 0;
     std::vector<uint64_t> h_rd_off;
-    DevBuf rd_seq, rd_off;
-    DevBuf mz_base, mz_end, mz_x, mz_y, mz_cnt, keep, mz_n, mz_poff;
-    DevBuf mz2_base, mz2_end, mz2_x, mz2_y, mz2_cnt;
+    Stage stage[2]; int st_next = 0;
+    DevBuf rd_dev;
+    const uint64_t *d_rd_off = nullptr, *d_pk_off = nullptr, *d_amb_off = nullptr, *d_words = nullptr;
+    SketchBufs sk1, sk2;                   // CLI (w, k) sketch; index (w, k) sketch for dv when they differ
+    DevBuf keep, mz_n, mz_poff;
     DevBuf tab_off, tab_key, tab_cnt;
     DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
     DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, flag, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
-    uint64_t* h_small = nullptr;          // pinned, 16 u64
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
+    DevBuf dstat;                          // batch status block (BS_* word, workspace needs, counters)
+    DevBuf chain_rdoff;                    // mm2g_chain_batch: prefix sums of the caller's qlen
+    uint64_t cap_tab = 0, cap_A = 0;       // filter-table entries / anchors the workspaces hold
+    uint64_t* h_stat = nullptr;            // pinned copy of dstat (8 u64)
+    hipEvent_t ev_done = nullptr;          // end of the queued batch
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
-    bool mapped = false, dv_separate = false;
+    bool mapped = false, collected = false, stop_after_sort = false, dv_separate = false;
+    bool redo = false;                     // inside wait_batch's re-map (MM2G_KNOB_WS_MIN applies to first maps only)
     uint64_t n_anchors = 0;
     KeyLayout kl{};
     mm2g_map_opts last_opts{};
-    std::vector<int16_t> h_lut; float lut_gap = -1; int lut_n = 0;
+    std::vector<int16_t> h_lut; float lut_gap = -1; int lut_n = 0; bool lut_dirty = true; void* lut_dev = nullptr;
     bool debug = false;
     // profiling
     bool prof = false;
@@ -122,17 +158,14 @@ struct mm2g_ctx {
     }
 };
 
-// MM2G_SYNC=1: synchronise after every stage and report the first failing
-// stage (and, in MM2G_CHECKED builds, the first out-of-range index).
-static bool g_sync_each = getenv("MM2G_SYNC") && atoi(getenv("MM2G_SYNC")) != 0;
-// a debug/tuning switch is on when the variable is set to a non-zero number
-static bool env_on(const char* name) { const char* v = getenv(name); return v && atoi(v) != 0; }
+// MM2G_KNOB_SYNC_EACH: synchronise after every stage and report the first
+// failing stage (and, in MM2G_CHECKED builds, the first out-of-range index).
 struct ProfScope {
     mm2g_ctx* c; int i; hipEvent_t e0{}; const char* name;
     ProfScope(mm2g_ctx* c_, const char* n) : c(c_), name(n) { i = c->prof_begin(n, e0); }
     ~ProfScope() {
         c->prof_end(i, e0);
-        if (g_sync_each) {
+        if (c->knob[MM2G_KNOB_SYNC_EACH]) {
             unsigned long long ck[4] = {0, 0, 0, 0};
             int e = mm2g_checked_read(ck, c->stream);
             if (e != 0 || ck[0] != 0) {
@@ -331,7 +364,10 @@ int mm2g_ctx_create(int device, mm2g_ctx** out) {
     std::unique_ptr<mm2g_ctx> c(new mm2g_ctx());
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipHostMalloc((void**)&c->h_small, 16 * sizeof(uint64_t), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c->h_stat, 8 * sizeof(uint64_t), hipHostMallocDefault));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+    for (auto& S : c->stage) HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+    for (int k = 0; k < MM2G_KNOB_COUNT; ++k) c->knob[k] = knob_default(k);
     *out = c.release();
     return 0;
 }
@@ -340,7 +376,9 @@ void mm2g_ctx_destroy(mm2g_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->h_stat) (void)hipHostFree(c->h_stat);
+    for (auto& S : c->stage) { if (S.p) (void)hipHostFree(S.p); if (S.ev) (void)hipEventDestroy(S.ev); }
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->h_out) (void)hipHostFree(c->h_out);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -420,7 +458,7 @@ int mm2g_ctx_index_mid_occ(mm2g_ctx* c, float frac, int32_t* out) {
     if (!c->have_index) return set_err(MM2G_E_STATE, "no index uploaded");
     HIPCHK(hipSetDevice(c->device));
     uint32_t nbins = 4096;
-    if (const char* e = getenv("MM2G_MIDHIST_BINS")) nbins = (uint32_t)std::max(2, std::min(16384, atoi(e)));   // tests
+    nbins = (uint32_t)std::max<int64_t>(2, std::min<int64_t>(16384, c->knob[MM2G_KNOB_MIDHIST_BINS]));
     const uint64_t cap = 1ULL << c->log2cap;
     const IxEntry* tab = (const IxEntry*)c->dix->tab.p;
     DevBuf dh, dn, dv;
@@ -471,78 +509,155 @@ void mm2g_map_opts_default(mm2g_map_opts* o) {
     o->min_cnt = 3; o->min_chain_score = 40; o->mask_level = 0.5f; o->pri_ratio = 0.8f; o->best_n = 5;
 }
 
+uint64_t mm2g_nt4_words_bound(const uint64_t* offs, uint32_t n_reads) { return offs ? nt4_words_bound(offs, n_reads) : 0; }
+int64_t mm2g_nt4_pack(const uint8_t* seq, const uint64_t* offs, uint32_t n_reads, uint64_t* pk_off, uint64_t* amb_off, uint64_t* words,
+                      uint64_t cap_words, int n_threads) {
+    if (n_reads && (!seq || !offs || !pk_off || !amb_off || !words)) return set_err(MM2G_E_ARG, "null argument");
+    for (uint32_t i = 0; i < n_reads; ++i)
+        if (offs[i + 1] < offs[i]) return set_err(MM2G_E_ARG, "offsets must be non-decreasing");
+    const int64_t w = nt4_pack(seq, offs, n_reads, pk_off, amb_off, words, cap_words, std::max(1, n_threads));
+    if (w < 0) return set_err(MM2G_E_ARG, "output capacity too small (%lld words needed at least)", (long long)-w);
+    return w;
+}
+
+// Record the batch geometry and queue the H2D copy of the staged buffer
+// (header + nt4 words) on the context stream.
+static int stage_commit(mm2g_ctx* c, Stage& S, uint32_t n, uint64_t total_words) {
+    uint64_t* d;
+    ENSURE(c->rd_dev, uint64_t, total_words, d);
+    HIPCHK(hipMemcpyAsync(d, S.p, total_words * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(S.ev, c->stream));
+    S.pending = true;
+    c->st_next ^= 1;
+    c->d_rd_off = d; c->d_pk_off = d + n + 1; c->d_amb_off = d + 2 * (size_t)n + 1; c->d_words = d + 3 * (size_t)n + 1;
+    c->n_reads = n; c->total_bases = c->h_rd_off[n];
+    c->mapped = false;
+    c->sk1.exact = c->sk2.exact = false;
+    return 0;
+}
+
+// The next free pinned staging buffer with room for `words` u64 (waits for its last H2D).
+static int stage_acquire(mm2g_ctx* c, uint64_t words, Stage** out) {
+    Stage& S = c->stage[c->st_next];
+    if (S.pending) { HIPCHK(hipEventSynchronize(S.ev)); S.pending = false; }
+    if (S.cap < words) {
+        if (S.p) (void)hipHostFree(S.p);
+        S.p = nullptr; S.cap = 0;
+        const uint64_t nc = words + words / 4 + 1024;
+        HIPCHK(hipHostMalloc((void**)&S.p, nc * 8, hipHostMallocDefault));
+        S.cap = nc;
+    }
+    *out = &S;
+    return 0;
+}
+
+static int check_offsets(mm2g_ctx* c, const uint64_t* offs, uint32_t n) {
+    c->h_rd_off.assign((size_t)n + 1, 0);
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (offs[i + 1] < offs[i]) return set_err(MM2G_E_ARG, "offsets must be non-decreasing");
+        const uint64_t L = offs[i + 1] - offs[i];
+        if (L >= (1ULL << 31)) return set_err(MM2G_E_UNSUP, "reads must be shorter than 2^31");
+        mx = std::max<uint32_t>(mx, (uint32_t)L);
+        c->h_rd_off[i + 1] = c->h_rd_off[i] + L;
+    }
+    c->max_read_len = mx;
+    return 0;
+}
+
 int mm2g_batch_set_reads(mm2g_ctx* c, const uint8_t* seq, const uint64_t* offs, uint32_t n_reads) {
     if (!c || (n_reads && (!seq || !offs))) return set_err(MM2G_E_ARG, "null argument");
     HIPCHK(hipSetDevice(c->device));
-    uint64_t total = n_reads ? offs[n_reads] - offs[0] : 0;
-    c->h_rd_off.assign(n_reads + 1, 0);
-    uint32_t mx = 0;
-    for (uint32_t i = 0; i < n_reads; ++i) {
-        if (offs[i + 1] < offs[i]) return set_err(MM2G_E_ARG, "offsets must be non-decreasing");
-        uint64_t L = offs[i + 1] - offs[i];
-        if (L >= (1ULL << 31)) return set_err(MM2G_E_UNSUP, "reads must be shorter than 2^31");
-        mx = std::max<uint32_t>(mx, (uint32_t)L);
-        c->h_rd_off[i + 1] = offs[i + 1] - offs[0];
-    }
-    uint8_t* dseq; uint64_t* doff;
-    ENSURE(c->rd_seq, uint8_t, total + 64, dseq);
-    ENSURE(c->rd_off, uint64_t, n_reads + 1, doff);
-    if (total) HIPCHK(hipMemcpyAsync(dseq, seq + offs[0], total, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(doff, c->h_rd_off.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    c->n_reads = n_reads; c->total_bases = total; c->max_read_len = mx;
-    c->mapped = false;
-    return 0;
+    static const uint64_t zero = 0;
+    if (!n_reads) offs = &zero;
+    if (int e = check_offsets(c, offs, n_reads)) return e;
+    const uint64_t hdr = 3 * (uint64_t)n_reads + 1;
+    Stage* S;
+    if (int e = stage_acquire(c, hdr + nt4_words_bound(offs, n_reads), &S)) return e;
+    uint64_t* h = S->p;
+    memcpy(h, c->h_rd_off.data(), ((size_t)n_reads + 1) * 8);
+    const int64_t nw = nt4_pack(seq, offs, n_reads, h + n_reads + 1, h + 2 * (size_t)n_reads + 1, h + hdr, S->cap - hdr,
+                                (int)c->knob[MM2G_KNOB_HOST_THREADS]);
+    if (nw < 0) return set_err(MM2G_E_NOMEM, "nt4 staging too small");
+    return stage_commit(c, *S, n_reads, hdr + (uint64_t)nw);
 }
 
-// Sketch the resident batch into (base, end, x, y, cnt); exact two-pass fallback
-// when a sequence overflows its L+16 slot.
-static int run_sketch(mm2g_ctx* c, int w, int k, DevBuf& b_base, DevBuf& b_end, DevBuf& b_x, DevBuf& b_y, DevBuf& b_cnt, uint64_t* total_out) {
+int mm2g_batch_set_reads_nt4(mm2g_ctx* c, const mm2g_nt4_batch* b) {
+    if (!c || !b || (b->n_reads && (!b->lens || !b->pk_off || !b->amb_off || !b->words)))
+        return set_err(MM2G_E_ARG, "null argument");
+    HIPCHK(hipSetDevice(c->device));
+    const uint32_t n = b->n_reads;
+    std::vector<uint64_t> offs((size_t)n + 1, 0);
+    for (uint32_t r = 0; r < n; ++r) {
+        const uint64_t L = b->lens[r];
+        if (b->pk_off[r] + (L + 31) / 32 > b->n_words) return set_err(MM2G_E_ARG, "read %u: codes beyond n_words", r);
+        if (b->amb_off[r] != ~0ULL && b->amb_off[r] + (L + 63) / 64 > b->n_words) return set_err(MM2G_E_ARG, "read %u: bitmap beyond n_words", r);
+        offs[r + 1] = offs[r] + L;
+    }
+    if (int e = check_offsets(c, offs.data(), n)) return e;
+    const uint64_t hdr = 3 * (uint64_t)n + 1;
+    Stage* S;
+    if (int e = stage_acquire(c, hdr + b->n_words, &S)) return e;
+    uint64_t* h = S->p;
+    memcpy(h, c->h_rd_off.data(), ((size_t)n + 1) * 8);
+    if (n) {
+        memcpy(h + n + 1, b->pk_off, (size_t)n * 8);
+        memcpy(h + 2 * (size_t)n + 1, b->amb_off, (size_t)n * 8);
+    }
+    if (b->n_words) memcpy(h + hdr, b->words, b->n_words * 8);
+    return stage_commit(c, *S, n, hdr + b->n_words);
+}
+
+// Sketch the resident batch into sk's slots (one slot of L+16 per read, or the
+// exact layout a previous overflow recorded).  A read whose minimizers do not
+// fit is clamped and flagged in *ovf; mm2g_batch_results re-runs the batch.
+static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf) {
     const uint32_t n = c->n_reads;
-    uint64_t *base, *end, *x; uint32_t *y, *cnt; int32_t* ovf;
-    ENSURE(b_base, uint64_t, n + 1, base); ENSURE(b_end, uint64_t, n + 1, end);
-    ENSURE(b_cnt, uint32_t, n + 1, cnt);
-    ENSURE(c->flag, int32_t, 4, ovf);
-    const uint64_t cap = c->total_bases + 16ull * n + 16;
-    ENSURE(b_x, uint64_t, cap, x); ENSURE(b_y, uint32_t, cap, y);
-    {
+    uint64_t *base, *end, *x; uint32_t *y, *cnt, *need;
+    ENSURE(B.base, uint64_t, n + 1, base); ENSURE(B.end, uint64_t, n + 1, end);
+    ENSURE(B.cnt, uint32_t, n + 1, cnt); ENSURE(B.need, uint32_t, n + 1, need);
+    const uint32_t slot = c->redo ? 0u : (uint32_t)std::max<int64_t>(0, std::min<int64_t>(c->knob[MM2G_KNOB_WS_MIN], 1 << 30));
+    if (!B.exact) B.cap = slot ? (uint64_t)slot * n + 16 : c->total_bases + 16ull * n + 16;
+    ENSURE(B.x, uint64_t, B.cap, x); ENSURE(B.y, uint32_t, B.cap, y);
+    if (!B.exact) {
         ProfScope ps(c, "mz_base");
-        LCHK(launch_mz_base(n, (const uint64_t*)c->rd_off.p, base, end, c->stream));
+        LCHK(launch_mz_base(n, c->d_rd_off, base, end, slot, c->stream));
     }
-    HIPCHK(hipMemsetAsync(ovf, 0, 16, c->stream));
-    SketchArgs a{(const uint8_t*)c->rd_seq.p, (const uint64_t*)c->rd_off.p, n, w, k, base, end, x, y, cnt, ovf};
-    {
-        ProfScope ps(c, "sketch");
-        uint64_t* skp = nullptr;
-        if (env_on("MM2G_SKETCH_PROF")) { HIPCHK(hipMalloc(&skp, (size_t)n * 64)); HIPCHK(hipMemsetAsync(skp, 0, (size_t)n * 64, c->stream)); a.prof = skp; }
-        LCHK(launch_sketch(a, grid_for(n), c->stream));
-        if (skp) dump_sketch_prof(c, skp, n);
-    }
-    HIPCHK(hipMemcpyAsync(c->h_small, ovf, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    int32_t over = (int32_t)(c->h_small[0] & 0xffffffffu);
-    if (over) {
-        std::vector<uint32_t> hc(n);
-        HIPCHK(hipMemcpy(hc.data(), cnt, n * 4, hipMemcpyDeviceToHost));
-        std::vector<uint64_t> hb(n + 1), he(n + 1);
-        uint64_t run = 0;
-        for (uint32_t i = 0; i < n; ++i) { hb[i] = run; run += hc[i]; he[i] = run; }
-        ENSURE(b_x, uint64_t, run + 1, x); ENSURE(b_y, uint32_t, run + 1, y);
-        HIPCHK(hipMemcpy(base, hb.data(), n * 8, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(end, he.data(), n * 8, hipMemcpyHostToDevice));
-        HIPCHK(hipMemsetAsync(ovf, 0, 16, c->stream));
-        SketchArgs b2{(const uint8_t*)c->rd_seq.p, (const uint64_t*)c->rd_off.p, n, w, k, base, end, x, y, cnt, ovf};
-        LCHK(launch_sketch(b2, grid_for(n), c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-    }
-    if (total_out) *total_out = cap;
+    SketchArgs a{nullptr, c->d_rd_off, n, w, k, base, end, x, y, cnt, ovf};
+    a.pk_words = c->d_words; a.pk_off = c->d_pk_off; a.amb_off = c->d_amb_off; a.mz_need = need;
+    ProfScope ps(c, "sketch");
+    uint64_t* skp = nullptr;
+    if (c->knob[MM2G_KNOB_SKETCH_PROF]) { HIPCHK(hipMalloc(&skp, (size_t)n * 64)); HIPCHK(hipMemsetAsync(skp, 0, (size_t)n * 64, c->stream)); a.prof = skp; }
+    LCHK(launch_sketch(a, grid_for(n), c->stream));
+    if (skp) dump_sketch_prof(c, skp, n);
     return 0;
 }
 
-static void build_lut(mm2g_ctx* c, int k, int n) {
+// After an overflow: slots sized by each read's true minimizer count.
+static int sketch_exact_layout(mm2g_ctx* c, SketchBufs& B) {
+    const uint32_t n = c->n_reads;
+    std::vector<uint32_t> need(n);
+    if (n) HIPCHK(hipMemcpyAsync(need.data(), B.need.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> hb((size_t)n + 1), he((size_t)n + 1);
+    uint64_t run = 0;
+    for (uint32_t i = 0; i < n; ++i) { hb[i] = run; run += need[i]; he[i] = run; }
+    B.cap = run + 1;
+    B.exact = true;
+    uint64_t *base, *end;
+    ENSURE(B.base, uint64_t, n + 1, base); ENSURE(B.end, uint64_t, n + 1, end);
+    if (n) {
+        HIPCHK(hipMemcpyAsync(base, hb.data(), (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(end, he.data(), (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+static void build_lut(mm2g_ctx* c, float gap, int n) {
     // comput_sc penalty (src/lchain.rs:28-31) for chn_pen_skip == 0 (main.rs:116):
     // (gap*dd + 0*dg + 0.5*log2(dd+1)) as i32, f32 op by op, glibc logf.
-    const float gap = 0.01f * 0.8f * (float)k;
+    // gap = chn_pen_gap = 0.01f * 0.8f * k (main.rs:106-107)
     if (gap == c->lut_gap && n <= c->lut_n) return;
     c->h_lut.assign(n, 0);
     for (int dd = 0; dd < n; ++dd) {
@@ -553,163 +668,79 @@ static void build_lut(mm2g_ctx* c, int k, int n) {
         c->h_lut[dd] = (int16_t)(int32_t)v;
     }
     c->lut_gap = gap; c->lut_n = n;
+    c->lut_dirty = true;
 }
 
-int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
-    if (!c || !o) return set_err(MM2G_E_ARG, "null argument");
-    if (!c->have_index) return set_err(MM2G_E_STATE, "no index uploaded");
+// Argument checks of the Align flow (main.rs:189-230) shared by map and the stage entry points.
+static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_t& mdx1) {
     if (!(o->w > 0 && o->w < 256 && o->k > 0 && o->k <= 28)) return set_err(MM2G_E_ARG, "invalid w/k (0 < w < 256, 0 < k <= 28)");
     if (o->min_cnt < 2) return set_err(MM2G_E_UNSUP, "-n < 2 is outside the supported parity envelope (DESIGN.md Q4)");
     if (o->bw < 0 || o->bw_long < 0) return set_err(MM2G_E_ARG, "negative bandwidth");
-    const int32_t mdx0 = std::max(o->max_gap, o->bw), mdx1 = std::max(o->max_gap, o->bw_long);
-    const int lut_need = std::max(o->bw, o->bw_long) + 1;
-    if (lut_need > 60000) return set_err(MM2G_E_UNSUP, "bandwidth > 59999 not supported");
+    mdx0 = std::max(o->max_gap, o->bw); mdx1 = std::max(o->max_gap, o->bw_long);
+    if (std::max(o->bw, o->bw_long) + 1 > 60000) return set_err(MM2G_E_UNSUP, "bandwidth > 59999 not supported");
     // rpos_j + max_dist_x is i32 in the reference; keep it from wrapping (DESIGN.md Q-envelope)
-    if ((uint64_t)c->hidx->max_len + (uint64_t)std::max(mdx0, mdx1) >= (1ULL << 31))
+    if (c->hidx && (uint64_t)c->hidx->max_len + (uint64_t)std::max(mdx0, mdx1) >= (1ULL << 31))
         return set_err(MM2G_E_UNSUP, "reference length + max gap must stay below 2^31");
-    HIPCHK(hipSetDevice(c->device));
-    const HostIndex& H = *c->hidx;
-    const uint32_t n = c->n_reads;
-    c->mapped = false;
-    c->last_opts = *o;
-    // key layout
-    KeyLayout kl;
-    kl.n_seq = H.n_seq;
-    kl.qb = std::max<uint32_t>(1, bit_width(c->max_read_len));
-    kl.rb = std::max<uint32_t>(1, bit_width(H.max_len));
-    kl.gb = std::max<uint32_t>(1, bit_width(2ull * H.n_seq));
-    if (kl.qb + kl.rb + kl.gb > 64) return set_err(MM2G_E_UNSUP, "anchor key needs %u bits (> 64)", kl.qb + kl.rb + kl.gb);
-    c->kl = kl;
-    ReadOut* out;
-    ENSURE(c->outb, ReadOut, n + 1, out);
-    HIPCHK(hipMemsetAsync(out, 0, sizeof(ReadOut) * (n + 1), c->stream));
-    if (n == 0) { c->mapped = true; c->n_anchors = 0; return 0; }
-    // 1. sketch (CLI w/k, rid 0: seeds.rs:7-11)
-    int e = run_sketch(c, o->w, o->k, c->mz_base, c->mz_end, c->mz_x, c->mz_y, c->mz_cnt, nullptr);
-    if (e) return e;
-    const uint64_t mcap = c->mz_x.cap / 8;
-    uint64_t* mz_base = (uint64_t*)c->mz_base.p; uint32_t* mz_cnt = (uint32_t*)c->mz_cnt.p;
-    // 2. query filter (seeds.rs:13-36; (10, 0.01) hard-wired at main.rs:195)
-    uint64_t* tab_off; uint8_t* keep;
-    ENSURE(c->tab_off, uint64_t, n + 1, tab_off);
-    ENSURE(c->keep, uint8_t, mcap, keep);
-    {
-        ProfScope ps(c, "scan");
-        LCHK(launch_excl_scan(mz_cnt, n, tab_off, 1, 10, c->stream));
-    }
-    HIPCHK(hipMemcpyAsync(c->h_small, tab_off + n, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const uint64_t tab_total = c->h_small[0];
-    uint64_t* tkey; uint32_t* tcnt;
-    ENSURE(c->tab_key, uint64_t, tab_total, tkey);
-    ENSURE(c->tab_cnt, uint32_t, tab_total, tcnt);
-    {
-        FilterArgs fa{n, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, tab_off, tkey, tcnt, keep, 10, 0.01f};
-        ProfScope ps(c, "filter");
-        LCHK(launch_filter(fa, o->k, grid_for(n), c->stream));
-    }
-    // 3. lookup + anchor count (index.rs:143-154, seeds.rs:42-57)
-    uint32_t *mz_n, *mz_poff, *a_cnt; uint64_t* a_off;
-    ENSURE(c->mz_n, uint32_t, mcap, mz_n); ENSURE(c->mz_poff, uint32_t, mcap, mz_poff);
-    ENSURE(c->a_cnt, uint32_t, n + 1, a_cnt); ENSURE(c->a_off, uint64_t, n + 1, a_off);
-    uint32_t* a_part;
-    ENSURE(c->a_part, uint32_t, (size_t)n * (SEED_PARTS - 1), a_part);
-    SeedArgs sa{n, (const uint64_t*)c->rd_off.p, mz_base, mz_cnt, (const uint64_t*)c->mz_x.p, (const uint32_t*)c->mz_y.p, keep,
-                (const IxEntry*)c->dix->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->dix->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k,
-                0, c->dix->ix_pos.cap / 8, mcap, out, a_part};
-    {
-        ProfScope ps(c, "seed_count");
-        LCHK(launch_seed_count(sa, grid_for(n), c->stream));
-    }
-    {
-        ProfScope ps(c, "scan");
-        LCHK(launch_excl_scan(a_cnt, n, a_off, 0, 0, c->stream));
-    }
-    HIPCHK(hipMemcpyAsync(c->h_small, a_off + n, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    const uint64_t A = c->h_small[0];
-    c->n_anchors = A;
-    uint64_t *keys, *ktmp; int32_t *fb, *pb;
-    ENSURE(c->keys, uint64_t, A, keys); ENSURE(c->keys_tmp, uint64_t, A, ktmp);
-    ENSURE(c->fbuf, int32_t, A, fb); ENSURE(c->ppbuf, int32_t, A, pb);
-    sa.keys = keys; sa.cap_keys = c->keys.cap / 8;
-    {
-        ProfScope ps(c, "seed_write");
-        LCHK(launch_seed_write(sa, grid_for(n), c->stream));
-    }
-    // 4. anchor sort (seeds.rs:58)
-    uint32_t* cnt2; uint64_t* smax;
-    ENSURE(c->cnt2, uint32_t, n, cnt2);
-    ENSURE(c->smax, uint64_t, n, smax);
-    // the singleton filter is off in debug mode (full anchor/DP arrays for the parity tests)
-    SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
-                (c->debug || env_on("MM2G_NO_FILTER")) ? 0u : c->dix->cells, cnt2, smax, 4096u, nullptr, 0u, SEG_THREAD, nullptr};
-    uint64_t* sprof = nullptr;
-    if (env_on("MM2G_SORT_PROF")) { HIPCHK(hipMalloc(&sprof, (size_t)n * 64)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 64, c->stream)); so.prof = sprof; }
-    if (const char* e = getenv("MM2G_SORT_SMALL")) so.small_max = std::min<uint32_t>((uint32_t)atoi(e), 4096u);   // tests
-    if (const char* e = getenv("MM2G_SEG_SMALL")) so.seg_small = std::max(1u, std::min<uint32_t>((uint32_t)atoi(e), SEG_THREAD));   // tests
-    {
-        ProfScope ps(c, "sort_small");
-        LCHK(launch_sort_read(0, so, c->stream));
-    }
-    {
-        ProfScope ps(c, "sort_large");
-        LCHK(launch_sort_read(1, so, c->stream));
-    }
-    if (sprof) dump_sort_prof(c, sprof, n);
-    // the sorted anchors are in the tmp buffer: swap the roles for everything downstream
-    std::swap(c->keys.p, c->keys_tmp.p); std::swap(c->keys.cap, c->keys_tmp.cap);
-    std::swap(keys, ktmp);
-    // 5. chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
-    build_lut(c, o->k, lut_need);
+    return 0;
+}
+
+// Chain DP + fallback + rescue (lchain.rs:59-176, 321-330; main.rs:209-215)
+// over the sorted keys of the batch (cnt2/smax: the sort's singleton filter).
+// full: exact f/pprev for every anchor (debug mode, mm2g_chain_batch with DP
+// arrays requested): no segment pruning, no lazy windows.
+static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const ChainKParams& P0, float gap, int npass, int32_t mdx1,
+                     int32_t mdy1, int32_t bw_long, uint64_t A_cap, const uint64_t* a_off, const uint32_t* a_cnt, uint64_t* keys,
+                     uint64_t* ktmp, const uint32_t* cnt2, const uint64_t* smax, ReadOut* out, const uint32_t* abort, bool full) {
+    int32_t *fb, *pb;
+    ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
+    build_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1);
     int16_t* lut; uint32_t* work;
     ENSURE(c->lut, int16_t, c->h_lut.size(), lut);
     ENSURE(c->work, uint32_t, 4, work);
-    HIPCHK(hipMemcpyAsync(lut, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice, c->stream));
+    if (c->lut_dirty || c->lut_dev != c->lut.p) {   // the pen LUT stays resident; copied only when it changes
+        HIPCHK(hipMemcpyAsync(lut, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->lut_dirty = false; c->lut_dev = c->lut.p;
+    }
     HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));
-    ChainKParams P{};
-    P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
-    P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
-    // heaviest reads first; grid = what is co-resident (one wave per read, static hand-out)
     uint32_t* order;
     ENSURE(c->order, uint32_t, n, order);
     int32_t* tmark;
-    ENSURE(c->tmark, int32_t, A, tmark);
-    const uint32_t lcap = (uint32_t)std::min<uint64_t>(A / (CHAIN_MED + 1) + 64, 0xffffffffu);
+    ENSURE(c->tmark, int32_t, A_cap, tmark);
+    const uint32_t lcap = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_MED + 1) + 64, 0xffffffffu);
     uint4* lseg; uint32_t *lseg_n, *lseg_order; unsigned long long* rbest;
     ENSURE(c->lseg, uint4, lcap, lseg);
     ENSURE(c->lseg_order, uint32_t, lcap, lseg_order);
     ENSURE(c->lseg_n, uint32_t, 4, lseg_n);
     ENSURE(c->rbest, unsigned long long, n, rbest);
-    const uint32_t mcap2 = (uint32_t)std::min<uint64_t>(A / (CHAIN_TINY + 1) + 64, 0xffffffffu);
+    const uint32_t mcap2 = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_TINY + 1) + 64, 0xffffffffu);
     uint4* mseg;
     ENSURE(c->mseg, uint4, mcap2, mseg);
     LCHK(launch_read_order(n, a_cnt, order, c->stream));
-    ChainArgs ca{n, (const uint64_t*)c->rd_off.p, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P, kl, out, work,
-                 std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, nullptr, order, A, std::min<int32_t>((int32_t)n, 4 * 256), tmark,
+    const int64_t* K = c->knob;
+    const bool lazy = !full && K[MM2G_KNOB_LAZY];
+    ChainArgs ca{n, rd_off, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P0, c->kl, out, work,
+                 std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, nullptr, order, A_cap, std::min<int32_t>((int32_t)n, 4 * 256), tmark,
                  lseg, lseg_n, lcap, lseg_order, rbest, cnt2, smax, mseg, lseg_n + 2, lseg_n + 3, mcap2, nullptr, 0u,
-                 (c->debug || env_on("MM2G_NO_LAZY")) ? 0u : 1u, nullptr, 0u};
+                 lazy ? 1u : 0u, nullptr, 0u};
+    ca.abort = abort;
     int32_t* fmin_buf = nullptr;
-    if (!c->debug && !env_on("MM2G_NO_PRUNE")) ENSURE(c->fmin, int32_t, n, fmin_buf);
+    if (!full && K[MM2G_KNOB_PRUNE]) ENSURE(c->fmin, int32_t, n, fmin_buf);
     uint32_t* item_off;
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
-    ca.seg_chunk = (uint32_t)SEG_CHUNK;
+    ca.seg_chunk = std::max<uint32_t>(64u, (uint32_t)K[MM2G_KNOB_SEG_CHUNK] & ~63u);
     // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
     // settle in a few no-break policy-iteration rounds.  Pass 0's long segments
     // are real chains whose windows carry many mark sources: k_chain_long is
-    // faster on the usual few-hundred-anchor ones.
-    const char* genv = getenv("MM2G_GIANT_MIN");   // tests: both passes
-    // Pass 0's exact mode is off by default: measured 15x (C3) and 6x (C5)
-    // slower than k_chain_long on real chains.
-    uint32_t giant_min[2] = {genv ? (uint32_t)std::max(2, atoi(genv)) : 0xffffffffu,
-                             genv ? (uint32_t)std::max(2, atoi(genv)) : 128u};
-    if (const char* e = getenv("MM2G_GIANT_MIN0")) giant_min[0] = (uint32_t)std::max(2, atoi(e));   // A/B
-    if (const char* e = getenv("MM2G_SEG_CHUNK")) ca.seg_chunk = std::max(64u, (uint32_t)atoi(e) & ~63u);   // tests
-    for (int pass = 0; pass < 2; ++pass) {
+    // faster on the usual few-hundred-anchor ones; its
+    // exact mode is off by default (measured 15x (C3) and 6x (C5) slower).
+    uint32_t giant_min[2] = {K[MM2G_KNOB_GIANT_MIN0] > 0 ? (uint32_t)std::max<int64_t>(2, K[MM2G_KNOB_GIANT_MIN0]) : 0xffffffffu,
+                             (uint32_t)std::max<int64_t>(2, K[MM2G_KNOB_GIANT_MIN])};
+    for (int pass = 0; pass < npass; ++pass) {
         if (pass == 1) {
-            ca.P.pass = 1; ca.P.bw = o->bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = std::max(o->max_gap, o->bw_long);
-            ca.P.lut_n = o->bw_long + 1; ca.lseg_n = lseg_n + 1;
+            ca.P.pass = 1; ca.P.bw = bw_long; ca.P.max_dist_x = mdx1; ca.P.max_dist_y = mdy1;
+            ca.P.lut_n = bw_long + 1; ca.lseg_n = lseg_n + 1;
         }
         int sb = chain_max_blocks(ca.P.lut_n, 0), lb = chain_max_blocks(ca.P.lut_n, 1), mb = chain_max_blocks(ca.P.lut_n, 2);
         if (sb <= 0) sb = 1024;
@@ -733,21 +764,19 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
             ProfScope ps(c, "chain_lb");
             LCHK(launch_chain_stage(5, ca, 2048, c->stream));
         }
-        ca.lseg_prof = env_on("MM2G_LSEG_PROF") ? 1u : 0u;
+        ca.lseg_prof = K[MM2G_KNOB_LSEG_PROF] ? 1u : 0u;
         for (int stg = 0; stg < 5; ++stg) {
             ca.giant_min = giant_min[pass];
             ca.giant_exact = pass == 0 ? 1u : 0u;
             // production only; the pin bitmap and the lo field bound the window (max_iter <= 5120)
-            if (stg == 2 && ca.lazy && ca.giant_min != 0xffffffffu && ca.P.max_iter <= 5120 && !env_on("MM2G_NO_GIANT")) {
+            if (stg == 2 && ca.lazy && ca.giant_min != 0xffffffffu && ca.P.max_iter <= 5120 && K[MM2G_KNOB_GIANT]) {
                 ProfScope ps(c, pass ? "chain_giant_rescue" : "chain_giant");
-                if (const char* e = getenv("MM2G_GIANT_LCAP")) ca.giant_lcap = (uint32_t)std::max(16, atoi(e)) & ~15u;   // tests
+                if (K[MM2G_KNOB_GIANT_LCAP] > 0) ca.giant_lcap = (uint32_t)std::max<int64_t>(16, K[MM2G_KNOB_GIANT_LCAP]) & ~15u;
                 LCHK(launch_chain_stage(7, ca, 256, c->stream));
                 // longer segments from a per-workgroup HBM slice (100 kb reads' rescue)
-                uint32_t gmax = 65536;
-                if (const char* e = getenv("MM2G_GIANT_GMAX")) gmax = (uint32_t)std::max(0, atoi(e)) & ~15u;
+                const uint32_t gmax = (uint32_t)std::max<int64_t>(0, K[MM2G_KNOB_GIANT_GMAX]) & ~15u;
                 if (gmax) {
-                    int gblocks = 256;
-                    if (const char* e = getenv("MM2G_GIANT_GBLOCKS")) gblocks = std::max(1, atoi(e));
+                    const int gblocks = (int)std::max<int64_t>(1, K[MM2G_KNOB_GIANT_GBLOCKS]);
                     unsigned char* scr;
                     ENSURE(c->giant_scr, unsigned char, (size_t)gblocks * gmax * 42, scr);
                     ca.giant_scr = scr;
@@ -777,41 +806,211 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
             fprintf(stderr, "\n");
         }
     }
-    // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
-    const bool sep = (H.w != o->w || H.k != o->k);
-    c->dv_separate = sep;
-    if (sep) {
-        if (!(H.w > 0 && H.w < 256 && H.k > 0 && H.k <= 28)) return set_err(MM2G_E_ARG, "index w/k invalid for the dv sketch");
-        e = run_sketch(c, H.w, H.k, c->mz2_base, c->mz2_end, c->mz2_x, c->mz2_y, c->mz2_cnt, nullptr);
-        if (e) return e;
+    return 0;
+}
+
+// Queue the whole path for the resident batch on the context stream (no host
+// synchronisation): sketch -> filter -> lookup -> anchors -> sort -> chain ->
+// dv, then the per-read results and the status block to pinned host memory.
+// `stop_after_sort`: the seed stage entry point (mm2g_seed_batch).
+static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort) {
+    int32_t mdx0, mdx1;
+    if (int e = check_opts(c, o, mdx0, mdx1)) return e;
+    HIPCHK(hipSetDevice(c->device));
+    const HostIndex& H = *c->hidx;
+    const uint32_t n = c->n_reads;
+    const int64_t* K = c->knob;
+    c->mapped = false;
+    c->collected = false;
+    c->stop_after_sort = stop_after_sort;
+    c->last_opts = *o;
+    // key layout
+    KeyLayout kl;
+    kl.n_seq = H.n_seq;
+    kl.qb = std::max<uint32_t>(1, bit_width(c->max_read_len));
+    kl.rb = std::max<uint32_t>(1, bit_width(H.max_len));
+    kl.gb = std::max<uint32_t>(1, bit_width(2ull * H.n_seq));
+    if (kl.qb + kl.rb + kl.gb > 64) return set_err(MM2G_E_UNSUP, "anchor key needs %u bits (> 64)", kl.qb + kl.rb + kl.gb);
+    c->kl = kl;
+    ReadOut* out;
+    ENSURE(c->outb, ReadOut, n + 1, out);
+    unsigned long long* st;
+    ENSURE(c->dstat, unsigned long long, 8, st);
+    uint32_t* st32 = (uint32_t*)st;
+    HIPCHK(hipMemsetAsync(out, 0, sizeof(ReadOut) * (n + 1), c->stream));
+    HIPCHK(hipMemsetAsync(st, 0, 64, c->stream));
+    if (c->h_out_cap < (size_t)n + 1) {
+        HIPCHK(hipStreamSynchronize(c->stream));   // a previous batch's copy may still target it
+        if (c->h_out) (void)hipHostFree(c->h_out);
+        c->h_out = nullptr; c->h_out_cap = 0;
+        HIPCHK(hipHostMalloc((void**)&c->h_out, ((size_t)n + 1) * sizeof(ReadOut), hipHostMallocDefault));
+        c->h_out_cap = (size_t)n + 1;
     }
-    DvArgs da{n, a_off, keys, (const uint32_t*)ktmp, sep ? (const uint64_t*)c->mz2_base.p : mz_base,
-              sep ? (const uint32_t*)c->mz2_cnt.p : mz_cnt, sep ? (const uint32_t*)c->mz2_y.p : (const uint32_t*)c->mz_y.p, kl, o->k, out,
-              c->keys.cap / 8, (sep ? c->mz2_y.cap : c->mz_y.cap) / 4};
+    if (n == 0) {
+        HIPCHK(hipMemcpyAsync(c->h_stat, st, 64, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipEventRecord(c->ev_done, c->stream));
+        c->mapped = true;
+        return 0;
+    }
+    // 1. sketch (CLI w/k, rid 0: seeds.rs:7-11)
+    if (int e = run_sketch(c, o->w, o->k, c->sk1, (int32_t*)st32)) return e;
+    const uint64_t mcap = c->sk1.cap;
+    uint64_t* mz_base = (uint64_t*)c->sk1.base.p; uint32_t* mz_cnt = (uint32_t*)c->sk1.cnt.p;
+    // 2. query filter (seeds.rs:13-36; (10, 0.01) hard-wired at main.rs:195).  Only
+    //    reads whose count table outgrows LDS use the global table; its size is
+    //    estimated from the read lengths and checked on the device.
     {
+        uint64_t est = 0;
+        for (uint32_t r = 0; r < n; ++r) {
+            const uint64_t m = 2 * (c->h_rd_off[r + 1] - c->h_rd_off[r]) / (uint64_t)(o->w + 1) + 64;
+            uint64_t ts = 1;
+            while (ts < 2 * m) ts <<= 1;
+            if (m > 10 && (ts > 4096 || o->k > 16)) est += ts;
+        }
+        c->cap_tab = std::max(c->cap_tab, est);
+        if (c->knob[MM2G_KNOB_WS_MIN] > 0 && !c->redo) c->cap_tab = (uint64_t)c->knob[MM2G_KNOB_WS_MIN];   // tests: force the re-map
+    }
+    uint64_t* tab_off; uint8_t* keep;
+    ENSURE(c->tab_off, uint64_t, n + 1, tab_off);
+    ENSURE(c->keep, uint8_t, mcap, keep);
+    {
+        ProfScope ps(c, "scan");
+        LCHK(launch_excl_scan(mz_cnt, n, tab_off, 1, 10, o->k, std::max<uint64_t>(c->cap_tab, 1), st32, BS_TAB, 1, c->stream));
+    }
+    uint64_t* tkey; uint32_t* tcnt;
+    ENSURE(c->tab_key, uint64_t, c->cap_tab, tkey);
+    ENSURE(c->tab_cnt, uint32_t, c->cap_tab, tcnt);
+    {
+        FilterArgs fa{n, mz_base, mz_cnt, (const uint64_t*)c->sk1.x.p, tab_off, tkey, tcnt, keep, 10, 0.01f, c->cap_tab};
+        ProfScope ps(c, "filter");
+        LCHK(launch_filter(fa, o->k, grid_for(n), c->stream));
+    }
+    // 3. lookup + anchor count (index.rs:143-154, seeds.rs:42-57); the anchor
+    //    workspace keeps its capacity across batches, checked on the device
+    uint32_t *mz_n, *mz_poff, *a_cnt; uint64_t* a_off;
+    ENSURE(c->mz_n, uint32_t, mcap, mz_n); ENSURE(c->mz_poff, uint32_t, mcap, mz_poff);
+    ENSURE(c->a_cnt, uint32_t, n + 1, a_cnt); ENSURE(c->a_off, uint64_t, n + 1, a_off);
+    uint32_t* a_part;
+    ENSURE(c->a_part, uint32_t, (size_t)n * (SEED_PARTS - 1), a_part);
+    SeedArgs sa{n, c->d_rd_off, mz_base, mz_cnt, (const uint64_t*)c->sk1.x.p, (const uint32_t*)c->sk1.y.p, keep,
+                (const IxEntry*)c->dix->tab.p, c->log2cap, c->mid_occ, (const uint64_t*)c->dix->ix_pos.p, mz_n, mz_poff, a_cnt, a_off, nullptr, kl, o->k,
+                0, c->dix->ix_pos.cap / 8, mcap, out, a_part};
+    sa.abort = st32;
+    {
+        ProfScope ps(c, "seed_count");
+        LCHK(launch_seed_count(sa, grid_for(n), c->stream));
+    }
+    c->cap_A = std::max<uint64_t>(c->cap_A, 3 * c->total_bases + 65536);
+    if (c->knob[MM2G_KNOB_WS_MIN] > 0 && !c->redo) c->cap_A = (uint64_t)c->knob[MM2G_KNOB_WS_MIN];   // tests: force the re-map
+    const uint64_t A_cap = c->cap_A;
+    {
+        ProfScope ps(c, "scan");
+        LCHK(launch_excl_scan(a_cnt, n, a_off, 0, 0, o->k, A_cap, st32, BS_ANCHORS, 2, c->stream));
+    }
+    uint64_t *keys, *ktmp;
+    ENSURE(c->keys, uint64_t, A_cap, keys); ENSURE(c->keys_tmp, uint64_t, A_cap, ktmp);
+    sa.keys = keys; sa.cap_keys = c->keys.cap / 8;
+    {
+        ProfScope ps(c, "seed_write");
+        LCHK(launch_seed_write(sa, grid_for(n), c->stream));
+    }
+    // 4. anchor sort (seeds.rs:58).  The singleton filter needs every max_dist_x
+    //    of both DP passes within one 2^CELL_SHIFT cell (DESIGN.md "Anchor sort");
+    //    it is off in debug mode (full anchor/DP arrays for the parity tests).
+    uint32_t* cnt2; uint64_t* smax;
+    ENSURE(c->cnt2, uint32_t, n, cnt2);
+    ENSURE(c->smax, uint64_t, n, smax);
+    const bool filt = !c->debug && !stop_after_sort && K[MM2G_KNOB_FILTER] && std::max(mdx0, mdx1) <= (1 << CELL_SHIFT);
+    SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
+                filt ? c->dix->cells : 0u, cnt2, smax, (uint32_t)std::min<int64_t>(K[MM2G_KNOB_SORT_SMALL], 4096), nullptr, 0u,
+                (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_SEG_SMALL], SEG_THREAD)), nullptr};
+    so.abort = st32;
+    uint64_t* sprof = nullptr;
+    if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 64)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 64, c->stream)); so.prof = sprof; }
+    {
+        ProfScope ps(c, "sort_small");
+        LCHK(launch_sort_read(0, so, c->stream));
+    }
+    {
+        ProfScope ps(c, "sort_large");
+        LCHK(launch_sort_read(1, so, c->stream));
+    }
+    if (sprof) dump_sort_prof(c, sprof, n);
+    // the sorted anchors are in the tmp buffer: swap the roles for everything downstream
+    std::swap(c->keys.p, c->keys_tmp.p); std::swap(c->keys.cap, c->keys_tmp.cap);
+    std::swap(keys, ktmp);
+    if (!stop_after_sort) {
+        // 5. chain DP + fallback + rescue
+        ChainKParams P{};
+        P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
+        P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
+        if (int e = run_chain(c, n, c->d_rd_off, P, 0.01f * 0.8f * (float)o->k, 2, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
+                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug))
+            return e;
+        // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
+        const bool sep = (H.w != o->w || H.k != o->k);
+        c->dv_separate = sep;
+        if (sep) {
+            if (!(H.w > 0 && H.w < 256 && H.k > 0 && H.k <= 28)) return set_err(MM2G_E_ARG, "index w/k invalid for the dv sketch");
+            if (int e = run_sketch(c, H.w, H.k, c->sk2, (int32_t*)(st32 + 1))) return e;
+        }
+        SketchBufs& D = sep ? c->sk2 : c->sk1;
+        DvArgs da{n, a_off, keys, (const uint32_t*)ktmp, (const uint64_t*)D.base.p, (const uint32_t*)D.cnt.p, (const uint32_t*)D.y.p, kl, o->k,
+                  out, c->keys.cap / 8, D.y.cap / 4};
+        da.abort = st32;
         ProfScope ps(c, "dv");
         LCHK(launch_dv(da, c->stream));
     }
+    LCHK(launch_batch_sums(n, mz_cnt, cnt2, st, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_out, out, (size_t)n * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_stat, st, 64, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipEventRecord(c->ev_done, c->stream));
     c->mapped = true;
     return 0;
 }
 
+// Wait for the queued batch; when a workspace was too small, grow it and map
+// the batch again (reads are still resident), at most a few times.
+static int wait_batch(mm2g_ctx* c) {
+    if (!c->mapped) return set_err(MM2G_E_STATE, "batch not mapped");
+    if (c->collected) return 0;
+    for (int it = 0;; ++it) {
+        HIPCHK(hipEventSynchronize(c->ev_done));
+        const uint32_t* s32 = (const uint32_t*)c->h_stat;
+        const uint32_t bits = s32[0], dv_ovf = s32[1];
+        if (!bits && !dv_ovf) break;
+        if (it >= 4) return set_err(MM2G_E_STATE, "batch workspaces did not converge (status %u)", bits);
+        if (bits & BS_SKETCH) { if (int e = sketch_exact_layout(c, c->sk1)) return e; }
+        if (dv_ovf) { if (int e = sketch_exact_layout(c, c->sk2)) return e; }
+        if (bits & BS_TAB) c->cap_tab = std::max(c->cap_tab, c->h_stat[1] + c->h_stat[1] / 4 + 1024);
+        if (bits & BS_ANCHORS) c->cap_A = std::max(c->cap_A, c->h_stat[2] + c->h_stat[2] / 4 + 65536);
+        const mm2g_map_opts o = c->last_opts;
+        c->redo = true;
+        const int e = map_enqueue(c, &o, c->stop_after_sort);
+        c->redo = false;
+        if (e) return e;
+    }
+    c->n_anchors = c->h_stat[2];
+    c->prof_collect();
+    c->collected = true;
+    return 0;
+}
+
+int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
+    if (!c || !o) return set_err(MM2G_E_ARG, "null argument");
+    if (!c->have_index) return set_err(MM2G_E_STATE, "no index uploaded");
+    return map_enqueue(c, o, false);
+}
+
 int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     if (!c) return set_err(MM2G_E_ARG, "null context");
-    if (!c->mapped) return set_err(MM2G_E_STATE, "batch not mapped");
+    if (!c->mapped || c->stop_after_sort) return set_err(MM2G_E_STATE, "batch not mapped");
     if (n > c->n_reads) return set_err(MM2G_E_ARG, "n exceeds the batch size");
     HIPCHK(hipSetDevice(c->device));
-    if (c->h_out_cap < c->n_reads + 1) {
-        if (c->h_out) (void)hipHostFree(c->h_out);
-        c->h_out_cap = c->n_reads + 1;
-        HIPCHK(hipHostMalloc((void**)&c->h_out, c->h_out_cap * sizeof(ReadOut), hipHostMallocDefault));
-    }
-    if (c->n_reads) HIPCHK(hipMemcpyAsync(c->h_out, c->outb.p, c->n_reads * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    c->prof_collect();
+    if (int e = wait_batch(c)) return e;
     const HostIndex& H = *c->hidx;
     const int kdv = c->dv_separate ? H.k : c->last_opts.k;
-    uint64_t cnt[6] = {c->total_bases, 0, 0, c->n_anchors, 0, 0};
+    uint64_t cnt[6] = {c->total_bases, c->h_stat[3], 0, c->n_anchors, 0, 0};
     for (uint32_t i = 0; i < c->n_reads; ++i) {
         const ReadOut& o = c->h_out[i];
         cnt[4] += (o.flags & RF_RESCUED) ? (uint64_t)o.n_anchors : 0;
@@ -849,20 +1048,8 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
             r.dv = frac >= 1.0f ? 0.0f : 1.0f - powf(frac, 1.0f / fmaxf(avg_k, 1.0f));
         }
     }
-    // minimizer counters
-    {
-        std::vector<uint32_t> mc(c->n_reads);
-        HIPCHK(hipMemcpy(mc.data(), c->mz_cnt.p, c->n_reads * 4, hipMemcpyDeviceToHost));
-        for (auto v : mc) cnt[1] += v;
-    }
     for (int t = 0; t < 6; ++t) c->counters[t] = cnt[t];
-    {   // anchors left after the sort's singleton filter (the DP input)
-        std::vector<uint32_t> k2(c->n_reads);
-        if (c->n_reads) HIPCHK(hipMemcpy(k2.data(), c->cnt2.p, c->n_reads * 4, hipMemcpyDeviceToHost));
-        uint64_t kept = 0;
-        for (auto v : k2) kept += v;
-        c->counters[6] = kept;
-    }
+    c->counters[6] = c->h_stat[4];    // anchors left after the sort's singleton filter (the DP input)
     return 0;
 }
 
@@ -916,13 +1103,29 @@ int mm2g_batch_sketch(mm2g_ctx* c, int w, int k, uint32_t rid, uint64_t* out_off
     HIPCHK(hipSetDevice(c->device));
     const uint32_t n = c->n_reads;
     for (uint32_t i = 0; i < n; ++i)
-        if (c->h_rd_off[i + 1] == c->h_rd_off[i]) return set_err(MM2G_E_ARG, "empty sequence (src/sketch.rs:40)");
-    int e = run_sketch(c, w, k, c->mz2_base, c->mz2_end, c->mz2_x, c->mz2_y, c->mz2_cnt, nullptr);
-    if (e) return e;
+        if (c->h_rd_off[i + 1] == c->h_rd_off[i]) return set_err(MM2G_E_ARG, "empty sequence (src/sketch.rs:30-32)");
+    c->mapped = false;                      // the sketch reuses the dv sketch's slots
+    SketchBufs& B = c->sk2;
+    B.exact = false;
+    int32_t* ovf;
+    unsigned long long* st;
+    ENSURE(c->dstat, unsigned long long, 8, st);
+    ovf = (int32_t*)st + 1;
+    for (int it = 0;; ++it) {
+        HIPCHK(hipMemsetAsync(st, 0, 64, c->stream));
+        if (int e = run_sketch(c, w, k, B, ovf)) return e;
+        int32_t o = 0;
+        HIPCHK(hipMemcpyAsync(&o, ovf, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (!o) break;
+        if (it) return set_err(MM2G_E_STATE, "sketch slots did not converge");
+        if (int e = sketch_exact_layout(c, B)) return e;
+    }
     std::vector<uint32_t> hc(n); std::vector<uint64_t> hb(n);
     if (n) {
-        HIPCHK(hipMemcpy(hc.data(), c->mz2_cnt.p, n * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(hb.data(), c->mz2_base.p, n * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(hc.data(), B.cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(hb.data(), B.base.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
     }
     uint64_t run = 0;
     for (uint32_t i = 0; i < n; ++i) { if (out_off) out_off[i] = run; run += hc[i]; }
@@ -933,8 +1136,8 @@ int mm2g_batch_sketch(mm2g_ctx* c, int w, int k, uint32_t rid, uint64_t* out_off
     for (uint32_t i = 0; i < n; ++i) {
         x.resize(hc[i]); y.resize(hc[i]);
         if (hc[i]) {
-            HIPCHK(hipMemcpy(x.data(), (uint64_t*)c->mz2_x.p + hb[i], hc[i] * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(y.data(), (uint32_t*)c->mz2_y.p + hb[i], hc[i] * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(x.data(), (uint64_t*)B.x.p + hb[i], hc[i] * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(y.data(), (uint32_t*)B.y.p + hb[i], hc[i] * 4, hipMemcpyDeviceToHost));
         }
         const uint64_t o0 = out_off ? out_off[i] : 0;
         for (uint32_t t = 0; t < hc[i]; ++t) {
@@ -945,27 +1148,10 @@ int mm2g_batch_sketch(mm2g_ctx* c, int w, int k, uint32_t rid, uint64_t* out_off
     return 0;
 }
 
-int mm2g_ctx_set_debug(mm2g_ctx* c, int on) { if (!c) return set_err(MM2G_E_ARG, "null context"); c->debug = on != 0; return 0; }
-
-// Unpack the sorted keys of read r back into the reference's (x, y).
-int64_t mm2g_debug_anchors(mm2g_ctx* c, uint32_t r, uint64_t* xy, int64_t cap) {
-    if (!c || !c->mapped || r >= c->n_reads) return set_err(MM2G_E_STATE, "no mapped batch / bad read index");
-    HIPCHK(hipSetDevice(c->device));
-    uint64_t off[2];
-    HIPCHK(hipMemcpy(off, (uint64_t*)c->a_off.p + r, 16, hipMemcpyDeviceToHost));
-    int64_t A = (int64_t)(off[1] - off[0]);
-    if (!c->debug) {   // production sort: only the anchors kept by the singleton filter are sorted
-        uint32_t kept = 0;
-        HIPCHK(hipMemcpy(&kept, (uint32_t*)c->cnt2.p + r, 4, hipMemcpyDeviceToHost));
-        A = kept;
-    }
-    if (!xy) return A;
-    std::vector<uint64_t> k((size_t)A);
-    if (A) HIPCHK(hipMemcpy(k.data(), (uint64_t*)c->keys.p + off[0], A * 8, hipMemcpyDeviceToHost));
-    const KeyLayout& kl = c->kl;
+// Sorted device keys of one read -> the reference's Anchor (x, y) (seeds.rs:62-79).
+static void unpack_keys(const KeyLayout& kl, uint64_t span, const uint64_t* k, int64_t A, uint64_t* xy) {
     const uint64_t qm = (1ULL << kl.qb) - 1, rm = (1ULL << kl.rb) - 1;
-    const uint64_t span = (uint64_t)c->last_opts.k;
-    for (int64_t i = 0; i < A && i < cap; ++i) {
+    for (int64_t i = 0; i < A; ++i) {
         const uint64_t g = k[i] >> (kl.rb + kl.qb), p = (k[i] >> kl.qb) & rm, q = k[i] & qm;
         uint64_t x;
         if (g == 2ull * kl.n_seq) x = 0xffffffff80000000ULL | p;
@@ -973,11 +1159,193 @@ int64_t mm2g_debug_anchors(mm2g_ctx* c, uint32_t r, uint64_t* xy, int64_t cap) {
         else x = (g << 32) | p;
         xy[2 * i] = x; xy[2 * i + 1] = (span << 32) | q;
     }
+}
+
+int64_t mm2g_seed_batch(mm2g_ctx* c, const mm2g_map_opts* o, uint64_t* a_off, uint64_t* xy, uint64_t cap) {
+    if (!c || !o || !a_off) return set_err(MM2G_E_ARG, "null argument");
+    if (!c->have_index) return set_err(MM2G_E_STATE, "no index uploaded");
+    HIPCHK(hipSetDevice(c->device));
+    const bool same = c->mapped && c->stop_after_sort && !memcmp(&c->last_opts, o, sizeof *o);
+    if (!same)
+        if (int e = map_enqueue(c, o, true)) return e;
+    if (int e = wait_batch(c)) return e;
+    const uint32_t n = c->n_reads;
+    HIPCHK(hipMemcpyAsync(a_off, c->a_off.p, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint64_t A = n ? a_off[n] : 0;
+    if (!n) a_off[0] = 0;
+    if (!xy) return (int64_t)A;
+    if (A > cap) return set_err(MM2G_E_ARG, "output capacity too small (%llu anchors)", (unsigned long long)A);
+    std::vector<uint64_t> k(A);
+    if (A) HIPCHK(hipMemcpy(k.data(), c->keys.p, A * 8, hipMemcpyDeviceToHost));
+    unpack_keys(c->kl, (uint64_t)o->k, k.data(), (int64_t)A, xy);
+    return (int64_t)A;
+}
+
+void mm2g_chain_params_default(mm2g_chain_params* p, int k) {
+    // default_chain_params (src/main.rs:105-123)
+    p->max_dist_x = 5000; p->max_dist_y = 5000; p->bw = 500; p->max_chain_iter = 5000; p->min_chain_score = 40; p->min_cnt = 3;
+    p->chn_pen_gap = 0.01f * 0.8f * (float)k; p->chn_pen_skip = 0.0f; p->max_chain_skip = 25; p->max_drop = 500;
+    p->bw_long = 20000; p->rmq_rescue_size = 1000; p->rmq_rescue_ratio = 0.1f;
+}
+
+int mm2g_chain_batch(mm2g_ctx* c, const mm2g_chain_params* p, uint32_t n, const uint64_t* a_off, const uint64_t* xy, const int32_t* qlen,
+                     int rescue, mm2g_chain_result* res, int32_t* f, int32_t* pprev, uint32_t* chain) {
+    if (!c || !p || !a_off || (n && !qlen) || !res) return set_err(MM2G_E_ARG, "null argument");
+    const uint64_t A = a_off[n] - a_off[0];
+    if (A && !xy) return set_err(MM2G_E_ARG, "null anchors");
+    if (p->chn_pen_skip != 0.0f) return set_err(MM2G_E_UNSUP, "chn_pen_skip != 0 (the reference fixes it at 0, main.rs:116)");
+    if (p->min_cnt < 2) return set_err(MM2G_E_UNSUP, "min_cnt < 2 is outside the supported parity envelope (DESIGN.md Q4)");
+    if (p->bw < 0 || p->bw_long < 0 || p->max_chain_iter < 1 || p->max_chain_skip < 0) return set_err(MM2G_E_ARG, "invalid chain parameters");
+    if (std::max(p->bw, p->bw_long) + 1 > 60000) return set_err(MM2G_E_UNSUP, "bandwidth > 59999 not supported");
+    HIPCHK(hipSetDevice(c->device));
+    // key layout from the anchors themselves: groups by (rev, rid), the Q19
+    // pseudo-group (x>>32 == 0xffffffff) last; order-preserving, so the caller's
+    // (x, y) order must be the key order (checked)
+    uint64_t max_rid = 0, max_p = 0, max_q = 0;
+    int64_t span = -1;
+    for (uint64_t i = 0; i < A; ++i) {
+        const uint64_t x = xy[2 * i], y = xy[2 * i + 1];
+        const uint32_t hi = (uint32_t)(x >> 32);
+        if (hi != 0xffffffffu) {
+            if (x & 0x80000000ULL) return set_err(MM2G_E_UNSUP, "anchor %llu: rpos >= 2^31 outside the Q19 group", (unsigned long long)i);
+            max_rid = std::max<uint64_t>(max_rid, hi & 0x7fffffffu);
+        }
+        max_p = std::max<uint64_t>(max_p, x & 0x7fffffffULL);
+        max_q = std::max<uint64_t>(max_q, y & 0xffffffffULL);
+        const int64_t sp = (int64_t)((y >> 32) & 0xff);
+        if ((y >> 40) != 0) return set_err(MM2G_E_UNSUP, "anchor %llu: y above the span byte", (unsigned long long)i);
+        if (span < 0) span = sp;
+        else if (sp != span) return set_err(MM2G_E_UNSUP, "anchors of different spans (the device DP keeps one span)");
+    }
+    if (span < 0) span = 15;
+    KeyLayout kl;
+    kl.n_seq = (uint32_t)max_rid + 1;
+    kl.qb = std::max<uint32_t>(1, bit_width(max_q));
+    kl.rb = std::max<uint32_t>(1, bit_width(max_p));
+    kl.gb = std::max<uint32_t>(1, bit_width(2ull * kl.n_seq));
+    if (kl.qb + kl.rb + kl.gb > 64) return set_err(MM2G_E_UNSUP, "anchor key needs %u bits (> 64)", kl.qb + kl.rb + kl.gb);
+    std::vector<uint64_t> keys(A), ho(n + 1), hro(n + 1, 0);
+    std::vector<uint32_t> hcnt(n);
+    for (uint32_t r = 0; r < n; ++r) {
+        if (a_off[r + 1] < a_off[r]) return set_err(MM2G_E_ARG, "a_off must be non-decreasing");
+        if (qlen[r] < 0) return set_err(MM2G_E_ARG, "negative qlen");
+        ho[r] = a_off[r] - a_off[0]; hcnt[r] = (uint32_t)(a_off[r + 1] - a_off[r]);
+        hro[r + 1] = hro[r] + (uint64_t)qlen[r];
+        for (uint64_t i = a_off[r]; i < a_off[r + 1]; ++i) {
+            const uint64_t x = xy[2 * (i - a_off[0])], y = xy[2 * (i - a_off[0]) + 1];
+            const uint32_t hi = (uint32_t)(x >> 32);
+            const uint64_t rid = hi & 0x7fffffffu;
+            const uint64_t g = hi == 0xffffffffu ? 2ull * kl.n_seq : (x >> 63) ? kl.n_seq + rid : rid;
+            const uint64_t key = (g << (kl.rb + kl.qb)) | ((x & 0x7fffffffULL) << kl.qb) | (y & 0xffffffffULL);
+            if (i > a_off[r] && key < keys[i - 1 - a_off[0]])
+                return set_err(MM2G_E_UNSUP, "read %u: anchors are not sorted by (x, y) (build_anchors_filtered order, seeds.rs:58)", r);
+            keys[i - a_off[0]] = key;
+        }
+    }
+    ho[n] = A;
+    c->mapped = false;      // the batch workspaces are reused
+    c->kl = kl;
+    const uint64_t A_cap = std::max<uint64_t>(A, 1);
+    uint64_t *dk, *dt, *doff, *dro, *smax; uint32_t *dcnt, *cnt2; ReadOut* out;
+    ENSURE(c->keys, uint64_t, A_cap, dk); ENSURE(c->keys_tmp, uint64_t, A_cap, dt);
+    ENSURE(c->a_off, uint64_t, n + 1, doff); ENSURE(c->a_cnt, uint32_t, n + 1, dcnt);
+    ENSURE(c->cnt2, uint32_t, n + 1, cnt2); ENSURE(c->smax, uint64_t, n + 1, smax);
+    ENSURE(c->chain_rdoff, uint64_t, n + 1, dro);
+    ENSURE(c->outb, ReadOut, n + 1, out);
+    HIPCHK(hipMemcpyAsync(dk, keys.data(), A * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(doff, ho.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(dro, hro.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if (n) {
+        HIPCHK(hipMemcpyAsync(dcnt, hcnt.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(cnt2, hcnt.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));   // every anchor enters the DP
+    }
+    HIPCHK(hipMemsetAsync(smax, 0, ((size_t)n + 1) * 8, c->stream));
+    HIPCHK(hipMemsetAsync(out, 0, sizeof(ReadOut) * ((size_t)n + 1), c->stream));
+    ChainKParams P{};
+    P.max_dist_x = std::max(p->max_dist_x, p->bw); P.max_dist_y = std::max(p->max_dist_y, p->bw);   // lchain.rs:63-66
+    P.bw = p->bw; P.max_iter = p->max_chain_iter; P.max_skip = p->max_chain_skip;
+    P.span = (int32_t)span; P.rescue_size = p->rmq_rescue_size; P.rescue_ratio_f = 1.0f - p->rmq_rescue_ratio; P.pass = 0; P.lut_n = p->bw + 1;
+    const int32_t mdx1 = std::max(p->max_dist_x, p->bw_long), mdy1 = std::max(p->max_dist_y, p->bw_long);
+    if (int e = run_chain(c, n, dro, P, p->chn_pen_gap, rescue ? 2 : 1, mdx1, mdy1, p->bw_long, A_cap, doff, dcnt, dk, dt, cnt2, smax, out,
+                          nullptr, c->debug || f || pprev))
+        return e;
+    std::vector<ReadOut> ho2(n);
+    if (n) HIPCHK(hipMemcpyAsync(ho2.data(), out, (size_t)n * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
+    if (f && A) HIPCHK(hipMemcpyAsync(f, c->fbuf.p, A * 4, hipMemcpyDeviceToHost, c->stream));
+    if (pprev && A) HIPCHK(hipMemcpyAsync(pprev, c->ppbuf.p, A * 4, hipMemcpyDeviceToHost, c->stream));
+    std::vector<uint32_t> cb;
+    if (chain && A) { cb.resize(A); HIPCHK(hipMemcpyAsync(cb.data(), dt, A * 4, hipMemcpyDeviceToHost, c->stream)); }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->prof_collect();
+    for (uint32_t r = 0; r < n; ++r) {
+        const ReadOut& o = ho2[r];
+        mm2g_chain_result& R = res[r];
+        memset(&R, 0, sizeof R);
+        R.n_anchors = (int32_t)hcnt[r];
+        if (!(o.flags & RF_MAPPED)) continue;
+        R.flags = MM2G_R_MAPPED | ((rescue && (o.flags & RF_RESCUED)) ? MM2G_R_RESCUED : 0) | ((o.flags & RF_PANIC) ? MM2G_R_PANIC : 0);
+        R.score = o.score; R.cm = o.cm; R.qs = o.qs; R.qe = o.qe; R.ts = o.ts; R.te = o.te;
+        const uint32_t g = (uint32_t)o.group;
+        if (g == 2u * kl.n_seq) { R.rid = 0x7fffffff; R.rev = 1; }
+        else if (g >= kl.n_seq) { R.rid = (int32_t)(g - kl.n_seq); R.rev = 1; }
+        else { R.rid = (int32_t)g; R.rev = 0; }
+        // chain_dp_all's chains[0]: the pprev walk from best_i, reversed to ascending (lchain.rs:162-173)
+        if (chain)
+            for (int32_t t = 0; t < o.cm; ++t) chain[ho[r] + t] = cb[ho[r] + (uint64_t)(o.cm - 1 - t)];
+    }
+    return 0;
+}
+
+int mm2g_ctx_set_debug(mm2g_ctx* c, int on) { if (!c) return set_err(MM2G_E_ARG, "null context"); c->debug = on != 0; return 0; }
+
+int mm2g_ctx_set_knob(mm2g_ctx* c, int knob, int64_t value) {
+    if (!c) return set_err(MM2G_E_ARG, "null context");
+    if (knob <= 0 || knob >= MM2G_KNOB_COUNT) return set_err(MM2G_E_ARG, "unknown knob %d", knob);
+    c->knob[knob] = value;
+    return 0;
+}
+int64_t mm2g_ctx_get_knob(const mm2g_ctx* c, int knob) {
+    if (!c) return set_err(MM2G_E_ARG, "null context");
+    if (knob <= 0 || knob >= MM2G_KNOB_COUNT) return set_err(MM2G_E_ARG, "unknown knob %d", knob);
+    return c->knob[knob];
+}
+int mm2g_set_index_knob(int knob, int64_t value) {
+    if (knob <= 0 || knob >= MM2G_IKNOB_COUNT) return set_err(MM2G_E_ARG, "unknown index knob %d", knob);
+    g_index_knob[knob].store(value);
+    return 0;
+}
+
+// The debug accessors read what the last mm2g_batch_map left on the device:
+// they wait for it first (the context stream is non-blocking).
+static int debug_ready(mm2g_ctx* c, uint32_t r) {
+    if (!c || !c->mapped || r >= c->n_reads) return set_err(MM2G_E_STATE, "no mapped batch / bad read index");
+    HIPCHK(hipSetDevice(c->device));
+    if (int e = wait_batch(c)) return e;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Unpack the sorted keys of read r back into the reference's (x, y).
+int64_t mm2g_debug_anchors(mm2g_ctx* c, uint32_t r, uint64_t* xy, int64_t cap) {
+    if (int e = debug_ready(c, r)) return e;
+    uint64_t off[2];
+    HIPCHK(hipMemcpy(off, (uint64_t*)c->a_off.p + r, 16, hipMemcpyDeviceToHost));
+    int64_t A = (int64_t)(off[1] - off[0]);
+    if (!c->debug && !c->stop_after_sort) {   // production sort: only the anchors kept by the singleton filter are sorted
+        uint32_t kept = 0;
+        HIPCHK(hipMemcpy(&kept, (uint32_t*)c->cnt2.p + r, 4, hipMemcpyDeviceToHost));
+        A = kept;
+    }
+    if (!xy) return A;
+    std::vector<uint64_t> k((size_t)A);
+    if (A) HIPCHK(hipMemcpy(k.data(), (uint64_t*)c->keys.p + off[0], A * 8, hipMemcpyDeviceToHost));
+    const int64_t m = std::min<int64_t>(A, cap);
+    unpack_keys(c->kl, (uint64_t)c->last_opts.k, k.data(), m, xy);
     return A;
 }
 int64_t mm2g_debug_dp(mm2g_ctx* c, uint32_t r, int32_t* f, int32_t* pprev, int64_t cap) {
-    if (!c || !c->mapped || r >= c->n_reads) return set_err(MM2G_E_STATE, "no mapped batch / bad read index");
-    HIPCHK(hipSetDevice(c->device));
+    if (int e = debug_ready(c, r)) return e;
     uint64_t off[2];
     HIPCHK(hipMemcpy(off, (uint64_t*)c->a_off.p + r, 16, hipMemcpyDeviceToHost));
     const int64_t A = (int64_t)(off[1] - off[0]);
@@ -987,11 +1355,10 @@ int64_t mm2g_debug_dp(mm2g_ctx* c, uint32_t r, int32_t* f, int32_t* pprev, int64
     return A;
 }
 int64_t mm2g_debug_keep(mm2g_ctx* c, uint32_t r, uint8_t* keep, int64_t cap) {
-    if (!c || !c->mapped || r >= c->n_reads) return set_err(MM2G_E_STATE, "no mapped batch / bad read index");
-    HIPCHK(hipSetDevice(c->device));
+    if (int e = debug_ready(c, r)) return e;
     uint64_t b; uint32_t m;
-    HIPCHK(hipMemcpy(&b, (uint64_t*)c->mz_base.p + r, 8, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&m, (uint32_t*)c->mz_cnt.p + r, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&b, (uint64_t*)c->sk1.base.p + r, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&m, (uint32_t*)c->sk1.cnt.p + r, 4, hipMemcpyDeviceToHost));
     if (keep && m) HIPCHK(hipMemcpy(keep, (uint8_t*)c->keep.p + b, std::min<int64_t>(m, cap), hipMemcpyDeviceToHost));
     return m;
 }

@@ -336,8 +336,11 @@ int32_t HostIndex::calc_mid_occ(float frac) const {
     return (int32_t)c[i] + 1;
 }
 
+// Process-wide switches of the index build / .mmi load (mm2g_set_index_knob).
+std::atomic<int64_t> g_index_knob[8] = {};
+
 static int load_threads() {
-    if (const char* e = getenv("MM2G_LOAD_THREADS")) return std::max(1, atoi(e));
+    if (const int64_t t = g_index_knob[3].load()) return (int)std::max<int64_t>(1, t);   // MM2G_IKNOB_LOAD_THREADS
     return (int)std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
 }
 

@@ -1,5 +1,6 @@
 // Host-side index (src/index.rs) and FASTA input for the MI355X path.
 #pragma once
+#include <atomic>
 #include <stdint.h>
 #include <string>
 #include <vector>
@@ -66,6 +67,8 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
                      const std::vector<std::string>* names, int w, int k, int b, int flag, HostIndex& idx, std::string& err,
                      bool& unsupported);
 bool load_mmi(const char* path, HostIndex& idx, std::string& err);
+// mm2g_set_index_knob values (index = MM2G_IKNOB_*; 0 = default)
+extern std::atomic<int64_t> g_index_knob[8];
 bool save_mmi(const HostIndex& idx, const char* path, std::string& err);
 
 }  // namespace mm2g

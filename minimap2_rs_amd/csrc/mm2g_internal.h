@@ -72,6 +72,10 @@ __host__ __device__ inline uint32_t ix_slot(uint64_t h, uint32_t log2cap) {
 
 
 // ---- kernel arguments (mm2g_kernels.hip) --------------------------------
+// Batch status word (u32 at the start of the context's status block, copied
+// back with the results): a workspace that was too small for this batch.  The
+// host grows it and maps the batch again (mm2g_batch_results).
+enum : uint32_t { BS_SKETCH = 1, BS_TAB = 2, BS_ANCHORS = 4, BS_SKETCH_DV = 8 };
 struct SketchArgs {
     const uint8_t* seq;
     const uint64_t* rd_off;     // n+1 offsets into seq
@@ -93,6 +97,13 @@ struct SketchArgs {
     const uint32_t* view_pre = nullptr;
     const uint32_t* emit_from = nullptr;
     const uint8_t* view_last = nullptr;
+    // Query reads in the device nt4 format (include/mm2g.h, "nt4 read batch"):
+    // read r's 2-bit codes start at pk_words[pk_off[r]], its ambiguity bitmap
+    // (if any) at pk_words[amb_off[r]] (U64MAX = none).  Null: ASCII `seq`.
+    const uint64_t* pk_words = nullptr;
+    const uint64_t* pk_off = nullptr;
+    const uint64_t* amb_off = nullptr;
+    uint32_t* mz_need = nullptr;   // per sequence: the unclamped minimizer count (mz_cnt is clamped to the slot)
 };
 struct FilterArgs {
     uint32_t n;
@@ -101,6 +112,7 @@ struct FilterArgs {
     uint64_t* tab_key; uint32_t* tab_cnt;
     uint8_t* keep;
     int q_occ_max; float q_occ_frac;
+    uint64_t cap_tab;          // entries of tab_key/tab_cnt: a read whose table would end beyond it is skipped (batch flagged)
 };
 struct SeedArgs {
     uint32_t n;
@@ -116,6 +128,7 @@ struct SeedArgs {
     uint64_t cap_keys, cap_pos, cap_mz;   // bounds for the MM2G_CHECKED build
     ReadOut* out;                         // m_kept
     uint32_t* a_part;                     // per read, SEED_PARTS-1 entries: anchors before part k (k = 1..)
+    const uint32_t* abort = nullptr;      // batch status word (BS_*): kernels after the anchor scan exit on BS_ANCHORS
 };
 // seed_write splits each read's minimizers into this many contiguous parts
 // (whole 64-minimizer chunks), one wave each; seed_count records where they start
@@ -139,6 +152,7 @@ struct SortArgs {
     uint32_t lds_words;     // dynamic LDS of k_sort_read (set by launch_sort_read)
     uint32_t seg_small;     // cell segments up to this length (<= 1024) are ranked one thread per anchor
     uint32_t* meta;         // per anchor scratch (the DP's f buffer): kept-cell rank of each scattered key
+    const uint32_t* abort = nullptr;
 };
 struct ChainArgs {
     uint32_t n;
@@ -177,6 +191,7 @@ struct ChainArgs {
     uint32_t giant_gmax;     // global variant: anchors per workgroup scratch slice (0 = off)
     void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
+    const uint32_t* abort = nullptr;
 };
 struct DvArgs {
     uint32_t n;
@@ -185,6 +200,7 @@ struct DvArgs {
     KeyLayout kl; int span;
     ReadOut* out;
     uint64_t cap_keys, cap_mz;
+    const uint32_t* abort = nullptr;
 };
 
 }  // namespace mm2g
@@ -204,8 +220,16 @@ int launch_chain_stage(int stage, const mm2g::ChainArgs& a, int blocks, hipStrea
 int chain_max_blocks(int lut_n, int which);   // co-resident workgroups (0 = k_chain_seg, 1 = k_chain_long, 2 = k_chain_med)
 int launch_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order, hipStream_t st);
 int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
-int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st);
-int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, hipStream_t st);
+// out[i] = exclusive prefix of f(in[t]); mode 0 identity, mode 1 the global filter
+// table size of a read with in[t] minimizers (0 when it fits k_filter_lds).  When
+// cap > 0 and the total exceeds it, `bit` is OR-ed into status[0]; status[slot]
+// receives the total.
+int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k, uint64_t cap, uint32_t* status,
+                     uint32_t bit, int slot, hipStream_t st);
+// per-batch sums for the counters: status64[3] = sum mz_cnt, status64[4] = sum cnt2
+int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st);
+// minimizer slots: read r gets [rd_off[r] + 16r, rd_off[r+1] + 16(r+1)), or `slot` entries each when non-zero (tests)
+int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st);
 int launch_mid_hist(const mm2g::IxEntry* tab, uint64_t cap, uint32_t nbins, unsigned long long* hist, uint32_t* ovf, uint32_t ovf_cap,
                     uint32_t* ovf_n, hipStream_t st);
 int launch_ix_build(const uint64_t* keys, const uint32_t* offs, const uint32_t* ns, uint64_t nk, mm2g::IxEntry* tab, uint32_t log2cap, hipStream_t st);

@@ -103,7 +103,7 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
                      const std::vector<std::string>* names, int w, int k, int b, int flag, HostIndex& idx, std::string& err,
                      bool& unsupported) {
     unsupported = false;
-    const bool prof = getenv("MM2G_IXPROF") && atoi(getenv("MM2G_IXPROF")) != 0;
+    const bool prof = g_index_knob[2].load() != 0;   // MM2G_IKNOB_IXPROF
     auto t_last = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
         if (!prof) return;
@@ -140,7 +140,7 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     for (size_t i = 0; i < n; ++i)
         if (lens[i]) IXCHK(hipMemcpyAsync(d_seq + idx.seq[i].offset, seqs[i], lens[i], hipMemcpyHostToDevice, st));
     int64_t chunk = IX_CHUNK;
-    if (const char* e = getenv("MM2G_IXCHUNK")) chunk = std::max<int64_t>(256, atoll(e));   // tests
+    if (const int64_t v = g_index_knob[1].load()) chunk = std::max<int64_t>(256, v);   // MM2G_IKNOB_IXCHUNK (tests)
     const int64_t warm = 2 * (w + k) + 64;
     std::vector<uint64_t> v_off, v_base, v_end;
     std::vector<uint32_t> v_len, v_pre, v_from, v_rid;

@@ -9,6 +9,7 @@
 #include <stdint.h>
 #include <limits.h>
 #include <algorithm>
+#include <type_traits>
 #include "mm2g_internal.h"
 
 using namespace mm2g;
@@ -194,7 +195,44 @@ DEVI void codes8(uint64_t v, uint32_t& code16, uint32_t& valid8) {
 }
 DEVI uint32_t rev8(uint32_t v) { return __builtin_bitreverse32(v) >> 24; }
 
-template <bool K32>
+// Base sources of k_sketch.  raw(p0) loads the 8 bases at p0 (a multiple of 8;
+// positions outside [0, L) read as ambiguous), decode() turns that into
+// code16/valid8 as above, code(p) is nt4 (src/nt4.rs:2-10) of one base.
+//   SeqAscii: ASCII bytes (index-build views into a contig, SketchArgs view_*).
+//   SeqNt4:   the device read format (include/mm2g.h "nt4 read batch"): 2-bit
+//             codes, base i at bits 2(i%8) of 16-bit word i/8; reads with an
+//             ambiguous base also carry a bitmap (bit i%8 of byte i/8).
+struct SeqAscii {
+    const uint8_t* s; int64_t L;
+    DEVI uint64_t raw(int64_t p0) const { return load_bases8(s, p0, L); }
+    DEVI void decode(uint64_t v, uint32_t& code16, uint32_t& valid8) const { codes8(v, code16, valid8); }
+    DEVI uint32_t code(int64_t p) const { return nt4d(s[p]); }
+};
+DEVI uint32_t rev2_16(uint32_t x) {
+    x = ((x >> 2) & 0x3333u) | ((x & 0x3333u) << 2);
+    x = ((x >> 4) & 0x0F0Fu) | ((x & 0x0F0Fu) << 4);
+    return ((x >> 8) | (x << 8)) & 0xffffu;
+}
+struct SeqNt4 {
+    const uint16_t* s2; const uint8_t* am; int64_t L;
+    DEVI uint64_t raw(int64_t p0) const {
+        if (p0 < 0 || p0 >= L) return 0;
+        const uint64_t nv = L - p0 < 8 ? (uint64_t)(L - p0) : 8u;
+        const uint64_t v = s2[p0 >> 3], m = am ? am[p0 >> 3] : 0u;
+        return v | (m << 16) | (nv << 24);
+    }
+    DEVI void decode(uint64_t v, uint32_t& code16, uint32_t& valid8) const {
+        const uint32_t nv = (uint32_t)(v >> 24) & 15u;
+        code16 = rev2_16((uint32_t)v & 0xffffu);
+        valid8 = ~(uint32_t)(v >> 16) & ((1u << nv) - 1u);
+    }
+    DEVI uint32_t code(int64_t p) const {
+        if (am && ((am[p >> 3] >> (p & 7)) & 1u)) return 4u;
+        return ((uint32_t)s2[p >> 3] >> (2 * (p & 7))) & 3u;
+    }
+};
+
+template <bool K32, typename Src>
 #ifndef SK_WPE
 #define SK_WPE 4            // waves per SIMD: caps k_sketch at 128 VGPRs
 #endif
@@ -220,7 +258,13 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
             roff = uni64(a.rd_off[r]);
             L = (int64_t)(uni64(a.rd_off[r + 1]) - roff);
         }
-        const uint8_t* s = a.seq + roff;
+        Src src;
+        if constexpr (std::is_same<Src, SeqNt4>::value) {
+            const uint64_t ao = uni64(a.amb_off[r]);
+            src = Src{(const uint16_t*)(a.pk_words + uni64(a.pk_off[r])), ao == U64MAX ? nullptr : (const uint8_t*)(a.pk_words + ao), L};
+        } else {
+            src = Src{a.seq + roff, L};
+        }
         const uint64_t obase = uni64(a.out_base[r]), oend = uni64(a.out_end[r]);
         if (L == 0) { if (lane == 0) a.mz_cnt[r] = 0; continue; }
         uint64_t pt[6] = {0, 0, 0, 0, 0, 0}, tz = a.prof ? wall_clock64() : 0;
@@ -236,7 +280,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
         // bases of this lane's chunk, prefetched one tile ahead; lanes 0-3 also
         // keep the previous tile's last 32 bases (codes | reversed validity << 16)
         uint32_t code16, valid8;
-        codes8(load_bases8(s, (int64_t)lane * SK_CH, L), code16, valid8);
+        src.decode(src.raw((int64_t)lane * SK_CH), code16, valid8);
         uint32_t halo = 0;
         for (int64_t t0 = 0; t0 < L; t0 += SK_TS) {
             // opaque per tile: keeps lane-derived values from being hoisted and held
@@ -248,7 +292,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
             const int64_t pe = ps + SK_CH < L ? ps + SK_CH : L;
             // next tile's bases: loaded now, decoded before this tile's first store
             // (vmcnt also counts stores: decoding later would wait for them)
-            const uint64_t nbytes = t0 + SK_TS < L ? load_bases8(s, ps + SK_TS, L) : 0;
+            const uint64_t nbytes = t0 + SK_TS < L ? src.raw(ps + SK_TS) : 0;
             const uint32_t own = code16 | (rev8(valid8) << 16);
             wave_lds_sync();
             SK_PT(0);
@@ -279,12 +323,12 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                     int64_t wsp = ps;
                     int need = slow ? k - 1 : 0;
                     while (any(need > 0 && wsp > -pre)) {   // back to the contig start (views: before the view)
-                        if (need > 0 && wsp > -pre) { --wsp; if (nt4d(s[wsp]) < 4) --need; }
+                        if (need > 0 && wsp > -pre) { --wsp; if (src.code(wsp) < 4) --need; }
                     }
                     int64_t pw = slow ? wsp : ps;
                     while (any(pw < ps)) {
                         if (pw < ps) {
-                            const uint32_t c = nt4d(s[pw]);
+                            const uint32_t c = src.code(pw);
                             if (c < 4) { kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1); }
                             ++pw;
                         }
@@ -354,7 +398,7 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
             SK_PT(2);
 #define SK_Y(q) ((((uint32_t)(hbase + (q))) << 1) | (uint32_t)(LZ[SKP((q))] >> 15))
             uint32_t code16n, valid8n;
-            codes8(nbytes, code16n, valid8n);
+            src.decode(nbytes, code16n, valid8n);
             // ---- phase 2: reference step logic, count then write
             uint32_t myoff = 0, tot = 0;
             bool fast_done = false;
@@ -518,8 +562,12 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                 ++count;
             }
             if (lane == 0) {
-                a.mz_cnt[r] = (uint32_t)(count > 0xffffffffULL ? 0xffffffffULL : count);
-                if (obase + count > oend) atomicOr(a.overflow, 1);
+                // a count beyond the slot is clamped (every later kernel stays inside the
+                // buffers) and flagged; the true count lets the host size an exact re-run
+                const uint64_t capn = oend - obase;
+                a.mz_cnt[r] = (uint32_t)(count > capn ? capn : count);
+                if (a.mz_need) a.mz_need[r] = (uint32_t)(count > 0xffffffffULL ? 0xffffffffULL : count);
+                if (count > capn) atomicOr(a.overflow, 1);
             }
         }
         SK_PT(4);
@@ -559,10 +607,11 @@ __global__ __launch_bounds__(1024) void k_filter(FilterArgs a, int a_k) {
     const uint64_t mb = a.mz_base[r];
     const uint32_t m = a.mz_cnt[r];
     uint8_t* keep = a.keep + mb;
-    const uint64_t tb = a.tab_off[r];
-    const uint32_t ts = (uint32_t)(a.tab_off[r + 1] - tb);
+    const uint32_t ts = tab_size_for(m, a.q_occ_max);
     if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) return;   // seeds.rs:14-15: k_filter_lds
     if (filter_lds_ok(ts, a_k)) return;                        // done by k_filter_lds
+    const uint64_t tb = a.tab_off[r];                          // prefix of the global tables only
+    if (tb + ts > a.cap_tab) return;                           // workspace too small: batch flagged BS_TAB by the scan
     uint64_t* tk = a.tab_key + tb; uint32_t* tc = a.tab_cnt + tb;
     for (uint32_t i = tid; i < ts; i += 1024) { tk[i] = U64MAX; tc[i] = 0; }
     __threadfence_block();
@@ -612,8 +661,7 @@ __global__ __launch_bounds__(256) void k_filter_lds(FilterArgs a, int k) {
     if (r >= a.n) return;
     const uint64_t mb = a.mz_base[r];
     const uint32_t m = a.mz_cnt[r];
-    const uint64_t tb = a.tab_off[r];
-    const uint32_t ts = (uint32_t)(a.tab_off[r + 1] - tb);
+    const uint32_t ts = tab_size_for(m, a.q_occ_max);
     uint8_t* keep = a.keep + mb;
     if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) {      // seeds.rs:14-15 (and m <= q_occ_max)
         for (uint32_t i = threadIdx.x; i < m; i += 256) keep[i] = 1;
@@ -730,6 +778,7 @@ DEVI uint64_t pack_anchor(uint64_t rr, uint32_t my, int32_t qlen, int span, cons
 }
 
 __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint32_t s_inc[4][64], s_poff[4][64], s_y[4][64];
     const int lane = lane_id(), wv = wave_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
@@ -797,6 +846,7 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
 constexpr int SORT_SMALL = 4096;
 
 __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t s[SORT_SMALL];
     const uint32_t r = blockIdx.x;
     if (r >= a.n) return;
@@ -1058,6 +1108,7 @@ DEVI void radix_range(uint64_t* src, uint64_t* dst, uint64_t* out, uint32_t A, u
 }
 
 __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t red[32];
     __shared__ uint32_t s_sc[16], s_kept, s_nbig;
     __shared__ uint2 s_big[BIG_MAX];
@@ -1507,6 +1558,7 @@ DEVI unsigned long long best_key(int32_t f, int32_t i) {
 // heavy read (k_chain_lb, k_chain_seg).  In the rescue pass only rescued reads
 // have items.  item_off[t] = first item of order[t]; item_off[n] = total.
 __global__ __launch_bounds__(1024) void k_seg_items(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint32_t sc[16];
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     uint32_t carry = 0;
@@ -1548,6 +1600,7 @@ DEVI uint32_t item_owner(const uint32_t* item_off, uint32_t n, uint32_t it) {
 // wave each).  The read's best (last argmax f) is merged with a packed
 // 64-bit atomicMax.
 __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     extern __shared__ __align__(16) unsigned char smem[];
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
@@ -1752,6 +1805,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
 // largest f nor a tie of it: k_chain_seg skips it (not in debug mode, where
 // the full f/pprev arrays are kept).
 __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     extern __shared__ __align__(16) unsigned char smem[];
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
@@ -1823,6 +1877,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
 // when anchor j is finished.
 constexpr int MJ = 4;
 __global__ __launch_bounds__(256) void k_chain_med(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     extern __shared__ __align__(16) unsigned char smem[];
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
@@ -1953,6 +2008,7 @@ __global__ __launch_bounds__(1024) void k_lseg_order(const uint32_t* lseg_n, uin
 
 // ---- 5b. one long segment per wave, wave-cooperative (heaviest first)
 __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     extern __shared__ __align__(16) unsigned char smem[];
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
@@ -2253,6 +2309,7 @@ constexpr int GIANT_MKW = 160;    // mark bitmap words (window <= max_iter 5000)
 // a.giant_gmax anchors; same algorithm, pointer doubling by ping-pong.
 template <bool G>
 __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ uint32_t s_flag;
     __shared__ unsigned long long s_best;
@@ -2578,6 +2635,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
 // chain_trange (178-200) and the rescue test of rescue_long_join (316-330).
 constexpr int FIN_CH = 2048;   // pprev entries staged per wave (LDS) for the chain walk
 __global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     // one wave per read; the pprev walk reads chunks of FIN_CH entries staged in
     // LDS (coalesced) instead of one dependent HBM load per chain anchor
     __shared__ int32_t s_pp[4][FIN_CH];
@@ -2642,7 +2700,16 @@ __global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
     const int32_t qe = (int32_t)(kb & qmask) + 1;
     int32_t qs = (int32_t)(kr & qmask) - (span - 1); if (qs < 0) qs = 0;
     int32_t ts, te;
-    if (g == 2u * a.kl.n_seq) { ts = 0; te = -1; }    // Q19: rpos = p - 2^31 < 0
+    if (g == 2u * a.kl.n_seq) {
+        // Q19: rpos = (x as i32) = p - 2^31 < 0 (paf.rs:133-145, wrapping i32).
+        // te starts at -1 and only rpos + 1 > -1 raises it.  rpos - (span-1)
+        // wraps to a large positive value exactly when p < span-1; p rises
+        // along the chain, so the minimum is negative (ts clamps to 0) unless
+        // every anchor wraps, and then it is the root's.
+        const uint32_t pb = (uint32_t)((kb >> qb) & rmask), pr = (uint32_t)((kr >> qb) & rmask);
+        te = max(-1, (int32_t)(pb | 0x80000000u) + 1);
+        ts = pb >= (uint32_t)(span - 1) ? 0 : (int32_t)(0x80000000u + pr - (uint32_t)(span - 1));
+    }
     else {
         te = (int32_t)((kb >> qb) & rmask) + 1;
         ts = (int32_t)((kr >> qb) & rmask) - (span - 1); if (ts < 0) ts = 0;
@@ -2689,6 +2756,7 @@ __global__ __launch_bounds__(1024) void k_read_order(uint32_t n, const uint32_t*
 
 constexpr int DV_LDS = 4096;   // minimizer positions staged per read (longer reads read HBM)
 __global__ __launch_bounds__(64) void k_dv(DvArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ int32_t Ps[DV_LDS];
     const uint32_t r = blockIdx.x;
     if (r >= a.n) return;
@@ -2766,7 +2834,8 @@ __global__ __launch_bounds__(64) void k_dv(DvArgs a) {
 // ============================================================================
 // out[i] = sum_{t<i} f(in[t]) for i in [0, n]; mode 0: identity, mode 1: filter
 // table size.  Single workgroup, 1024 threads, chunked with carry.
-__global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max) {
+__global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k,
+                                                    uint64_t cap, uint32_t* status, uint32_t bit, int slot) {
     __shared__ uint64_t wsum[16];
     __shared__ uint64_t carry_s;
     const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
@@ -2775,7 +2844,11 @@ __global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t
     for (uint32_t c0 = 0; c0 < n; c0 += 1024) {
         const uint32_t i = c0 + tid;
         uint64_t v = 0;
-        if (i < n) { uint32_t x = in[i]; v = mode == 1 ? (uint64_t)tab_size_for(x, q_occ_max) : (uint64_t)x; }
+        if (i < n) {
+            const uint32_t x = in[i];
+            if (mode == 1) { const uint32_t ts = tab_size_for(x, q_occ_max); v = filter_lds_ok(ts, k) ? 0 : ts; }
+            else v = x;
+        }
         uint64_t inc = wave_incl_scan(v, [](uint64_t x, uint64_t y) { return x + y; });
         if (lane == 63) wsum[wv] = inc;
         __syncthreads();
@@ -2787,12 +2860,35 @@ __global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t
         if (tid == 1023) carry_s = carry + woff + inc;
         __syncthreads();
     }
-    if (tid == 0) out[n] = carry_s;
+    if (tid == 0) {
+        const uint64_t tot = carry_s;
+        out[n] = tot;
+        if (status) {
+            ((unsigned long long*)status)[slot] = tot;
+            if (cap && tot > cap) atomicOr(status, bit);
+        }
+    }
 }
 
-__global__ void k_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end) {
+// per-batch sums for mm2g_batch_counters (st[3] = minimizers, st[4] = anchors in the DP)
+__global__ __launch_bounds__(1024) void k_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* st) {
+    __shared__ unsigned long long ws[2][16];
+    unsigned long long a = 0, b = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) { a += mz_cnt[i]; b += cnt2 ? cnt2[i] : 0u; }
+    a = wave_sum64(a); b = wave_sum64(b);
+    if (lane_id() == 0) { ws[0][threadIdx.x >> 6] = a; ws[1][threadIdx.x >> 6] = b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long x = 0, y = 0;
+        for (int t = 0; t < 16; ++t) { x += ws[0][t]; y += ws[1][t]; }
+        st[3] = x; st[4] = y;
+    }
+}
+
+__global__ void k_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
+    if (slot) { base[r] = (uint64_t)slot * r; end[r] = (uint64_t)slot * (r + 1); return; }   // tests: fixed slots
     base[r] = rd_off[r] + 16ull * r;
     end[r] = rd_off[r + 1] + 16ull * (r + 1);
 }
@@ -2846,8 +2942,13 @@ __global__ __launch_bounds__(256) void k_mid_hist(const IxEntry* tab, uint64_t c
 
 int launch_sketch(const SketchArgs& a, int n_blocks, hipStream_t st) {
     const size_t lds = sketch_wave_lds(a.w) * 4;
-    if (a.k <= 16) hipLaunchKernelGGL(k_sketch<true>, dim3(n_blocks), dim3(256), lds, st, a);
-    else hipLaunchKernelGGL(k_sketch<false>, dim3(n_blocks), dim3(256), lds, st, a);
+    if (a.pk_words) {
+        if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqNt4>), dim3(n_blocks), dim3(256), lds, st, a);
+        else hipLaunchKernelGGL((k_sketch<false, SeqNt4>), dim3(n_blocks), dim3(256), lds, st, a);
+    } else {
+        if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqAscii>), dim3(n_blocks), dim3(256), lds, st, a);
+        else hipLaunchKernelGGL((k_sketch<false, SeqAscii>), dim3(n_blocks), dim3(256), lds, st, a);
+    }
     LAUNCH_CHECK();
     return 0;
 }
@@ -2931,14 +3032,20 @@ int launch_dv(const DvArgs& a, hipStream_t st) {
     LAUNCH_CHECK();
     return 0;
 }
-int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, hipStream_t st) {
-    hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(1024), 0, st, in, n, out, mode, q_occ_max);
+int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k, uint64_t cap, uint32_t* status,
+                     uint32_t bit, int slot, hipStream_t st) {
+    hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(1024), 0, st, in, n, out, mode, q_occ_max, k, cap, status, bit, slot);
     LAUNCH_CHECK();
     return 0;
 }
-int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, hipStream_t st) {
+int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st) {
+    hipLaunchKernelGGL(k_batch_sums, dim3(1), dim3(1024), 0, st, n, mz_cnt, cnt2, status64);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st) {
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_mz_base, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, base, end);
+    hipLaunchKernelGGL(k_mz_base, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, base, end, slot);
     LAUNCH_CHECK();
     return 0;
 }

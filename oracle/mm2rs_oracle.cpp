@@ -778,7 +778,12 @@ static bool paf_from_chain_with_primary(const Index& idx, const std::vector<Anch
     if (qs < 0) qs = 0;
     if (ts < 0) ts = 0;
     size_t rid0 = (size_t)((anchors[chain[0]].x >> 32) & 0x7fffffff);
-    if (rid0 >= idx.seq.size()) { rec.panic = true; return false; }   // Rust: index out of bounds -> panic (Q19)
+    if (rid0 >= idx.seq.size()) {   // Rust: index out of bounds -> panic (Q19)
+        // the fields computed before the panic, for per-read comparisons (orc_align_records)
+        rec.panic = true; rec.qlen = (u32)qlen_sz; rec.qstart = (u32)qs; rec.qend = (u32)qe; rec.strand = strand;
+        rec.tstart = (u32)ts; rec.tend = (u32)te; rec.cm = cm;
+        return false;
+    }
     const IndexSeq& sq = idx.seq[rid0];
     std::string tname = sq.has_name ? sq.name : std::string("*");
     u32 tlen = sq.len;
@@ -849,6 +854,15 @@ static ChainParams default_chain_params(int32_t k) {
 // Per-read accounting the bench uses for algorithmic bytes
 static bool g_quiet = false;   // orc_set_quiet: silence per-read panic notes (bench)
 struct ReadCounts { u64 m_all = 0, m_kept = 0, anchors = 0, rescued = 0, inner_iters = 0, lines = 0, panics = 0; };
+// One read's outcome for per-read comparisons (orc_align_records), also for
+// reads on which the reference panics (Q19): the first chain's PAF columns as
+// paf_from_chain_with_primary computes them before the out-of-bounds index.
+struct ReadRec {
+    int32_t flags = 0;       // 1 a chain (a PAF line or a panic), 2 rescued, 8 panic
+    int32_t n_anchors = 0, score = 0, cm = 0, qs = 0, qe = 0, ts = 0, te = 0, rid = 0, rev = 0;
+    float dv = 0.0f;
+    int32_t m_kept = 0;
+};
 
 struct AlignOpts {
     int32_t w = 10, k = 15; float frac = 2e-4f; int32_t max_gap = 5000; int32_t bw = -1, bw_long = -1;
@@ -858,13 +872,14 @@ struct AlignOpts {
 // main.rs:189-230 Align flow for ONE read (the reference maps only the first
 // record; we apply it to every record and concatenate — SURVEY §0.3)
 static void align_one(const Index& idx, int32_t mid_occ, const AlignOpts& o, const std::string& qname, const uint8_t* q, size_t qlen,
-                      std::vector<std::string>& lines, ReadCounts* rc) {
+                      std::vector<std::string>& lines, ReadCounts* rc, ReadRec* rr = nullptr) {
     std::vector<Minimizer> mv = collect_query_minimizers(q, qlen, (size_t)o.w, (size_t)o.k);
     if (rc) rc->m_all += mv.size();
     filter_query_minimizers(mv, 10, 0.01f);
     if (rc) rc->m_kept += mv.size();
     std::vector<Anchor> anchors = build_anchors_filtered(idx, mv, (int32_t)qlen, mid_occ);
     if (rc) rc->anchors += anchors.size();
+    if (rr) { rr->n_anchors = (int32_t)anchors.size(); rr->m_kept = (int32_t)mv.size(); }
     ChainParams p = default_chain_params(o.k);
     p.max_dist_x = o.max_gap; p.max_dist_y = o.max_gap;
     p.min_cnt = o.min_cnt; p.min_chain_score = o.min_chain_score;
@@ -879,13 +894,22 @@ static void align_one(const Index& idx, int32_t mid_occ, const AlignOpts& o, con
     }
     bool rescued = false;
     DpResult resc = rescue_long_join(anchors, all, p, (int32_t)qlen, &rescued, rc ? &cs : nullptr);
+    if (rr && rescued) rr->flags |= 2;
     if (rc) { rc->rescued += rescued ? anchors.size() : 0; rc->inner_iters += cs.inner_iters; }
     std::vector<std::vector<size_t>> merged = merge_adjacent_chains_with_gap(anchors, resc.chains, p.max_dist_y, p.max_dist_y);
     std::vector<std::vector<size_t>> chains; int32_t s1, s2;
     select_and_filter_chains(anchors, merged, resc.scores, o.mask_level, o.pri_ratio, o.best_n, chains, s1, s2);
     for (size_t ci = 0; ci < chains.size(); ++ci) {   // paf.rs:238-248
         PafRecord rec;
-        if (paf_from_chain_with_primary(idx, anchors, chains[ci], qname, q, qlen, ci == 0, rec)) {
+        const bool ok = paf_from_chain_with_primary(idx, anchors, chains[ci], qname, q, qlen, ci == 0, rec);
+        if (rr && ci == 0 && (ok || rec.panic)) {
+            rr->flags |= 1 | (rec.panic ? 8 : 0);
+            rr->score = s1; rr->cm = (int32_t)rec.cm; rr->qs = (int32_t)rec.qstart; rr->qe = (int32_t)rec.qend;
+            rr->ts = (int32_t)rec.tstart; rr->te = (int32_t)rec.tend;
+            rr->rid = (int32_t)((anchors[chains[ci][0]].x >> 32) & 0x7fffffff); rr->rev = rec.strand == '-';
+            rr->dv = ok ? rec.dv : 0.0f;
+        }
+        if (ok) {
             rec.s1 = (u32)std::max(s1, 0); rec.s2 = (u32)std::max(s2, 0);
             lines.push_back(write_paf(rec));
             if (rc) rc->lines += 1;
@@ -1108,6 +1132,36 @@ long long orc_align_seqs(void* idx, int n, const char* const* names, const uint8
     if (f && f != stdout) fclose(f);
     if (counts) { counts[0] = rc.m_all; counts[1] = rc.m_kept; counts[2] = rc.anchors; counts[3] = rc.rescued; counts[4] = rc.inner_iters; counts[5] = rc.lines; counts[6] = rc.panics; }
     return nl;
+}
+
+// Per-read outcomes (ReadRec, 12 int32 each: flags, n_anchors, score, cm, qs,
+// qe, ts, te, rid, rev, dv bits, m_kept) of the Align flow over in-memory reads.
+long long orc_align_records(void* idx, int n, const uint8_t* const* seqs, const uint64_t* lens, const int* oi, const float* of,
+                            int mid_occ, int nthreads, int32_t* rec) {
+    Index* I = (Index*)idx;
+    AlignOpts o;
+    o.w = oi[0]; o.k = oi[1]; o.max_gap = oi[2]; o.bw = oi[3]; o.bw_long = oi[4]; o.min_cnt = oi[5]; o.min_chain_score = oi[6]; o.best_n = (size_t)oi[7];
+    o.frac = of[0]; o.mask_level = of[1]; o.pri_ratio = of[2];
+    if (mid_occ < 0) { mid_occ = I->calc_mid_occ(o.frac); if (mid_occ < 10) mid_occ = 10; }
+    if (nthreads < 1) nthreads = 1;
+    std::atomic<int> next{0};
+    auto worker = [&]() {
+        std::vector<std::string> lines;
+        for (;;) {
+            const int r = next.fetch_add(1);
+            if (r >= n) break;
+            ReadRec R;
+            if (lens[r]) { lines.clear(); align_one(*I, mid_occ, o, std::string("q"), seqs[r], (size_t)lens[r], lines, nullptr, &R); }
+            int32_t* d = rec + 12 * (size_t)r;
+            d[0] = R.flags; d[1] = R.n_anchors; d[2] = R.score; d[3] = R.cm; d[4] = R.qs; d[5] = R.qe; d[6] = R.ts; d[7] = R.te;
+            d[8] = R.rid; d[9] = R.rev; memcpy(&d[10], &R.dv, 4); d[11] = R.m_kept;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(worker);
+    worker();
+    for (auto& x : th) x.join();
+    return n;
 }
 
 // Pen LUT value as the reference computes it inline (comput_sc), for LUT parity tests.

@@ -64,6 +64,9 @@ def lib() -> C.CDLL:
         L.orc_align_seqs.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, _P64, C.c_char_p, C.POINTER(C.c_int),
                                      C.POINTER(C.c_float), C.c_int, C.c_int, _P64, C.POINTER(C.c_double)]
         L.orc_set_quiet.argtypes = [C.c_int]
+        L.orc_align_records.restype = C.c_longlong
+        L.orc_align_records.argtypes = [C.c_void_p, C.c_int, C.c_void_p, _P64, C.POINTER(C.c_int), C.POINTER(C.c_float), C.c_int,
+                                        C.c_int, C.POINTER(C.c_int32)]
         L.orc_pen.restype = C.c_int
         L.orc_pen.argtypes = [C.c_int, C.c_int, C.c_int, C.c_float]
         L.orc_default_gap.restype = C.c_float
@@ -205,6 +208,26 @@ class OIndex:
                                  oi, of, mid_occ, threads, cnt, C.byref(t))
         keys = ["m_all", "m_kept", "anchors", "rescued_anchors", "inner_iters", "lines", "panics"]
         return n, dict(zip(keys, list(cnt))), t.value
+
+
+REC_FIELDS = ("flags", "n_anchors", "score", "cm", "qs", "qe", "ts", "te", "rid", "rev", "dv", "m_kept")
+
+
+def align_records(oi: "OIndex", seqs, mid_occ: int = -1, threads: int = 4, w: int = 10, k: int = 15, max_gap: int = 5000,
+                  bw: int = -1, bw_long: int = -1, min_cnt: int = 3):
+    """Per-read outcome of the Align flow (incl. reads on which the reference
+    panics, Q19): an (n, 12) int32 array with columns REC_FIELDS (dv as f32 bits)."""
+    n = len(seqs)
+    bufs = [C.create_string_buffer(bytes(s), max(len(s), 1)) for s in seqs]
+    ptrs = (C.c_void_p * max(n, 1))(*[C.cast(b, C.c_void_p).value for b in bufs])
+    lens = np.array([len(s) for s in seqs], dtype=np.uint64)
+    oi_ = (C.c_int * 10)(w, k, max_gap, bw, bw_long, min_cnt, 40, 5, 0, 0)
+    of = (C.c_float * 3)(2e-4, 0.5, 0.8)
+    rec = np.zeros((max(n, 1), 12), dtype=np.int32)
+    set_quiet(True)
+    lib().orc_align_records(oi.h, n, ptrs, lens.ctypes.data_as(_P64), oi_, of, mid_occ, threads,
+                            rec.ctypes.data_as(C.POINTER(C.c_int32)))
+    return rec[:n]
 
 
 def set_quiet(q: bool = True) -> None:

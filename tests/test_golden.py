@@ -172,8 +172,8 @@ def test_mmi_load_mapped_parallel(world, tmp_path, monkeypatch):
     dup.write_bytes(_mmi_rewrite(raw, lambda e: ([(e[0][0], 1 | 0)] + e) if e and (e[0][0] & 1) else e))
     want = [idx.get(g["key"]) for g in world["gets"]]
     for path in (p, str(rev), str(dup)):
-        for thr in ("1", "5"):
-            monkeypatch.setenv("MM2G_LOAD_THREADS", thr)
+        for thr in (1, 5):
+            M.set_index_knob("load_threads", thr)
             back = M.Index.load_from_mmi(path)
             assert tuple(back.stats()) == tuple(idx.stats())
             assert [back.get(g["key"]) for g in world["gets"]] == want
@@ -182,7 +182,7 @@ def test_mmi_load_mapped_parallel(world, tmp_path, monkeypatch):
             q = str(tmp_path / "re.mmi")
             back.save_to_mmi(q)
             assert open(q, "rb").read() == raw
-    monkeypatch.delenv("MM2G_LOAD_THREADS")
+    M.set_index_knob("load_threads", 0)
     cut = tmp_path / "cut.mmi"
     for n in (3, 20, 30, len(raw) // 3, len(raw) // 2, len(raw) - 1):
         cut.write_bytes(raw[:n])

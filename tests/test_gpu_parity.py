@@ -2,6 +2,7 @@
 
 All calls go through libmm2g.so's C ABI (minimap2_rs_amd wraps it with
 ctypes); the oracle is only the checker."""
+import contextlib
 import os
 import random
 
@@ -11,6 +12,8 @@ import pytest
 import minimap2_rs_amd as M
 from oracle import oracle as O
 from tools import simdata
+from tests.gpu_common import (_mutate, _production_vs_oracle, _rand_seq, _singleton_keep, assert_records, dense_world, knobs,  # noqa: F401
+                              small_world)
 
 pytestmark = pytest.mark.gpu
 
@@ -20,17 +23,6 @@ def dev():
     d = M.Device(0)
     yield d
     d.close()
-
-
-def _rand_seq(rng, n, p_n=0.0, p_low=0.1, alphabet=b"ACGT"):
-    s = bytearray(rng.choice(alphabet) for _ in range(n))
-    for i in range(n):
-        r = rng.random()
-        if r < p_n:
-            s[i] = ord(rng.choice("NnRYKM-*"))
-        elif r < p_n + p_low:
-            s[i] = s[i] | 0x20 if chr(s[i]).isalpha() else s[i]
-    return bytes(s)
 
 
 def _edge_seqs(rng):
@@ -68,28 +60,6 @@ def test_sketch_rid(dev):
     got = dev.sketch_sequences(seqs, 10, 15, rid=7)
     for i, s in enumerate(seqs):
         assert np.array_equal(got[i], O.sketch(s, 10, 15, 7, False))
-
-
-@pytest.fixture(scope="module")
-def small_world(tmp_path_factory):
-    td = tmp_path_factory.mktemp("world")
-    ref = str(td / "ref.fa")
-    simdata.write_genome("hg38", 0.0008, 21, ref)        # 24 contigs, ~2.5 Mb, hg38-shaped repeats
-    names, seqs = simdata.read_fasta_seqs(ref)
-    lens = np.array([len(s) for s in seqs], dtype=np.int64)
-    g = np.frombuffer(b"".join(seqs), dtype=np.uint8)
-    rb, offs, _ = simdata.reads(g, lens, 150, 6000, 22)
-    rnames = [f"r{i}" for i in range(150)]
-    rseqs = [rb[offs[i]:offs[i + 1]].tobytes() for i in range(150)]
-    rng = random.Random(3)
-    extra = [(b"ACGT" * 3), _rand_seq(rng, 5000), _rand_seq(rng, 30), b"N" * 100,
-             seqs[0][20000:21000], seqs[1][30000:30500].lower(), seqs[2][40000:52000]]
-    for i, s in enumerate(extra):
-        rnames.append(f"x{i}")
-        rseqs.append(s)
-    reads = str(td / "reads.fa")
-    simdata.write_fasta(reads, rnames, rseqs)
-    return ref, reads, rnames, rseqs
 
 
 def _map_nodebug(dev, rnames, rseqs):
@@ -152,55 +122,6 @@ def test_pipeline_determinism(dev, small_world):
     p1 = M.align(idx, rnames, rseqs, dev=dev)
     p2 = M.align(idx, rnames, rseqs, dev=dev)
     assert p1 == p2 and p1.count("\n") > 50
-
-
-def _mutate(rng, s: bytes, p: float) -> bytes:
-    b = bytearray(s)
-    for i in range(len(b)):
-        if rng.random() < p:
-            b[i] = ord(rng.choice("ACGT"))
-    return bytes(b)
-
-
-@pytest.fixture(scope="module")
-def dense_world(tmp_path_factory):
-    """Satellite arrays + segmental duplications: windows of thousands of
-    anchors once mid_occ is lifted (deep j-steps beyond the LDS ring, n_skip
-    breaks, max_iter clipping, rescue)."""
-    td = tmp_path_factory.mktemp("dense")
-    rng = random.Random(77)
-    mono = _rand_seq(rng, 171, p_low=0.0)
-    sat = b"".join(_mutate(rng, mono, 0.03) for _ in range(120))                 # ~20 kb alpha-like array
-    unit = _rand_seq(rng, 2000, p_low=0.0)
-    sd = b"".join(_mutate(rng, unit, 0.01) for _ in range(12))                   # 24 kb tandem segmental dup
-    c0 = _rand_seq(rng, 30000, p_low=0.0) + sat + _rand_seq(rng, 30000, p_low=0.0)
-    c1 = _rand_seq(rng, 10000, p_low=0.0) + sd + _rand_seq(rng, 10000, p_low=0.0)
-    sd2 = b"".join(_mutate(rng, unit[:1500], 0.02) for _ in range(10))          # 15 kb on an even rid
-    c2 = _rand_seq(rng, 40000, p_low=0.0) + sd2 + _rand_seq(rng, 8000, p_low=0.0)
-    ref = str(td / "dense.fa")
-    simdata.write_fasta(ref, ["c0", "c1", "c2"], [c0, c1, c2])
-    rnames, rseqs = [], []
-    for t in range(8):                       # inside the satellite
-        st = 30000 + rng.randrange(0, len(sat) - 4000)
-        rseqs.append(_mutate(rng, c0[st:st + 3500], 0.04))
-    for t in range(8):                       # inside / across the segmental dup
-        st = 10000 + rng.randrange(-3000, len(sd) - 3000)
-        rseqs.append(_mutate(rng, c1[st:st + 6000], 0.03))
-    for t in range(6):                       # unique sequence, one crossing into the array
-        st = rng.randrange(0, len(c2) - 5000)
-        rseqs.append(_mutate(rng, c2[st:st + 5000], 0.05))
-    rseqs.append(c0[27000:27000 + 6000])
-    for t in range(4):                       # chimeras: half unique, half elsewhere -> rescue DP
-        a0 = rng.randrange(0, 20000)
-        b0 = rng.randrange(0, 30000)
-        rseqs.append(_mutate(rng, c2[a0:a0 + 4000] + c0[b0:b0 + 4000], 0.03))
-    for t in range(4):                       # inside the even-rid duplication
-        st = 40000 + rng.randrange(0, len(sd2) - 5000)
-        rseqs.append(_mutate(rng, c2[st:st + 5000], 0.03))
-    rnames = [f"d{i}" for i in range(len(rseqs))]
-    reads = str(td / "dense_reads.fa")
-    simdata.write_fasta(reads, rnames, rseqs)
-    return ref, reads, rnames, rseqs
 
 
 @pytest.mark.parametrize("mid_occ", [20, 5000])
@@ -278,31 +199,16 @@ def test_golden_world_gpu(dev, tmp_path):
     got = dev.paf([r["name"] for r in gold["reads"]], res).splitlines()
     assert got == [r["paf"] for r in gold["reads"] if r["paf"]]
     assert _map_nodebug(dev, [r["name"] for r in gold["reads"]], seqs)[0].splitlines() == got
+    dev.set_debug(True)
 
 
-def test_singleton_filter_is_transparent(dev, small_world, dense_world):
-    """Every per-read result field is identical with the sort's singleton
-    filter on (production) and off (debug): dropped anchors only ever form
-    one-anchor segments, and the largest dropped key settles f == span ties."""
-    os.environ["MM2G_SORT_SMALL"] = "1"        # every read through k_sort_read (the filtering sort)
-    try:
-        _filter_transparent(dev, small_world, dense_world)
-    finally:
-        del os.environ["MM2G_SORT_SMALL"]
-
-
-def _filter_transparent(dev, small_world, dense_world):
-    for world, mid in ((small_world, None), (dense_world, 5000), (dense_world, 20)):
-        ref, reads, rnames, rseqs = world
-        idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
-        dev.upload_index(idx, mid if mid is not None else max(idx.calc_mid_occ(2e-4), 10))
-        dev.set_debug(True)
-        dev.set_reads(rseqs)
-        r1 = dev.map(M.map_opts())
-        a = [tuple(getattr(r1[i], f) for f in _RES_FIELDS) for i in range(len(rseqs))]
-        _, r2 = _map_nodebug(dev, rnames, rseqs)
-        b = [tuple(getattr(r2[i], f) for f in _RES_FIELDS) for i in range(len(rseqs))]
-        assert a == b
+def test_singleton_filter_vs_oracle(dev, small_world, dense_world):
+    """Production path with every read through k_sort_read (the filtering
+    sort): PAF and every per-read field equal the oracle's (dropped anchors
+    only ever form one-anchor segments; the largest dropped key settles
+    f == span ties)."""
+    with knobs(dev, sort_small=1):
+        _production_vs_oracle(dev, small_world, dense_world)
 
 
 def test_cli_align_gpu(small_world, tmp_path):
@@ -319,21 +225,6 @@ def test_cli_align_gpu(small_world, tmp_path):
     assert g == c and g.count("\n") > 50
 
 
-def _singleton_keep(a: np.ndarray) -> np.ndarray:
-    """The sort's singleton filter restated on (x, y) anchors: keep an anchor
-    iff its 32 kb cell of its (rid, strand) group -- or of the Q19
-    pseudo-group -- holds another anchor, or a neighbouring cell does."""
-    x = a[:, 0]
-    hi = x >> np.uint64(32)
-    gid = np.where(hi == np.uint64(0xffffffff), np.uint64(1 << 33), hi)
-    cell = (gid << np.uint64(20)) | ((x & np.uint64(0x7fffffff)) >> np.uint64(15))
-    u, inv, cnt = np.unique(cell, return_inverse=True, return_counts=True)
-    occ = set(u.tolist())
-    left = np.array([(c - 1) in occ for c in cell.tolist()], dtype=bool)
-    right = np.array([(c + 1) in occ for c in cell.tolist()], dtype=bool)
-    return (cnt[inv] >= 2) | left | right
-
-
 @pytest.mark.parametrize("seg_small", [1024, 64, 8, 1])
 def test_filtered_sort_parity(dev, small_world, dense_world, seg_small):
     """Production sort (cell buckets + per-segment ranking, singleton filter
@@ -341,9 +232,7 @@ def test_filtered_sort_parity(dev, small_world, dense_world, seg_small):
     the singletons, for every path -- thread-ranked small segments, block-
     ranked and radix-sorted big ones, the whole-read radix when too many big
     segments (seg_small 1) or too many anchors (> 65535) appear."""
-    os.environ["MM2G_SORT_SMALL"] = "1"
-    os.environ["MM2G_SEG_SMALL"] = str(seg_small)
-    try:
+    with knobs(dev, sort_small=1, seg_small=seg_small):
         rng = random.Random(5)
         for world, mids in ((small_world, (None,)), (dense_world, (20, 5000, 100000))):
             ref, reads, rnames, rseqs = world
@@ -364,10 +253,7 @@ def test_filtered_sort_parity(dev, small_world, dense_world, seg_small):
                         want = want[_singleton_keep(want)]
                     got = dev.debug_anchors(r)
                     assert np.array_equal(got, want), (seg_small, mid, r, len(got), len(want))
-    finally:
-        del os.environ["MM2G_SORT_SMALL"]
-        del os.environ["MM2G_SEG_SMALL"]
-        dev.set_debug(True)
+    dev.set_debug(True)
 
 
 @pytest.mark.parametrize("chunk", [64, 192])
@@ -375,8 +261,7 @@ def test_chunked_chain_items(dev, small_world, dense_world, tmp_path, chunk):
     """Reads cut into many small work items (a wave per chunk, each finishing
     the segment open at its end; the lower bound restarting per chunk): DP
     arrays (debug) and PAF (production, pruning on) still equal the oracle's."""
-    os.environ["MM2G_SEG_CHUNK"] = str(chunk)
-    try:
+    with knobs(dev, seg_chunk=chunk):
         for world, mid in ((small_world, None), (dense_world, 5000), (dense_world, 20)):
             ref, reads, rnames, rseqs = world
             oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
@@ -400,9 +285,7 @@ def test_chunked_chain_items(dev, small_world, dense_world, tmp_path, chunk):
             want = open(want_paf).read()
             assert dev.paf(rnames, res) == want
             assert _map_nodebug(dev, rnames, rseqs)[0] == want
-    finally:
-        del os.environ["MM2G_SEG_CHUNK"]
-        dev.set_debug(True)
+    dev.set_debug(True)
 
 
 def _mmi_bytes(idx, path):
@@ -413,9 +296,11 @@ def _mmi_bytes(idx, path):
 @pytest.mark.parametrize("chunk", [None, 4096, 300])
 def test_gpu_index_build(tmp_path, chunk):
     """GPU index build (sketch views, pair sort, bucket distribution, packed S)
-    equals the host build byte for byte (.mmi), with stats and mid_occ, on an
-    hg38-shaped and an E. coli-shaped genome plus edge contigs: N runs across
-    view boundaries, lowercase, contigs shorter than k, empty contigs."""
+    equals the oracle's build_index_from_fasta + save_to_mmi (index.rs:74-109,
+    233-307) byte for byte (.mmi), with stats and calc_mid_occ (index.rs:
+    111-141), on an hg38-shaped and an E. coli-shaped genome plus edge contigs:
+    N runs across view boundaries, lowercase, contigs shorter than k, empty
+    contigs.  The product's host build must agree as well."""
     rng = random.Random(11)
     names, lens, gbuf = simdata.genome("hg38", 0.0006, 5)
     seqs = [gbuf[int(o):int(o + l)].tobytes() for o, l in zip(np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)]
@@ -426,19 +311,23 @@ def test_gpu_index_build(tmp_path, chunk):
         s[st_:st_ + 60] = b"N" * 60
     seqs += [bytes(s), _rand_seq(rng, 9000, p_low=0.3), b"ACGTACGT", b"", _rand_seq(rng, 15, p_n=0.0), b"N" * 500 + _rand_seq(rng, 3000)]
     names += ["nruns", "lower", "short", "empty", "k15", "leadingN"]
-    if chunk is not None:
-        os.environ["MM2G_IXCHUNK"] = str(chunk)
+    M.set_index_knob("ixchunk", chunk or 0)
     try:
+        buf = np.frombuffer(b"".join(seqs), dtype=np.uint8)
+        lv = np.array([len(x) for x in seqs], dtype=np.uint64)
         for w, k in ((10, 15), (5, 11), (19, 19), (10, 27)):
-            ih = M.Index.build_from_seqs(names, seqs, w=w, k=k, b=14, threads=4)
-            buf = np.frombuffer(b"".join(seqs), dtype=np.uint8)
-            lv = np.array([len(x) for x in seqs], dtype=np.uint64)
+            oi = O.OIndex.build_from_buffer(names, buf, lv, w=w, k=k, b=14, threads=4)
             ig = M.Index.build_from_buffer(names, buf, lv, w=w, k=k, b=14, threads=4, device=0)
-            assert ih.stats() == ig.stats(), (w, k)
-            assert ih.calc_mid_occ(2e-4) == ig.calc_mid_occ(2e-4)
-            assert _mmi_bytes(ih, str(tmp_path / "h.mmi")) == _mmi_bytes(ig, str(tmp_path / "g.mmi")), (w, k)
+            ih = M.Index.build_from_seqs(names, seqs, w=w, k=k, b=14, threads=4)
+            assert ig.stats() == oi.stats() == ih.stats(), (w, k)
+            for fr in (2e-4, 0.01, 0.5):
+                assert ig.calc_mid_occ(fr) == oi.mid_occ(fr) == ih.calc_mid_occ(fr)
+            oi.save_mmi(str(tmp_path / "o.mmi"))
+            want = open(str(tmp_path / "o.mmi"), "rb").read()
+            assert _mmi_bytes(ig, str(tmp_path / "g.mmi")) == want, (w, k)
+            assert _mmi_bytes(ih, str(tmp_path / "h.mmi")) == want, (w, k)
     finally:
-        os.environ.pop("MM2G_IXCHUNK", None)
+        M.set_index_knob("ixchunk", 0)
 
 
 def test_cli_streaming_fastq(small_world, tmp_path):
@@ -485,30 +374,28 @@ def test_cli_anchors_chain(small_world, tmp_path):
         assert got == want, bw
 
 
-@pytest.mark.parametrize("giant_min,lcap", [(16, None), (200, None), (16, "64")])
-def test_giant_segments_jacobi(dev, small_world, dense_world, monkeypatch, giant_min, lcap):
+@pytest.mark.parametrize("giant_min,giant_min0,lcap", [(16, 0, 0), (200, 0, 0), (16, 0, 64), (16, 16, 0), (16, 16, 64)])
+def test_giant_segments(dev, small_world, dense_world, giant_min, giant_min0, lcap):
     """Long segments through k_chain_giant (policy iteration to the fixed point
     of the no-break DP, the reference loop verified wherever a window holds
-    more than max_skip mark sources, k_chain_long when it does not settle):
-    every result field equals the debug run's (exact sequential DP), and PAF
-    equals the oracle's.  lcap 64 sends every segment over 64 anchors to the
-    HBM-scratch variant (k_chain_giant<true>)."""
-    monkeypatch.setenv("MM2G_GIANT_MIN", str(giant_min))
-    if lcap:
-        monkeypatch.setenv("MM2G_GIANT_LCAP", lcap)
-    _filter_transparent(dev, small_world, dense_world)
+    more than max_skip mark sources, k_chain_long when it does not settle),
+    in the rescue pass and (giant_min0) pass 0's exact mode: PAF and every
+    per-read field equal the oracle's.  lcap 64 sends every segment over 64
+    anchors to the HBM-scratch variant (k_chain_giant<true>)."""
+    with knobs(dev, giant_min=giant_min, giant_min0=giant_min0, giant_lcap=lcap):
+        _production_vs_oracle(dev, small_world, dense_world, tag=f"giant {giant_min}/{giant_min0}/{lcap}")
 
 
-@pytest.mark.parametrize("bins", [None, "2", "3", "64"])
-def test_device_mid_occ(dev, small_world, dense_world, monkeypatch, bins):
+@pytest.mark.parametrize("bins", [4096, 2, 3, 64])
+def test_device_mid_occ(dev, small_world, dense_world, bins):
     """calc_mid_occ (index.rs:124-141) from the device table's count histogram
-    equals the host's sort of all counts, at quantiles inside the histogram and
-    in its overflow (few bins force the gathered-overflow path)."""
-    if bins:
-        monkeypatch.setenv("MM2G_MIDHIST_BINS", bins)
-    for ref in (small_world[0], dense_world[0]):
-        idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
-        dev.upload_index(idx, 10)
-        for fr in (0.0, 2e-4, 1e-3, 0.01, 0.1, 0.5, 0.9, 1.0, 1.5, -0.25):
-            assert dev.index_mid_occ(fr) == idx.calc_mid_occ(fr), (ref, fr)
+    equals the oracle's sort of all counts, at quantiles inside the histogram
+    and in its overflow (few bins force the gathered-overflow path)."""
+    with knobs(dev, midhist_bins=bins):
+        for ref in (small_world[0], dense_world[0]):
+            oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+            idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+            dev.upload_index(idx, 10)
+            for fr in (0.0, 2e-4, 1e-3, 0.01, 0.1, 0.5, 0.9, 1.0, 1.5, -0.25):
+                assert dev.index_mid_occ(fr) == oi.mid_occ(fr), (ref, fr)
     dev.set_mid_occ(10)

@@ -37,7 +37,7 @@ def main():
     idx.close()
     try:
         for thr in ("1", str(a.threads)):
-            os.environ["MM2G_LOAD_THREADS"] = thr
+            M.set_index_knob("load_threads", int(thr))
             t = time.time()
             back = M.Index.load_from_mmi(a.path)
             r[f"load_s_{thr}t"] = round(time.time() - t, 2)

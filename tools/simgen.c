@@ -13,6 +13,7 @@
 //          10 kb N telomeres and a 50 kb N gap; repeats soft-masked
 //          (lowercase), as hg38 is.
 //   ecoli  1 contig of 4,641,652 bp, GC 50.8 %, 1 % IS-like 1.3 kb copies.
+//   chr8chr12  hg38 chr8 + chr12 lengths (145 + 133 Mb), hg38-shaped (config C1).
 //   small  3 contigs (60, 45, 30 kb) shaped like hg38 (fixtures / unit tests).
 //   scale  multiplies every contig length (hg38 at scale 0.01 = 31 Mb).
 //
@@ -86,6 +87,14 @@ static int get_preset(const char* name, double scale, preset_t* p) {
     if (strcmp(name, "ecoli") == 0) {
         p->n = 1; p->lens[0] = (int64_t)(4641652 * scale); snprintf(p->names[0], 16, "NC_000913.3");
         p->gc = 0.508; p->is_frac = 0.01;
+        return 0;
+    }
+    if (strcmp(name, "chr8chr12") == 0) {   // config C1: hg38 chr8 + chr12 lengths
+        p->n = 2;
+        p->lens[0] = (int64_t)(HG38_LENS[7] * scale); p->lens[1] = (int64_t)(HG38_LENS[11] * scale);
+        snprintf(p->names[0], 16, "chr8"); snprintf(p->names[1], 16, "chr12");
+        p->gc = 0.41; p->alu_frac = 0.10; p->l1_frac = 0.17; p->sat_frac = 0.03; p->sd_frac = 0.05;
+        p->telomere_n = 10000; p->gap_n = 50000;
         return 0;
     }
     if (strcmp(name, "small") == 0) {
