@@ -84,6 +84,8 @@ def parse(argv=None):
     p.add_argument("--no-parity", action="store_true", help="skip the oracle parity check as well")
     p.add_argument("--host-index", action="store_true", help="build the index on the host instead of the GPU")
     p.add_argument("--resident-steps", type=int, default=3, help="extra: steps re-mapping reads already in HBM")
+    p.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                   help="context knob for A/B runs (include/mm2g.h MM2G_KNOB_*), e.g. sort_prof=1")
     p.add_argument("--streams", type=int, default=2,
                    help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index")
     return p.parse_args(argv)
@@ -285,6 +287,9 @@ def main():
     pack_thr = args.pack_threads or max(1, min(8, thr // S))
     for d in devs:
         d.set_knob("host_threads", pack_thr)
+        for kv in args.knob:
+            k, v = kv.split("=", 1)
+            d.set_knob(k, int(v))
     t0 = time.time()
     devs[0].upload_index(idx, 10)
     t_up = time.time() - t0

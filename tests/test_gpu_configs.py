@@ -5,7 +5,7 @@ inputs) against the CPU oracle.
       chr8/chr12-shaped pair and one 600 bp read, vs the oracle CLI
   C2  E. coli-shaped 4.64 Mb + 1,000 x 10 kb: every read vs the oracle
   C3  the full 3.09 Gb hg38-shaped index + 300 x 10 kb reads vs the oracle
-  C5  the same index + 20 x 100 kb reads: reads above 65,535 anchors (the
+  C5  the same index + 24 x 100 kb reads (+ 8 chimeras): reads above 65,535 anchors (the
       whole-read radix sort) and rescue segments beyond LDS (the HBM variant
       of k_chain_giant) vs the oracle's PAF, per-read outcome and DP arrays
 C4 is C3's workload sharded over 8 GPUs; its per-GPU path is C3's.
@@ -20,7 +20,7 @@ import pytest
 import minimap2_rs_amd as M
 from oracle import oracle as O
 from tools import simdata
-from tests.gpu_common import _singleton_keep, assert_records
+from tests.gpu_common import _singleton_keep, assert_records, knobs
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -125,19 +125,25 @@ def test_c3_hg38_300_x_10kb(hg38, tmp_path):
         assert np.array_equal(got[r], want), r
 
 
-def test_c5_hg38_20_x_100kb(hg38, tmp_path):
-    """C5: 20 x 100 kb reads (seed 5): reads with > 65,535 anchors (whole-read
-    radix sort) and rescue segments of thousands of anchors (k_chain_giant,
-    LDS and HBM variants).  PAF and per-read outcome equal the oracle's; for
-    rescued reads the production DP arrays (rescue pass, giant kernels on)
-    equal the oracle's chain_dp_all at bw_long on the same anchors."""
+def test_c5_hg38_100kb(hg38, tmp_path):
+    """C5: 24 x 100 kb reads (seed 5) plus 8 chimeras of two 50 kb halves
+    (rescued: their chains cover half the read): reads with > 65,535 anchors
+    (whole-read radix sort) and rescue segments of thousands of anchors
+    (k_chain_giant).  PAF and per-read outcome equal the oracle's, by default
+    and with every rescue segment over 64 anchors sent to the HBM-scratch
+    variant (k_chain_giant<true>); for rescued reads the production DP arrays
+    of the rescue pass equal the oracle's chain_dp_all at bw_long on the same
+    anchors."""
     names, lens, gbuf, oi, idx, mid, dev = hg38
-    seqs, rn = _reads(gbuf, lens, 20, 100000, 5)
+    seqs, rn = _reads(gbuf, lens, 24, 100000, 5)
+    for i in range(8):
+        a, b = seqs[i], seqs[8 + i]
+        seqs.append(a[:50000] + b[50000:])
+        rn.append(f"chim{i}")
     res, rec = _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5")
     assert rec[:, 1].max() > 65535
     rescued = [r for r in range(len(seqs)) if res[r].flags & 2]
-    assert rescued
-    big = 0
+    assert len(rescued) >= 4
     for r in rescued:
         want, _ = oi.anchors(seqs[r], 10, 15, mid)
         want = want[_singleton_keep(want)]
@@ -147,5 +153,12 @@ def test_c5_hg38_20_x_100kb(hg38, tmp_path):
         gf, gpp = dev.debug_dp(r)
         n = len(want)
         assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
-        big += int(n > 5000)
-    assert big > 0
+    with knobs(dev, giant_lcap=64):
+        res2, _ = _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5hbm")
+        for r in rescued:
+            want, _ = oi.anchors(seqs[r], 10, 15, mid)
+            want = want[_singleton_keep(want)]
+            f, pp, _, _, _ = O.chain_dp(want, 15, bw=20000)
+            gf, gpp = dev.debug_dp(r)
+            n = len(want)
+            assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
