@@ -392,6 +392,9 @@ int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
     std::vector<uint64_t> keys, pos; std::vector<uint32_t> offs, ns;
     H.flatten(keys, offs, ns, pos);
     if (pos.size() >= (1ULL << 32)) return set_err(MM2G_E_UNSUP, "more than 2^32 index positions");
+    if (H.n_seq >= IX_INLINE) return set_err(MM2G_E_UNSUP, "2^31 or more reference sequences");
+    for (size_t t = 0; t < keys.size(); ++t)          // Singles: the position inline (IxEntry)
+        if (ns[t] == 1) { const uint64_t p = pos[offs[t]]; offs[t] = (uint32_t)p; ns[t] = IX_INLINE | (uint32_t)(p >> 32); }
     const uint64_t nk = keys.size();
     uint32_t l2 = 1;
     while ((1ULL << l2) < 2 * std::max<uint64_t>(nk, 1)) ++l2;     // load factor <= 0.5
@@ -909,6 +912,8 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     }
     uint64_t *keys, *ktmp;
     ENSURE(c->keys, uint64_t, A_cap, keys); ENSURE(c->keys_tmp, uint64_t, A_cap, ktmp);
+    int32_t* fb;
+    ENSURE(c->fbuf, int32_t, A_cap, fb);    // the sort's per-key tags live here before the DP needs it
     sa.keys = keys; sa.cap_keys = c->keys.cap / 8;
     {
         ProfScope ps(c, "seed_write");
@@ -925,6 +930,8 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
                 filt ? c->dix->cells : 0u, cnt2, smax, (uint32_t)std::min<int64_t>(K[MM2G_KNOB_SORT_SMALL], 4096), nullptr, 0u,
                 (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_SEG_SMALL], SEG_THREAD)), nullptr};
     so.abort = st32;
+    so.meta = (uint32_t*)fb;
+    so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     uint64_t* sprof = nullptr;
     if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 64)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 64, c->stream)); so.prof = sprof; }
     {

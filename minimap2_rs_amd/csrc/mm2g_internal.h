@@ -60,11 +60,16 @@ struct ChainKParams {
 };
 
 // Device index layout: open-addressed table of distinct minimizer hashes.
+// A Single (one occurrence) keeps its position in the entry itself, so the
+// anchor pass needs no gather for it: n = IX_INLINE | (pos >> 32), off = the
+// low 32 bits of pos (pos = rid<<32 | rpos<<1 | strand, Index p/h values).
 struct IxEntry {
     uint64_t key;   // minimizer hash (key_span >> 8); U64MAX = empty
-    uint32_t off;   // first position in ix_pos
-    uint32_t n;     // occurrences (1 = Single)
+    uint32_t off;   // first position in ix_pos (Multi), low word of the position (Single)
+    uint32_t n;     // occurrences (Multi), IX_INLINE | high word of the position (Single)
 };
+constexpr uint32_t IX_INLINE = 0x80000000u;
+__host__ __device__ inline uint32_t ix_count(uint32_t n) { return (n & IX_INLINE) ? 1u : n; }
 
 __host__ __device__ inline uint32_t ix_slot(uint64_t h, uint32_t log2cap) {
     return (uint32_t)((h * 0x9E3779B97F4A7C15ULL) >> (64 - log2cap));
@@ -149,9 +154,9 @@ struct SortArgs {
     uint64_t* smax;         // per read: 1 + largest dropped (singleton) key, 0 = none
     uint32_t small_max;     // reads with more anchors go to k_sort_read (LDS bitonic below)
     uint64_t* prof;         // MM2G_SORT_PROF: per read 8 wall-clock stamps of k_sort_read's phases (else null)
-    uint32_t lds_words;     // dynamic LDS of k_sort_read (set by launch_sort_read)
+    uint32_t lds_words;     // dynamic LDS of k_sort_read: requested (0 = SORT_LDS), set by launch_sort_read
     uint32_t seg_small;     // cell segments up to this length (<= 1024) are ranked one thread per anchor
-    uint32_t* meta;         // per anchor scratch (the DP's f buffer): kept-cell rank of each scattered key
+    uint32_t* meta;         // per anchor scratch (the DP's f buffer): u16 kept-cell rank of each key (k_sort_read)
     const uint32_t* abort = nullptr;
 };
 struct ChainArgs {

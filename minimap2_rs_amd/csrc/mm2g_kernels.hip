@@ -750,10 +750,11 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
                     ++kn;
                 }
                 const uint32_t i = b0 + (uint32_t)u * 64 + lane;
+                // mz_n: the anchor count, or IX_INLINE | position high word for a Single
                 uint32_t nn = n[u];
-                if (nn > 1 && (int64_t)nn > (int64_t)a.mid_occ) nn = 0;   // Multi with len > mid_occ: skip
+                if (!(nn & IX_INLINE) && nn > 1 && (int64_t)nn > (int64_t)a.mid_occ) nn = 0;   // Multi with len > mid_occ: skip
                 if (i < m) { a.mz_n[mb + i] = nn; a.mz_poff[mb + i] = off[u]; }
-                acc += nn;
+                acc += ix_count(nn);
             }
         }
         acc = wave_sum(acc);
@@ -779,7 +780,7 @@ DEVI uint64_t pack_anchor(uint64_t rr, uint32_t my, int32_t qlen, int span, cons
 
 __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
-    __shared__ uint32_t s_inc[4][64], s_poff[4][64], s_y[4][64];
+    __shared__ uint32_t s_inc[4][64], s_poff[4][64], s_y[4][64], s_hi[4][64];
     const int lane = lane_id(), wv = wave_id();
     const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
     constexpr int U = 8;   // output batches whose position gathers are in flight together
@@ -800,12 +801,14 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
         for (uint32_t c0 = cb * 64; c0 < cend; c0 += 64) {
             const uint32_t i = c0 + lane;
             const bool vi = i < m;
-            const uint32_t n = vi ? a.mz_n[CK(mb + i, a.cap_mz)] : 0;
+            const uint32_t nraw = vi ? a.mz_n[CK(mb + i, a.cap_mz)] : 0;
             const uint32_t po = vi ? a.mz_poff[CK(mb + i, a.cap_mz)] : 0;
             const uint32_t yy = vi ? a.mz_y[CK(mb + i, a.cap_mz)] : 0;
+            const uint32_t n = ix_count(nraw);
             uint32_t tot;
             const uint32_t ex = wave_excl_sum(n, tot);
             s_inc[wv][lane] = ex + n; s_poff[wv][lane] = po; s_y[wv][lane] = yy;
+            s_hi[wv][lane] = nraw;
             wave_lds_sync();
             for (uint32_t tb = 0; tb < tot; tb += 64 * U) {
                 uint64_t rr[U];
@@ -822,7 +825,9 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
                             if (s_inc[wv][lo + step - 1] <= t) lo += step;
                         const uint32_t exo = lo ? s_inc[wv][lo - 1] : 0;
                         own[u] = lo;
-                        rr[u] = a.ix_pos[CK((uint64_t)s_poff[wv][lo] + (t - exo), a.cap_pos)];
+                        const uint32_t hi = s_hi[wv][lo];
+                        if (hi & IX_INLINE) rr[u] = ((uint64_t)(hi & ~IX_INLINE) << 32) | s_poff[wv][lo];   // Single: no gather
+                        else rr[u] = a.ix_pos[CK((uint64_t)s_poff[wv][lo] + (t - exo), a.cap_pos)];
                     }
                 }
 #pragma unroll
@@ -913,6 +918,9 @@ constexpr uint32_t SEG_RANK = 2048;      // up to this: block-wide rank count; b
 constexpr int BIG_MAX = 128;             // larger segments listed per read (more: radix over the read)
 constexpr int GOFF_LDS = 256;            // group offsets staged in LDS when 2 * n_seq + 2 fits
 constexpr int SORT_LDS = 157 * 1024;     // dynamic LDS of k_sort_read (one workgroup per CU; 2.4 KB static)
+#ifndef SORT_U
+#define SORT_U 8                          // keys per thread in flight in the block-wide passes over a read
+#endif
 
 // 8 independent loads per thread, then fn(i, x) for each (i < n): hides HBM
 // latency in the block-wide passes of k_sort_read
@@ -953,6 +961,23 @@ DEVI uint32_t count_below(const uint64_t* S, uint32_t lo, uint32_t hi, uint64_t 
         if (y < x || (incl && y == x)) { b += h + 1; n -= h + 1; } else n = h;
     }
     return b - lo;
+}
+
+// as block_pass8 over keys and their u16 tags (loaded together): fn(i, x, m)
+template <int U = 8, typename F>
+DEVI void block_pass_km(const uint64_t* src, const uint16_t* tag, uint32_t n, F fn) {
+    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * U) {
+        uint64_t x[U];
+        uint16_t m[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x;
+            x[u] = i < n ? src[i] : 0;
+            m[u] = i < n ? tag[i] : (uint16_t)0xffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; if (i < n) fn(i, x[u], m[u]); }
+    }
 }
 
 // as block_pass8, but fn(i, x, valid) runs on every lane (block-uniform trip
@@ -1132,6 +1157,9 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
     uint64_t* O = a.tmp + base;       // sorted output
     const bool filt = a.cells != 0;
     const uint32_t ng = 2u * a.n_seq + 2u;
+    // keys use gsh + group bits; the top 16 are free for a window rank when <= 48
+    const bool stash = gsh + (32u - (uint32_t)__builtin_clz(2u * a.n_seq | 1u)) <= 48u;
+    const uint64_t kmask = stash ? ((1ULL << 48) - 1) : U64MAX;
     const uint32_t* goff = a.goff;
     if (filt && ng <= (uint32_t)GOFF_LDS) {
         for (uint32_t i = tid; i < ng; i += 1024) s_goff[i] = a.goff[i];
@@ -1152,11 +1180,9 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
         // ---- P1: seen / seen-twice bitmaps
         for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
         __syncthreads();
-        block_pass8<8>(K, A0, [&](uint32_t, uint64_t x) {
+        block_pass8<SORT_U>(K, A0, [&](uint32_t, uint64_t x) {
             const uint32_t c = cell_of(x), w = c >> 5, bit = 1u << (c & 31);
-            bool seen = (B1[w] & bit) != 0;
-            if (!seen) seen = (atomicOr(&B1[w], bit) & bit) != 0;
-            if (seen && !(B2[w] & bit)) atomicOr(&B2[w], bit);
+            if (atomicOr(&B1[w], bit) & bit) atomicOr(&B2[w], bit);   // seen before: seen twice
         });
         __syncthreads();
         // ---- KC (in place of B2) and the word prefix of its popcounts (in place of B1)
@@ -1188,13 +1214,17 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                 return B1[w] + (uint32_t)__popc(kw & ((1u << b) - 1u));
             };
             auto c16 = [&](uint32_t rk) -> uint32_t { return (C[rk >> 1] >> ((rk & 1) << 4)) & 0xffffu; };
-            // ---- P2: counts per kept cell; the largest dropped key
+            // ---- P2: counts per kept cell; the largest dropped key.  Each key's
+            // kept-cell rank (0xffff = dropped) goes to the u16 tag array T16 in
+            // the DP's f buffer, so the window passes need no cell lookups.
             uint64_t smx = 0;
-            block_pass8<8>(K, A0, [&](uint32_t, uint64_t x) {
+            uint16_t* T16 = (uint16_t*)(a.meta + base);
+            block_pass8<SORT_U>(K, A0, [&](uint32_t i, uint64_t x) {
                 bool kept;
                 const uint32_t rk = rank_of(cell_of(x), kept);
                 if (kept) atomicAdd(&C[rk >> 1], 1u << ((rk & 1) << 4));
                 else smx = x + 1 > smx ? x + 1 : smx;
+                T16[i] = kept ? (uint16_t)rk : (uint16_t)0xffffu;
             });
             smx = block_max64(smx, red);
             // exclusive scan of the u16 counts, in place (offsets < A0 <= 65535)
@@ -1251,20 +1281,23 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                 }
                 const uint32_t nwin = ob - oa;
                 __syncthreads();
-                block_pass8<8>(K, A0, [&](uint32_t, uint64_t x) {
-                    bool kept;
-                    const uint32_t rk = rank_of(cell_of(x), kept);
-                    if (kept && rk >= ra && rk < rb) {
+                // window keys carry their rank in the top 16 bits when the key
+                // layout leaves them free: the rank rises with the key, so the
+                // order is unchanged, and segment lookups need no cell arithmetic
+                block_pass_km<SORT_U>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m) {
+                    const uint32_t rk = m;
+                    if (m != 0xffffu && rk >= ra && rk < rb) {
                         const uint32_t sh = (rk & 1) << 4;
                         const uint32_t pos = ((atomicAdd(&C[rk >> 1], 1u << sh) >> sh) & 0xffffu) - oa;
-                        S[pos] = x;
+                        S[pos] = stash ? (x | ((uint64_t)rk << 48)) : x;
                     }
                 });
                 __syncthreads();
                 // segment [s, e) of a key, window-relative (C holds end offsets for ranks < rb)
                 auto seg_of = [&](uint64_t x, uint32_t& s, uint32_t& e) {
-                    bool kept;
-                    const uint32_t rk = rank_of(cell_of(x), kept);
+                    uint32_t rk;
+                    if (stash) rk = (uint32_t)(x >> 48);
+                    else { bool kept; rk = rank_of(cell_of(x), kept); }
                     s = (rk ? c16(rk - 1) : 0u) - oa;
                     e = c16(rk) - oa;
                 };
@@ -1289,7 +1322,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                     seg_of(x, s, e);
                     const uint32_t L = e - s;
                     if (L > a.seg_small) {             // P4b; copied unsorted
-                        O[oa + i] = x;
+                        O[oa + i] = x & kmask;
                         if (i == s) {
                             const uint32_t slot = atomicAdd(&s_nbig, 1u);
                             if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s, oa + e);
@@ -1307,7 +1340,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                             rank += count_below(S, max(s, c << 6), min(e, (c << 6) + 64), x, c < co);
                         }
                     }
-                    O[oa + s + rank] = x;
+                    O[oa + s + rank] = x & kmask;
                 }
                 __syncthreads();
                 ra = rb;
@@ -2922,7 +2955,7 @@ __global__ __launch_bounds__(256) void k_mid_hist(const IxEntry* tab, uint64_t c
         const uint64_t t = b0 + threadIdx.x;
         bool one = false;
         if (t < cap && tab[t].key != U64MAX) {
-            const uint32_t n = tab[t].n;
+            const uint32_t n = ix_count(tab[t].n);
             one = n == 1;
             if (n < nbins) { if (!one) atomicAdd(&sh[n], 1u); }
             else if (ovf) { const uint32_t q = atomicAdd(ovf_n, 1u); if (q < ovf_cap) ovf[q] = n; }
@@ -2980,7 +3013,8 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
     else {
         // one workgroup per CU: 160 KiB LDS less the static arrays
         const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4, hb = (size_t)(RS_MAXP + 16) * RS_ND * 4;
-        size_t lds = std::max<size_t>({(size_t)SORT_LDS, bmb, hb});
+        size_t lds = std::max<size_t>({a.lds_words ? (size_t)a.lds_words * 4 : (size_t)SORT_LDS, bmb, hb});
+        lds = std::min<size_t>(lds, (size_t)SORT_LDS);
         SortArgs b = a;
         b.lds_words = (uint32_t)(lds / 4);
         hipLaunchKernelGGL(k_sort_read, dim3(a.n), dim3(1024), lds, st, b);
