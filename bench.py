@@ -11,10 +11,11 @@ written, exactly as SURVEY.md §8d times it:
   sketch -> query filter -> index lookup -> anchors -> sort -> chain DP
   (+rescue) -> epilogue -> per-read results to host -> PAF text.
 Every step maps a different batch (a pool of W+K batches is generated up
-front; the metric's 100k-read C3 set is 10 such batches).  `--streams S`
-contexts per GPU (own HIP stream and host thread each, one shared device
-index) pull (batch, share) units from a queue, so one context's host
-packing and PAF formatting overlap another's kernels.  Index build/upload and
+front; the metric's 100k-read C3 set is 10 such batches).  Each batch is
+cut into `--shares P` units (default 2); `--streams S` contexts per GPU
+(default 4; own HIP stream and host thread each, one shared device index)
+pull units from one queue, so the GPU always has queued units while other
+contexts pack reads or format PAF.  Index build/upload and
 mid_occ are outside the timed region.  The rate with reads already resident
 in HBM is reported in `extra`.
 
@@ -86,8 +87,10 @@ def parse(argv=None):
     p.add_argument("--resident-steps", type=int, default=3, help="extra: steps re-mapping reads already in HBM")
     p.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
                    help="context knob for A/B runs (include/mm2g.h MM2G_KNOB_*), e.g. sort_prof=1")
-    p.add_argument("--streams", type=int, default=2,
+    p.add_argument("--streams", type=int, default=4,
                    help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index")
+    p.add_argument("--shares", type=int, default=2,
+                   help="units each batch is cut into (0 = one per stream); contexts pull units from one queue")
     return p.parse_args(argv)
 
 
@@ -148,7 +151,7 @@ def kernel_sha() -> str:
 
 
 def bench_config_tag(args) -> str:
-    return f"reads={args.reads},read_len={args.read_len},streams={max(1, args.streams)},scale={args.scale},preset={args.preset}"
+    return f"reads={args.reads},read_len={args.read_len},streams={max(1, args.streams)},shares={args.shares},scale={args.scale},preset={args.preset}"
 
 
 def pmc_traffic(kernel: str, tag: str):
@@ -308,12 +311,13 @@ def main():
 
     opts = M.map_opts()
     ih = idx._h
-    cuts = share_cuts(args.reads, S)
+    P = args.shares if args.shares > 0 else S    # units per batch
+    cuts = share_cuts(args.reads, P)
     # per (batch, share) unit: names, result array, PAF buffer
     units = []
     for b in range(n_batches):
         rb, offs = batches[b]
-        for k in range(S):
+        for k in range(P):
             lo, hi = cuts[k], cuts[k + 1]
             nr = hi - lo
             sub = np.ascontiguousarray(offs[lo:hi + 1], dtype=np.uint64)     # absolute offsets into rb
@@ -343,7 +347,7 @@ def main():
     def run_steps(s0: int, s1: int):
         """Map the units of steps [s0, s1) (step s -> batch s mod n_batches) on
         the S contexts, each pulling the next unit from a shared queue."""
-        todo = [u for s in range(s0, s1) for u in units[(s % n_batches) * S:(s % n_batches + 1) * S]]
+        todo = [u for s in range(s0, s1) for u in units[(s % n_batches) * P:(s % n_batches + 1) * P]]
         nxt = [0]
         lock = threading.Lock()
         errs = []
@@ -382,7 +386,7 @@ def main():
             a0, c0 = prof.get(k, (0.0, 0))
             prof[k] = (a0 + ms, c0 + calls)
         d.prof_enable(False)
-    timed = [units[(s % n_batches) * S + k] for s in range(args.warmup, args.warmup + args.steps) for k in range(S)]
+    timed = [units[(s % n_batches) * P + k] for s in range(args.warmup, args.warmup + args.steps) for k in range(P)]
     cnt = {}
     for u in timed:
         for k, v in u["cnt"].items():
@@ -397,8 +401,8 @@ def main():
 
     # ---- extra: reads already resident in HBM (the round-1 headline) --------
     resident = None
-    if args.resident_steps > 0:
-        us = units[:S]
+    if args.resident_steps > 0 and P <= S:
+        us = units[:P]
         for d, u in zip(devs, us):
             rb = batches[u["b"]][0]
             L.check(lib.mm2g_batch_set_reads(d._h, rb.ctypes.data_as(C.c_void_p), u["offs"].ctypes.data_as(L._P64), u["n"]), "set_reads")
@@ -497,7 +501,7 @@ def main():
                             f"(nt4 pack + H2D + map + PAF in the timed region)",
                 "reads_per_gpu_step": args.reads, "read_len": args.read_len, "ref_bases": int(lens.sum()),
                 "distinct_batches": n_batches, "mid_occ": mid, "ranks": world,
-                "parallelism": f"reads sharded x{world} (index replicated), {S} streams per GPU",
+                "parallelism": f"reads sharded x{world} (index replicated), {S} streams per GPU, {P} units per batch",
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

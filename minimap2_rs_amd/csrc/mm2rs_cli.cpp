@@ -50,7 +50,7 @@ int main(int argc, char** argv) {
     std::string dump, out, preset, ropt;
     mm2g_map_opts mo; mm2g_map_opts_default(&mo);
     long long batch_bases = 256LL << 20;
-    int n_streams = 2;
+    int n_streams = 4;
     for (int i = 2; i < argc; ++i) {
         std::string a = argv[i];
         auto nxt = [&]() -> std::string { if (i + 1 >= argc) { usage(); exit(2); } return std::string(argv[++i]); };
