@@ -108,7 +108,7 @@ struct mm2g_ctx {
     DevBuf tab_off, tab_key, tab_cnt;
     DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
     DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist;
     DevBuf dstat;                          // batch status block (BS_* word, workspace needs, counters)
     DevBuf chain_rdoff;                    // mm2g_chain_batch: prefix sums of the caller's qlen
     uint64_t cap_tab = 0, cap_A = 0;       // filter-table entries / anchors the workspaces hold
@@ -177,36 +177,37 @@ struct ProfScope {
     }
 };
 
-// MM2G_SORT_PROF: phase times of k_sort_read (wall clock, 100 MHz) to stderr
+// MM2G_KNOB_SORT_PROF: phase times of k_sort_read (wall clock, 100 MHz) to stderr
 static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
-    std::vector<uint64_t> h((size_t)n * 8);
+    std::vector<uint64_t> h((size_t)n * 16);
     if (hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) return;
     (void)hipFree(d);
-    double ph[5] = {0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0;
+    double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0, nleg = 0;
     uint64_t t_lo = ~0ULL, t_hi = 0;
     uint32_t m = 0;
+    std::vector<uint32_t> q0, q2, q3;
     for (uint32_t r = 0; r < n; ++r) {
-        const uint64_t* p = &h[(size_t)r * 8];
-        if (!p[5]) continue;
+        const uint64_t* p = &h[(size_t)r * 16];
+        if (!p[11]) continue;
+        q3.push_back((uint32_t)p[13]);
         ++m;
-        for (int k = 0; k < 5; ++k) ph[k] += (double)(p[k + 1] - p[k]);
-        tot += (double)(p[5] - p[0]);
-        a0 += (double)p[6]; a2 += (double)(uint32_t)p[7]; np += (double)(p[7] >> 32);
-        t_lo = std::min(t_lo, p[0]); t_hi = std::max(t_hi, p[5]);
+        for (int k = 0; k < 8; ++k) ph[k] += (double)p[k];
+        tot += (double)(p[11] - p[10]);
+        a0 += (double)p[8]; a2 += (double)(uint32_t)p[9];
+        if ((p[9] >> 32) == 0xffffu) nleg += 1; else np += (double)(p[9] >> 32);
+        t_lo = std::min(t_lo, p[10]); t_hi = std::max(t_hi, p[11]);
+        q0.push_back((uint32_t)p[8]); q2.push_back((uint32_t)p[9]);
     }
     if (!m) return;
-    {   // quantiles of the per-read anchor counts before / after the singleton filter
-        std::vector<uint32_t> q0, q2;
-        for (uint32_t r = 0; r < n; ++r) { const uint64_t* p = &h[(size_t)r * 8]; if (p[5]) { q0.push_back((uint32_t)p[6]); q2.push_back((uint32_t)p[7]); } }
-        std::sort(q0.begin(), q0.end()); std::sort(q2.begin(), q2.end());
-        auto Q = [](const std::vector<uint32_t>& v, double f) { return v[std::min(v.size() - 1, (size_t)(f * v.size()))]; };
-        fprintf(stderr, "[sort_prof] A0 q10/50/90/99/max=%u/%u/%u/%u/%u  A q10/50/90/99/max=%u/%u/%u/%u/%u\n",
-                Q(q0, .1), Q(q0, .5), Q(q0, .9), Q(q0, .99), q0.back(), Q(q2, .1), Q(q2, .5), Q(q2, .9), Q(q2, .99), q2.back());
-    }
-    fprintf(stderr, "[sort_prof] reads=%u A0=%.0f A=%.0f nbig=%.2f us/read: p1-2=%.1f p3=%.1f p4a=%.1f p4b=%.1f tail=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
-            m, a0 / m, a2 / m, np / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
-            tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
+    std::sort(q0.begin(), q0.end()); std::sort(q2.begin(), q2.end()); std::sort(q3.begin(), q3.end());
+    auto Q = [](const std::vector<uint32_t>& v, double f) { return v[std::min(v.size() - 1, (size_t)(f * v.size()))]; };
+    fprintf(stderr, "[sort_prof] A0 q10/50/90/99/max=%u/%u/%u/%u/%u  A q10/50/90/99/max=%u/%u/%u/%u/%u  kept cells q10/50/90/99/max=%u/%u/%u/%u/%u\n",
+            Q(q0, .1), Q(q0, .5), Q(q0, .9), Q(q0, .99), q0.back(), Q(q2, .1), Q(q2, .5), Q(q2, .9), Q(q2, .99), q2.back(),
+            Q(q3, .1), Q(q3, .5), Q(q3, .9), Q(q3, .99), q3.back());
+    fprintf(stderr, "[sort_prof] reads=%u (whole-read radix %.0f) A0=%.0f A=%.0f nbig=%.2f windows=%.2f us/read: p1+kc=%.1f p2=%.1f gather=%.1f segs=%.1f chunk=%.1f rank=%.1f p4b/radix=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
+            m, nleg, a0 / m, a2 / m, np / m, ph[7] / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
+            ph[5] / m / 100, ph[6] / m / 100, tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
 }
 
 // MM2G_SKETCH_PROF: phase times of k_sketch summed over each read's tiles
@@ -922,8 +923,9 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     // 4. anchor sort (seeds.rs:58).  The singleton filter needs every max_dist_x
     //    of both DP passes within one 2^CELL_SHIFT cell (DESIGN.md "Anchor sort");
     //    it is off in debug mode (full anchor/DP arrays for the parity tests).
-    uint32_t* cnt2; uint64_t* smax;
+    uint32_t* cnt2; uint64_t* smax; uint32_t* rlist;
     ENSURE(c->cnt2, uint32_t, n, cnt2);
+    ENSURE(c->rlist, uint32_t, n + 1, rlist);
     ENSURE(c->smax, uint64_t, n, smax);
     const bool filt = !c->debug && !stop_after_sort && K[MM2G_KNOB_FILTER] && std::max(mdx0, mdx1) <= (1 << CELL_SHIFT);
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
@@ -931,9 +933,10 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
                 (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_SEG_SMALL], SEG_THREAD)), nullptr};
     so.abort = st32;
     so.meta = (uint32_t*)fb;
+    so.rlist = rlist; so.rcount = rlist + n;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     uint64_t* sprof = nullptr;
-    if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 64)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 64, c->stream)); so.prof = sprof; }
+    if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 128)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 128, c->stream)); so.prof = sprof; }
     {
         ProfScope ps(c, "sort_small");
         LCHK(launch_sort_read(0, so, c->stream));
@@ -941,6 +944,10 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     {
         ProfScope ps(c, "sort_large");
         LCHK(launch_sort_read(1, so, c->stream));
+    }
+    {
+        ProfScope ps(c, "sort_radix");
+        LCHK(launch_sort_read(2, so, c->stream));
     }
     if (sprof) dump_sort_prof(c, sprof, n);
     // the sorted anchors are in the tmp buffer: swap the roles for everything downstream

@@ -158,6 +158,8 @@ struct SortArgs {
     uint32_t seg_small;     // cell segments up to this length (<= 1024) are ranked one thread per anchor
     uint32_t* meta;         // per anchor scratch (the DP's f buffer): u16 kept-cell rank of each key (k_sort_read)
     const uint32_t* abort = nullptr;
+    uint32_t* rlist = nullptr;   // reads k_sort_read leaves to k_sort_radix ([n]), and their count (zeroed by k_sort_small)
+    uint32_t* rcount = nullptr;
 };
 struct ChainArgs {
     uint32_t n;

@@ -851,6 +851,7 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
 constexpr int SORT_SMALL = 4096;
 
 __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.rcount = 0;   // k_sort_read's list for k_sort_radix
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t s[SORT_SMALL];
     const uint32_t r = blockIdx.x;
@@ -952,6 +953,34 @@ DEVI void wave_bitonic64(uint64_t& x, uint32_t& p) {
     }
 }
 
+// bitonic sort of one 64-bit key per lane across the wave
+DEVI void wave_bitonic64_np(uint64_t& x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t yl = (uint32_t)__shfl_xor((int)(uint32_t)x, j, 64);
+            const uint32_t yh = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), j, 64);
+            const uint64_t y = ((uint64_t)yh << 32) | yl;
+            const bool up = (lane & k) == 0, low = (lane & j) == 0;
+            if ((low == up) ? (y < x) : (y > x)) x = y;
+        }
+    }
+}
+
+// number of keys in the sorted S[lo, hi) of 64-bit keys below x (or <= x when
+// incl), comparing only their low dwords S32[2 j] (keys that agree above them)
+DEVI uint32_t count_below_lo(const uint32_t* S32, uint32_t lo, uint32_t hi, uint32_t x, bool incl) {
+    uint32_t b = lo, n = hi - lo;
+    while (n) {
+        const uint32_t h = n >> 1;
+        const uint32_t y = S32[2 * (b + h)];
+        if (y < x || (incl && y == x)) { b += h + 1; n -= h + 1; } else n = h;
+    }
+    return b - lo;
+}
+
 // number of keys in the sorted S[lo, hi) below x (or <= x when incl)
 DEVI uint32_t count_below(const uint64_t* S, uint32_t lo, uint32_t hi, uint64_t x, bool incl) {
     uint32_t b = lo, n = hi - lo;
@@ -977,6 +1006,24 @@ DEVI void block_pass_km(const uint64_t* src, const uint16_t* tag, uint32_t n, F 
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; if (i < n) fn(i, x[u], m[u]); }
+    }
+}
+
+// as block_pass_km, but fn(i, x, m, valid) runs on every lane (block-uniform
+// trip count) so that fn may ballot / shuffle
+template <int U = 8, typename F>
+DEVI void block_pass_kmu(const uint64_t* src, const uint16_t* tag, uint32_t n, F fn) {
+    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * U) {
+        uint64_t x[U];
+        uint16_t m[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x;
+            x[u] = i < n ? src[i] : 0;
+            m[u] = i < n ? tag[i] : (uint16_t)0xffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; fn(i, x[u], m[u], i < n); }
     }
 }
 
@@ -1149,17 +1196,18 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
     if (base + A0 > a.cap_keys) { if (threadIdx.x == 0) CK(base + A0, a.cap_keys); return; }
 #endif
     const int tid = threadIdx.x, lane = lane_id();
-#define SORT_STAMP(ph) do { if (a.prof && tid == 0) a.prof[(uint64_t)r * 8 + (ph)] = wall_clock64(); } while (0)
-    SORT_STAMP(0);
+    // MM2G_KNOB_SORT_PROF: per-phase wall-clock sums of thread 0 (after barriers),
+    // accumulated in the read's 16 profile words (no registers held across the kernel)
+    uint64_t* const pq = a.prof ? a.prof + (uint64_t)r * 16 : nullptr;
+    if (pq && tid == 0) pq[10] = pq[12] = wall_clock64();
+#define SORT_PH(k) do { if (pq && tid == 0) { const uint64_t t_ = wall_clock64(); pq[k] += t_ - pq[12]; pq[12] = t_; } } while (0)
+#define SORT_END(nb, nk) do { if (pq && tid == 0) { pq[8] = A0; pq[9] = ((uint64_t)(nb) << 32) | (nk); pq[11] = wall_clock64(); } } while (0)
     const uint32_t qb = a.qb, gsh = a.qb + a.rb;
     const uint64_t rmask = (1ULL << a.rb) - 1;
     uint64_t* K = a.keys + base;      // unsorted anchors (seed_write); scratch once read for the last time
     uint64_t* O = a.tmp + base;       // sorted output
     const bool filt = a.cells != 0;
     const uint32_t ng = 2u * a.n_seq + 2u;
-    // keys use gsh + group bits; the top 16 are free for a window rank when <= 48
-    const bool stash = gsh + (32u - (uint32_t)__builtin_clz(2u * a.n_seq | 1u)) <= 48u;
-    const uint64_t kmask = stash ? ((1ULL << 48) - 1) : U64MAX;
     const uint32_t* goff = a.goff;
     if (filt && ng <= (uint32_t)GOFF_LDS) {
         for (uint32_t i = tid; i < ng; i += 1024) s_goff[i] = a.goff[i];
@@ -1175,8 +1223,10 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
     const uint32_t LW = a.lds_words;
     uint32_t* B1 = dyn;
     uint32_t* B2 = dyn + nw;
-    bool legacy = !filt || A0 > 65535u;
-    if (!legacy) {
+    // reads the cell path does not take are listed for k_sort_radix (whole-read radix)
+    auto defer = [&]() { if (tid == 0) { a.rlist[atomicAdd(a.rcount, 1u)] = r; SORT_END(0xffffu, 0u); } };
+    if (!filt || A0 > 65535u) { defer(); return; }
+    {
         // ---- P1: seen / seen-twice bitmaps
         for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
         __syncthreads();
@@ -1199,13 +1249,21 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
         uint32_t nkc;
         uint32_t run = block_excl_sum(loc, nkc, s_sc);      // its barriers end the B1 reads
         for (uint32_t w = wa; w < wb; ++w) { B1[w] = run; run += (uint32_t)__popc(B2[w]); }
+        SORT_PH(0);
+        if (pq && tid == 0) pq[13] = nkc;
         const uint32_t cw = (nkc + 1) >> 1;                  // u16 counts, two per word
-        const uint32_t wofs = (2 * nw + cw + 1) & ~1u;       // 8-byte aligned window area
-        const uint32_t W = wofs < LW ? (LW - wofs) >> 1 : 0u;   // keys per window
-        legacy = W < SEG_RANK;
-        if (!legacy) {
-            uint32_t* C = dyn + 2 * nw;
-            uint64_t* S = dyn64 + (wofs >> 1);
+        // C (u16 per kept cell) sits at the top of the LDS.  The bitmaps are dead
+        // after P2 (the tags and the window keys carry the ranks), so the windows
+        // use everything below C.  Window keys carry their kept-cell rank in the
+        // top 16 bits, which the key layout must leave free.
+        const uint32_t cofs = LW >= cw + 2 ? (LW - cw) & ~1u : 0u;
+        const uint32_t kbits = gsh + (32u - (uint32_t)__builtin_clz(2u * a.n_seq | 1u));
+        const uint32_t W = cofs >> 1;                        // keys per window
+        if (kbits > 48u || qb + CELL_SHIFT > 32u || cofs < 2 * nw || W < SEG_RANK) { defer(); return; }
+        {
+            constexpr uint64_t kmask = (1ULL << 48) - 1;
+            uint32_t* C = dyn + cofs;
+            uint64_t* S = dyn64;
             for (uint32_t i = tid; i < cw; i += 1024) C[i] = 0;
             __syncthreads();
             auto rank_of = [&](uint32_t c, bool& kept) -> uint32_t {
@@ -1216,7 +1274,8 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
             auto c16 = [&](uint32_t rk) -> uint32_t { return (C[rk >> 1] >> ((rk & 1) << 4)) & 0xffffu; };
             // ---- P2: counts per kept cell; the largest dropped key.  Each key's
             // kept-cell rank (0xffff = dropped) goes to the u16 tag array T16 in
-            // the DP's f buffer, so the window passes need no cell lookups.
+            // the DP's f buffer, so the window passes need no cell lookups (and
+            // the bitmaps can be overwritten by the first window).
             uint64_t smx = 0;
             uint16_t* T16 = (uint16_t*)(a.meta + base);
             block_pass8<SORT_U>(K, A0, [&](uint32_t i, uint64_t x) {
@@ -1241,7 +1300,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
             }
             if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
             __syncthreads();
-            SORT_STAMP(1);
+            SORT_PH(1);
             // ---- P3/P4: windows of whole kept cells (<= W keys), each gathered from K
             // into LDS by cell (C turns from start into end offsets as cells are
             // filled), chunk-sorted and ranked per cell segment into O.
@@ -1258,10 +1317,8 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                     __syncthreads();
                     if (tid == 0) s_kept = 0;
                     __syncthreads();
-                    block_pass_u<8>(K, A0, [&](uint32_t, uint64_t x, bool valid) {
-                        bool kept = false;
-                        const uint32_t rk = valid ? rank_of(cell_of(x), kept) : 0u;
-                        const bool mine = valid && kept && rk == ra;
+                    block_pass_kmu<8>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m, bool valid) {
+                        const bool mine = valid && (uint32_t)m == ra;
                         const uint64_t mb = ballot(mine);
                         uint32_t wb0 = 0;
                         if (lane == 0 && mb) wb0 = atomicAdd(&s_kept, (uint32_t)__popcll(mb));
@@ -1276,46 +1333,53 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                         if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa, ob);
                     }
                     __syncthreads();
+                    SORT_PH(2);
                     ra = ra + 1;
                     continue;
                 }
                 const uint32_t nwin = ob - oa;
                 __syncthreads();
-                // window keys carry their rank in the top 16 bits when the key
-                // layout leaves them free: the rank rises with the key, so the
-                // order is unchanged, and segment lookups need no cell arithmetic
+                // window keys carry their rank in the top 16 bits: the rank rises
+                // with the key, so the order is unchanged, and a key's segment is
+                // one shift away
                 block_pass_km<SORT_U>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m) {
                     const uint32_t rk = m;
                     if (m != 0xffffu && rk >= ra && rk < rb) {
                         const uint32_t sh = (rk & 1) << 4;
                         const uint32_t pos = ((atomicAdd(&C[rk >> 1], 1u << sh) >> sh) & 0xffffu) - oa;
-                        S[pos] = stash ? (x | ((uint64_t)rk << 48)) : x;
+                        S[pos] = x | ((uint64_t)rk << 48);
                     }
                 });
                 __syncthreads();
+                SORT_PH(2);
+                if (pq && tid == 0) pq[7] += 1;
                 // segment [s, e) of a key, window-relative (C holds end offsets for ranks < rb)
                 auto seg_of = [&](uint64_t x, uint32_t& s, uint32_t& e) {
-                    uint32_t rk;
-                    if (stash) rk = (uint32_t)(x >> 48);
-                    else { bool kept; rk = rank_of(cell_of(x), kept); }
+                    const uint32_t rk = (uint32_t)(x >> 48);
                     s = (rk ? c16(rk - 1) : 0u) - oa;
                     e = c16(rk) - oa;
                 };
                 // A: chunks holding a segment longer than SEG_TINY: one wave sorts 64 keys
                 const uint32_t nch = (nwin + 63) >> 6;
-                for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 16) {
-                    const uint32_t i = q * 64 + (uint32_t)lane;
-                    const bool valid = i < nwin;
-                    uint64_t x = valid ? S[i] : U64MAX;
-                    uint32_t s = 0, e = 0;
-                    if (valid) seg_of(x, s, e);
-                    if (!any(valid && e - s > SEG_TINY && e - s <= a.seg_small)) continue;
-                    uint32_t dummy = 0;
-                    wave_bitonic64(x, dummy);
-                    if (valid) S[i] = x;
+                for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 32) {   // two chunks at a time (q, q + 16)
+                    const uint32_t ia = q * 64 + (uint32_t)lane, ib = ia + 16 * 64;
+                    const bool va = ia < nwin, vb = ib < nwin;
+                    uint64_t xa = S[va ? ia : 0], xb = S[vb ? ib : 0];
+                    uint32_t sa, ea, sb, eb;
+                    seg_of(xa, sa, ea);
+                    seg_of(xb, sb, eb);
+                    xa = va ? xa : U64MAX; xb = vb ? xb : U64MAX;
+                    const bool na = any(va && ea - sa > SEG_TINY && ea - sa <= a.seg_small);
+                    const bool nb = any(vb && eb - sb > SEG_TINY && eb - sb <= a.seg_small);
+                    if (na) { wave_bitonic64_np(xa); if (va) S[ia] = xa; }
+                    if (nb) { wave_bitonic64_np(xb); if (vb) S[ib] = xb; }
                 }
                 __syncthreads();
-                // B: ranks inside the segments
+                SORT_PH(4);
+                // B: ranks inside the segments.  Keys of one segment share every bit
+                // above the cell-local lb <= 32 (rank, group, cell), so they compare
+                // by their low dwords.
+                const uint32_t* S32 = (const uint32_t*)S;
                 for (uint32_t i = tid; i < nwin; i += 1024) {
                     const uint64_t x = S[i];
                     uint32_t s, e;
@@ -1329,29 +1393,30 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                         }
                         continue;
                     }
+                    const uint32_t xl = (uint32_t)x;
                     uint32_t rank = 0;
                     if (L <= SEG_TINY) {
-                        for (uint32_t j = s; j < e; ++j) { const uint64_t y = S[j]; rank += (y < x || (y == x && j < i)) ? 1u : 0u; }
+                        for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
                     } else {
                         const uint32_t co = i >> 6;
                         rank = i - max(s, co << 6);
                         for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
                             if (c == co) continue;
-                            rank += count_below(S, max(s, c << 6), min(e, (c << 6) + 64), x, c < co);
+                            rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
                         }
                     }
                     O[oa + s + rank] = x & kmask;
                 }
                 __syncthreads();
+                SORT_PH(5);
                 ra = rb;
             }
-            SORT_STAMP(2);
-            SORT_STAMP(3);
             // ---- P4b: cells over seg_small, one at a time by the whole block (K is scratch now)
             const uint32_t nbig = s_nbig;
-            if (nbig > (uint32_t)BIG_MAX) {
-                radix_range(O, K, O, A, qb, dyn, red);
-            } else {
+            bool big_radix = nbig > (uint32_t)BIG_MAX;
+            for (uint32_t b = 0; b < nbig && !big_radix; ++b) big_radix = s_big[b].y - s_big[b].x > SEG_RANK;
+            if (big_radix) { defer(); return; }       // K is still intact: k_sort_radix redoes the read
+            {
                 for (uint32_t b = 0; b < nbig; ++b) {
                     const uint2 sg = s_big[b];
                     const uint32_t L = sg.y - sg.x;
@@ -1374,62 +1439,92 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                         __syncthreads();
                         if (i0 < L) O[sg.x + r0] = x0;
                         if (i1 < L) O[sg.x + r1] = x1;
-                    } else {
-                        radix_range(O + sg.x, K + sg.x, O + sg.x, L, qb, dyn, red);
                     }
                 }
             }
-            SORT_STAMP(4);
-            if (a.prof && tid == 0) { a.prof[(uint64_t)r * 8 + 5] = wall_clock64(); a.prof[(uint64_t)r * 8 + 6] = A0; a.prof[(uint64_t)r * 8 + 7] = ((uint64_t)nbig << 32) | A; }
+            SORT_PH(6);
+            SORT_END(nbig, A);
             return;
         }
-        __syncthreads();
     }
-    // ---- radix path over the whole read (with the bitmap singleton filter when cells exist)
-    uint64_t* src = K;
-    uint64_t* dst = O;
-    uint32_t A = A0;
-    uint64_t smx = 0;     // 1 + largest dropped key
-    if (filt) {
-        if (tid == 0) s_kept = 0;
-        for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
+#undef SORT_PH
+#undef SORT_END
+}
+
+// Whole-read LSD radix for the reads k_sort_read listed (A0 > 65535, no cell
+// table, a key layout the 32-bit windows cannot hold, too many kept cells for
+// the LDS, or cell segments beyond SEG_RANK), with the bitmap singleton filter
+// when cells exist.  One workgroup per listed read (grid-stride over the list).
+__global__ __launch_bounds__(1024) void k_sort_radix(SortArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;
+    __shared__ uint64_t red[32];
+    __shared__ uint32_t s_kept;
+    __shared__ uint32_t s_goff[GOFF_LDS];
+    extern __shared__ uint64_t dyn64[];
+    uint32_t* dyn = (uint32_t*)dyn64;
+    const int tid = threadIdx.x, lane = lane_id();
+    const uint32_t nlist = *a.rcount;
+    const uint32_t qb = a.qb, gsh = a.qb + a.rb;
+    const uint64_t rmask = (1ULL << a.rb) - 1;
+    const bool filt = a.cells != 0;
+    const uint32_t ng = 2u * a.n_seq + 2u;
+    const uint32_t* goff = a.goff;
+    if (filt && ng <= (uint32_t)GOFF_LDS) {
+        for (uint32_t i = tid; i < ng; i += 1024) s_goff[i] = a.goff[i];
+        goff = s_goff;
+    }
+    auto cell_of = [&](uint64_t x) -> uint32_t {
+        return goff[(uint32_t)(x >> gsh)] + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
+    };
+    const uint32_t nw = (a.cells + 31) >> 5;
+    uint32_t* B1 = dyn;
+    uint32_t* B2 = dyn + nw;
+    for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
+        const uint32_t r = a.rlist[li];
+        const uint64_t base = a.a_off[r];
+        const uint32_t A0 = (uint32_t)(a.a_off[r + 1] - base);
+        uint64_t* K = a.keys + base;
+        uint64_t* O = a.tmp + base;
+        uint64_t* src = K;
+        uint64_t* dst = O;
+        uint32_t A = A0;
+        uint64_t smx = 0;     // 1 + largest dropped key
         __syncthreads();
-        block_pass8<4>(K, A0, [&](uint32_t, uint64_t x) {
-            const uint32_t c = cell_of(x);
-            const uint32_t bit = 1u << (c & 31);
-            if (atomicOr(&B1[c >> 5], bit) & bit) atomicOr(&B2[c >> 5], bit);
-        });
-        __syncthreads();
-        // keep non-singletons (compacted into O, order irrelevant: sorted below)
-        block_pass_u<4>(K, A0, [&](uint32_t, uint64_t x, bool valid) {
-            bool keep = false;
-            if (valid) {
+        if (filt) {
+            if (tid == 0) s_kept = 0;
+            for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
+            __syncthreads();
+            block_pass8<4>(K, A0, [&](uint32_t, uint64_t x) {
                 const uint32_t c = cell_of(x);
-                const bool twice = (B2[c >> 5] >> (c & 31)) & 1u;
-                const bool left = (B1[(c - 1) >> 5] >> ((c - 1) & 31)) & 1u;
-                const bool right = (B1[(c + 1) >> 5] >> ((c + 1) & 31)) & 1u;
-                keep = twice || left || right;
-                if (!keep) smx = x + 1 > smx ? x + 1 : smx;
-            }
-            const uint64_t km = ballot(keep);
-            uint32_t wbase = 0;
-            if (lane == 0 && km) wbase = atomicAdd(&s_kept, (uint32_t)__popcll(km));
-            wbase = (uint32_t)__shfl((int)wbase, 0, 64);
-            if (keep) O[CK(wbase + (uint32_t)__popcll(km & lanemask_lt()), A0)] = x;
-        });
-        smx = block_max64(smx, red);
-        A = s_kept;
-        src = O; dst = K;
-        __syncthreads();
+                const uint32_t bit = 1u << (c & 31);
+                if (atomicOr(&B1[c >> 5], bit) & bit) atomicOr(&B2[c >> 5], bit);
+            });
+            __syncthreads();
+            // keep non-singletons (compacted into O, order irrelevant: sorted below)
+            block_pass_u<4>(K, A0, [&](uint32_t, uint64_t x, bool valid) {
+                bool keep = false;
+                if (valid) {
+                    const uint32_t c = cell_of(x);
+                    const bool twice = (B2[c >> 5] >> (c & 31)) & 1u;
+                    const bool left = (B1[(c - 1) >> 5] >> ((c - 1) & 31)) & 1u;
+                    const bool right = (B1[(c + 1) >> 5] >> ((c + 1) & 31)) & 1u;
+                    keep = twice || left || right;
+                    if (!keep) smx = x + 1 > smx ? x + 1 : smx;
+                }
+                const uint64_t km = ballot(keep);
+                uint32_t wbase = 0;
+                if (lane == 0 && km) wbase = atomicAdd(&s_kept, (uint32_t)__popcll(km));
+                wbase = (uint32_t)__shfl((int)wbase, 0, 64);
+                if (keep) O[CK(wbase + (uint32_t)__popcll(km & lanemask_lt()), A0)] = x;
+            });
+            smx = block_max64(smx, red);
+            A = s_kept;
+            src = O; dst = K;
+            __syncthreads();
+        }
+        if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
+        radix_range(src, dst, O, A, qb, dyn, red);
     }
-    if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
-    SORT_STAMP(1);
-    SORT_STAMP(2);
-    radix_range(src, dst, O, A, qb, dyn, red);
-    SORT_STAMP(3);
-    SORT_STAMP(4);
-    if (a.prof && tid == 0) { a.prof[(uint64_t)r * 8 + 5] = wall_clock64(); a.prof[(uint64_t)r * 8 + 6] = A0; a.prof[(uint64_t)r * 8 + 7] = (0xffffULL << 32) | A; }
-#undef SORT_STAMP
 }
 
 // ============================================================================
@@ -3009,15 +3104,19 @@ int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
 }
 int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
     if (a.n == 0) return 0;
+    const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4;
     if (stage == 0) hipLaunchKernelGGL(k_sort_small, dim3(a.n), dim3(256), 0, st, a);
-    else {
-        // one workgroup per CU: 160 KiB LDS less the static arrays
-        const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4, hb = (size_t)(RS_MAXP + 16) * RS_ND * 4;
-        size_t lds = std::max<size_t>({a.lds_words ? (size_t)a.lds_words * 4 : (size_t)SORT_LDS, bmb, hb});
+    else if (stage == 1) {
+        // the requested LDS (default SORT_LDS: one workgroup per CU), at least the two bitmaps
+        size_t lds = std::max<size_t>(a.lds_words ? (size_t)a.lds_words * 4 : (size_t)SORT_LDS, bmb);
         lds = std::min<size_t>(lds, (size_t)SORT_LDS);
         SortArgs b = a;
         b.lds_words = (uint32_t)(lds / 4);
         hipLaunchKernelGGL(k_sort_read, dim3(a.n), dim3(1024), lds, st, b);
+    } else {
+        const size_t hb = (size_t)(RS_MAXP + 16) * RS_ND * 4;
+        const size_t lds = std::min<size_t>(std::max<size_t>(bmb, hb), (size_t)SORT_LDS);
+        hipLaunchKernelGGL(k_sort_radix, dim3(std::min<uint32_t>(a.n, 512)), dim3(1024), lds, st, a);
     }
     LAUNCH_CHECK();
     return 0;
