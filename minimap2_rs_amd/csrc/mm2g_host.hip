@@ -937,6 +937,8 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     uint64_t* sprof = nullptr;
     if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 128)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 128, c->stream)); so.prof = sprof; }
+    const int64_t stop_at = K[MM2G_KNOB_STOP_AT];   // measurement only: later stages skipped, results invalid
+    if (stop_at != 1) {
     {
         ProfScope ps(c, "sort_small");
         LCHK(launch_sort_read(0, so, c->stream));
@@ -953,12 +955,13 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     // the sorted anchors are in the tmp buffer: swap the roles for everything downstream
     std::swap(c->keys.p, c->keys_tmp.p); std::swap(c->keys.cap, c->keys_tmp.cap);
     std::swap(keys, ktmp);
-    if (!stop_after_sort) {
+    }
+    if (!stop_after_sort && stop_at != 1 && stop_at != 2) {
         // 5. chain DP + fallback + rescue
         ChainKParams P{};
         P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
         P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
-        if (int e = run_chain(c, n, c->d_rd_off, P, 0.01f * 0.8f * (float)o->k, 2, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
+        if (int e = run_chain(c, n, c->d_rd_off, P, 0.01f * 0.8f * (float)o->k, stop_at == 3 ? 1 : 2, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
                               a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug))
             return e;
         // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
@@ -973,7 +976,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
                   out, c->keys.cap / 8, D.y.cap / 4};
         da.abort = st32;
         ProfScope ps(c, "dv");
-        LCHK(launch_dv(da, c->stream));
+        if (stop_at != 4) LCHK(launch_dv(da, c->stream));
     }
     LCHK(launch_batch_sums(n, mz_cnt, cnt2, st, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_out, out, (size_t)n * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
