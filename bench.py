@@ -465,6 +465,34 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
         "avg_launch_ms": round(avg_s * 1e3, 4), "alg_bytes_per_launch": int(bytes_per_launch),
     }
+    # The same kernel on a quiet GPU: one context maps one batch's units one
+    # after another (after the timed region), so its launches share the GPU with
+    # nothing; the timed region's launches overlap the other contexts' kernels
+    # and their durations include that sharing.
+    iso = None
+    if rank == 0:
+        d0 = devs[0]
+        us0 = units[:P]
+        d0.prof_reset()
+        d0.prof_enable(True)
+        a_iso = 0
+        for u in us0:
+            rb = batches[u["b"]][0]
+            L.check(lib.mm2g_batch_set_reads(d0._h, rb.ctypes.data_as(C.c_void_p), u["offs"].ctypes.data_as(L._P64), u["n"]), "set_reads")
+            L.check(lib.mm2g_batch_map(d0._h, C.byref(opts)), "batch_map")
+            L.check(lib.mm2g_batch_results(d0._h, u["res"], u["n"]), "batch_results")
+            na_u = np.frombuffer(u["res"], dtype=RES_DTYPE, count=u["n"])["n_anchors"].astype(np.int64)
+            a_iso += int(na_u[na_u > SORT_SMALL].sum()) if dom == "sort_large" else 0
+        pi = d0.prof()
+        d0.prof_enable(False)
+        if dom in pi and pi[dom][1] > 0:
+            i_ms, i_calls = pi[dom]
+            i_avg = i_ms / 1e3 / i_calls
+            i_bytes = (16 * a_iso / i_calls) if dom == "sort_large" else bytes_per_launch
+            i_ach = i_bytes / i_avg / 1e9
+            iso = {"kernel": d_sym, "avg_launch_ms": round(i_avg * 1e3, 4), "alg_bytes_per_launch": int(i_bytes),
+                   "achieved": round(i_ach, 3), "frac": round(i_ach / HBM_PEAK_GBS, 6),
+                   "note": "one context, one batch's units mapped back to back after the timed region (no other kernels on the GPU)"}
     # whole-path algorithmic bytes (SURVEY.md §8d B(read) summed) over the step time
     B_path = (L_tot + 3) // 4 + 16 * mk + 48 * A + 24 * Ar
     path_gbs = B_path / elapsed / 1e9 if world == 1 else None
@@ -510,6 +538,7 @@ def main():
                 "per_kernel": per_kernel,
                 "counters_per_step": {k: v / args.steps for k, v in cnt.items()},
                 "resident_in_hbm": resident,
+                "roofline_isolated": iso,
                 "path_alg_GBps": round(path_gbs, 3) if path_gbs else None,
                 "path_frac_of_8TBps": round(path_gbs / HBM_PEAK_GBS, 6) if path_gbs else None,
                 "dp_pairs_per_s": dp_pairs_s,

@@ -15,8 +15,21 @@ from __future__ import annotations
 
 import argparse
 import csv
+import hashlib
 import json
+import os
 from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernel_sha() -> str:
+    """Same hash as bench.py kernel_sha(): the kernel sources the counters were taken on."""
+    h = hashlib.sha256()
+    for f in ("mm2g_kernels.hip", "mm2g_internal.h"):
+        with open(os.path.join(ROOT, "minimap2_rs_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def per_kernel(path: str, counter: str):
@@ -42,7 +55,7 @@ def main():
     w = per_kernel(a.write_csv, "WRITE_SIZE")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs, --kernel-trace)",
            "correction": "hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE = half of wide-read bytes)",
-           "command": a.cmd, "bench_config": a.config, "kernels": {}}
+           "command": a.cmd, "bench_config": a.config, "kernels_sha": kernel_sha(), "kernels": {}}
     for k in sorted(set(f) | set(w)):
         fb, fn = f.get(k, (0.0, 0))
         wb, wn = w.get(k, (0.0, 0))
