@@ -336,6 +336,10 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                 }
             }
             SK_PT(1);
+            // k <= 16: the k-mer registers fit 32 bits (2k <= 32)
+            using KT = typename std::conditional<K32, uint32_t, uint64_t>::type;
+            KT kf2 = (KT)kf, kr2 = (KT)kr;
+            const KT kmask = (KT)mask;
             bool rs = false; int32_t lc = 0;
 #pragma unroll
             for (int t = 0; t < SK_CH; ++t) {
@@ -345,11 +349,11 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                     const uint32_t c = (code16 >> (2 * (7 - t))) & 3u;
                     uint64_t x = U64MAX; uint16_t fl = 0, z = 0;
                     if ((valid8 >> t) & 1u) {
-                        kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1);
+                        kf2 = ((kf2 << 2) | (KT)c) & kmask; kr2 = (kr2 >> 2) | ((KT)(3 ^ c) << shift1);
                         fl = 1;
-                        if (kf != kr) {
-                            z = kf < kr ? 0 : 1;
-                            const uint64_t km = z ? kr : kf;
+                        if (kf2 != kr2) {
+                            z = kf2 < kr2 ? 0 : 1;
+                            const uint64_t km = z ? kr2 : kf2;
                             uint64_t h;
                             if (K32) h = hash64d<uint32_t>((uint32_t)km, (uint32_t)mask);
                             else h = hash64d<uint64_t>(km, mask);
