@@ -2236,10 +2236,17 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 // is the plain running maximum in visiting order: the largest sv,
                 // first visited (largest j) among equal ones.  No prefix scans, no
                 // marks.  Tried while it keeps succeeding (and every 16th anchor).
+                // Chains (many mark sources): when the first window's maximum is
+                // visited within the first max_skip visits (no break can come
+                // before it) and more than max_skip marked visits follow it inside
+                // that window (none of them is a new maximum, so n_skip only climbs),
+                // the reference breaks inside the window after the maximum: the
+                // result is that maximum, and deeper j are never visited.
                 bool done = false;
                 if (a.lazy && (try_simple || i >= next_try)) {
                     int32_t bv = INT_MIN, bj = -1;
                     uint32_t nmk = 0;
+                    bool cut = false;
                     for (int32_t jtop = i - 1; jtop >= lo && nmk <= (uint32_t)P.max_skip; jtop -= 64) {
                         const int32_t j = jtop - lane;
                         const bool inr = j >= lo;
@@ -2262,14 +2269,29 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                         ok = ok && dd <= bw;
                         const int32_t dg = dr < dq ? dr : dq;
                         const int32_t sv = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0] + fj;
-                        nmk += (uint32_t)__popcll(ballot(ok && ppj >= lo));
+                        const bool mk = ok && ppj >= lo;
+                        nmk += (uint32_t)__popcll(ballot(mk));
                         const int32_t v = ok ? sv : INT_MIN;
                         const int32_t m = rdl(scan_max(v), 63);
                         if (m > bv) { bv = m; bj = jtop - ctz64(ballot(v == m)); }
                         cpairs += (uint64_t)__popcll(ballot(inr));
                         ++n_steps;
+                        if (jtop == i - 1 && nmk > (uint32_t)P.max_skip && bv > span && i - 1 - bj <= P.max_skip) {
+                            // marked lanes of this window (t[pprev[j]] = i from earlier lanes)
+                            const int32_t tb = jtop - ppj;
+                            const bool mk_in = mk && tb < 64;
+                            const uint64_t mkM = ballot(mk_in);
+                            uint64_t M = 0;
+                            if (ballot(mk_in && tb != lane + 1) == 0) M = mkM << 1;
+                            else {
+                                const uint64_t tbit = mk_in ? (1ULL << (tb & 63)) : 0ULL;
+                                M = ((uint64_t)wave_or32((uint32_t)(tbit >> 32)) << 32) | wave_or32((uint32_t)tbit);
+                            }
+                            const uint64_t after = ~0ULL << (i - bj);          // lanes after the maximum's
+                            cut = (uint32_t)__popcll(ballot(ok) & M & after) > (uint32_t)P.max_skip;
+                        }
                     }
-                    done = nmk <= (uint32_t)P.max_skip;
+                    done = nmk <= (uint32_t)P.max_skip || cut;
                     if (done && bv > span) { max_f = bv; max_j = bj; }
                     try_simple = done;
                     if (done) backoff = 16;
