@@ -256,7 +256,8 @@ enum {
     MM2G_KNOB_GIANT_GMAX = 7,    /* anchors per workgroup slice of the HBM giant variant; 0 = off [65536]     */
     MM2G_KNOB_GIANT_GBLOCKS = 8, /* workgroups of the HBM giant variant [256]                                 */
     MM2G_KNOB_FILTER = 9,        /* the sort's singleton filter [1]                                           */
-    MM2G_KNOB_LAZY = 10,         /* k_chain_long skips windows that cannot beat max_f [1]                     */
+    MM2G_KNOB_LAZY = 10,         /* k_chain_long skips windows that cannot beat max_f, and its simple paths;
+                                    2: also in debug mode (exact f/pprev either way; tests) [1]               */
     MM2G_KNOB_PRUNE = 11,        /* pass-0 segment pruning by the best-f lower bound [1]                      */
     MM2G_KNOB_GIANT = 12,        /* the giant-segment kernels [1]                                             */
     MM2G_KNOB_SKETCH_PROF = 13,  /* phase profile of k_sketch to stderr [0]                                   */

@@ -722,7 +722,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     ENSURE(c->mseg, uint4, mcap2, mseg);
     LCHK(launch_read_order(n, a_cnt, order, c->stream));
     const int64_t* K = c->knob;
-    const bool lazy = !full && K[MM2G_KNOB_LAZY];
+    const bool lazy = (!full && K[MM2G_KNOB_LAZY]) || K[MM2G_KNOB_LAZY] == 2;   // 2: also with full DP arrays (tests)
     ChainArgs ca{n, rd_off, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P0, c->kl, out, work,
                  std::min(c->keys.cap, c->fbuf.cap / 4 * 8) / 8, nullptr, order, A_cap, std::min<int32_t>((int32_t)n, 4 * 256), tmark,
                  lseg, lseg_n, lcap, lseg_order, rbest, cnt2, smax, mseg, lseg_n + 2, lseg_n + 3, mcap2, nullptr, 0u,

@@ -116,6 +116,38 @@ def test_pipeline_parity(dev, small_world, tmp_path):
     assert _map_nodebug(dev, rnames, rseqs)[0] == got          # production path (singleton filter on)
 
 
+@pytest.mark.parametrize("mid_occ", [None, 20, 5000])
+def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ):
+    """The production DP shortcuts keep every f/pprev exact: k_chain_long's
+    simple paths (no mark source can break the loop; a chain's maximum visited
+    early with a break proven inside the first window) and lazy windows, and
+    the giant-segment kernels, here run with the full DP arrays kept (debug
+    mode, lazy=2), equal the oracle's chain_dp_all for every read."""
+    world = small_world if mid_occ is None else dense_world
+    ref, reads, rnames, rseqs = world
+    oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+    idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+    mid = max(idx.calc_mid_occ(2e-4), 10) if mid_occ is None else mid_occ
+    dev.upload_index(idx, mid)
+    with knobs(dev, lazy=2, giant_min=64):
+        dev.set_debug(True)
+        dev.set_reads(rseqs)
+        res = dev.map(M.map_opts())
+        n = 0
+        for r, q in enumerate(rseqs):
+            want_a, _ = oi.anchors(q, 10, 15, mid)
+            if len(want_a) == 0:
+                continue
+            rescued = bool(res[r].flags & 2)
+            f, pp, chain, score, _ = O.chain_dp(want_a, 15, bw=(20000 if rescued else 500))
+            gf, gpp = dev.debug_dp(r)
+            assert np.array_equal(gf, f) and np.array_equal(gpp.astype(np.int64), pp), \
+                f"DP differs for read {r} (rescued={rescued}): " + _dp_diff(gf, gpp, f, pp, want_a)
+            n += 1
+        assert n >= len(rseqs) // 2
+    dev.set_debug(False)
+
+
 def test_pipeline_determinism(dev, small_world):
     ref, reads, rnames, rseqs = small_world
     idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
