@@ -769,6 +769,12 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
             LCHK(launch_chain_stage(5, ca, 2048, c->stream));
         }
         ca.lseg_prof = K[MM2G_KNOB_LSEG_PROF] ? 1u : 0u;
+        unsigned long long* gprof = nullptr;
+        if (ca.lseg_prof) {
+            HIPCHK(hipMalloc(&gprof, 16 * 8));
+            HIPCHK(hipMemsetAsync(gprof, 0, 16 * 8, c->stream));
+        }
+        ca.gprof = gprof;
         for (int stg = 0; stg < 5; ++stg) {
             ca.giant_min = giant_min[pass];
             ca.giant_exact = pass == 0 ? 1u : 0u;
@@ -790,6 +796,17 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
             }
             ProfScope ps(c, names[pass][stg]);
             LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));
+        }
+        if (gprof) {   // k_chain_giant phase sums (wall clock, 100 MHz)
+            unsigned long long g[16];
+            HIPCHK(hipMemcpyAsync(g, gprof, sizeof g, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            (void)hipFree(gprof);
+            ca.gprof = nullptr;
+            fprintf(stderr, "[giant_prof] pass %d: %llu segments, %llu anchors, %llu iterations, %llu pins, %llu fallbacks; block-us: total %.0f "
+                            "setup %.0f eval %.0f changed %.0f improve %.0f children %.0f markcheck %.0f pin %.0f write %.0f\n",
+                    pass, g[8], g[9], g[10], g[11], g[13], g[12] / 100.0, g[0] / 100.0, g[1] / 100.0, g[2] / 100.0, g[3] / 100.0,
+                    g[4] / 100.0, g[5] / 100.0, g[6] / 100.0, g[7] / 100.0);
         }
         if (ca.lseg_prof) {   // the slowest long segments of this pass
             uint32_t nl = 0;

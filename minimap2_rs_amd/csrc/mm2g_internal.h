@@ -199,6 +199,7 @@ struct ChainArgs {
     void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
     const uint32_t* abort = nullptr;
+    unsigned long long* gprof = nullptr;   // MM2G_LSEG_PROF: k_chain_giant phase sums (16 counters)
 };
 struct DvArgs {
     uint32_t n;

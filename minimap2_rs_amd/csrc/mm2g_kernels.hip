@@ -2509,6 +2509,8 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
         const uint64_t* K = a.keys + base;
         const uint64_t g_t0 = a.lseg_prof ? wall_clock64() : 0;
         int g_its = 0;
+        uint64_t gl = g_t0;   // MM2G_LSEG_PROF phase sums (thread 0, after barriers)
+#define GP(k) do { if (a.gprof && tid == 0) { const uint64_t t_ = wall_clock64(); atomicAdd(&a.gprof[k], (unsigned long long)(t_ - gl)); gl = t_; } } while (0)
         for (int t = tid; t < len; t += 1024) { gk[t] = K[s + t]; f0[t] = span; }
         __syncthreads();
         // window start (lchain.rs:75-77): first j with p_i <= p_j + max_dist_x, and max_iter
@@ -2520,6 +2522,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
             glo[t] = (uint16_t)min(t - l2, 65535);
         }
         __syncthreads();
+        GP(0);
         auto sc_of = [&](uint64_t ki, uint64_t kj, bool& ok) -> int32_t {   // comput_sc (lchain.rs:17-34)
             const int32_t dq = (int32_t)(ki & qmask) - (int32_t)(kj & qmask);
             const int32_t dr = (int32_t)((ki >> qb) & rmask) - (int32_t)((kj >> qb) & rmask);
@@ -2560,8 +2563,12 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                 }
                 vres = v0;
             } else {
+                // rounds stop once every pointer has reached a root (the forest's
+                // depth, not its size, sets their number: shallow forests settle
+                // in a few)
                 for (int d = 0; d < dbl; ++d) {
                     int32_t nv[4], np[4];
+                    bool live = false;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         const int t = tid + k * 1024;
@@ -2569,6 +2576,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                             const int32_t p = gptr[t];
                             nv[k] = p >= 0 ? val[t] + val[p] : val[t];
                             np[k] = p >= 0 ? gptr[p] : -1;
+                            live = live || np[k] >= 0;
                         }
                     }
                     __syncthreads();
@@ -2577,7 +2585,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                         const int t = tid + k * 1024;
                         if (t < len) { val[t] = nv[k]; gptr[t] = np[k]; }
                     }
-                    __syncthreads();
+                    if (!__syncthreads_or(live)) break;
                 }
             }
             return vres;
@@ -2661,6 +2669,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
             bool conv = false;
             for (int it = 0; it < GIANT_IT && !conv; ++it) {
                 const int32_t* vres = eval_forest();
+                GP(1);
                 if (tid == 0) s_flag = 0;
                 // Values that moved in this evaluation, as a prefix count (gch is free
                 // until the children lists).  An anchor none of whose predecessors
@@ -2676,6 +2685,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                     carry += (int)tot;
                 }
                 __syncthreads();
+                GP(2);
                 uint32_t ch = 0;
                 for (int t = tid; t < len; t += 1024) {
                     const uint32_t lw = glo[t];
@@ -2697,15 +2707,15 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                 conv = s_flag == 0;
                 ++g_its;
                 __syncthreads();
+                GP(3);
             }
-            if (!conv) {                         // k_chain_long runs it
-                if (a.lseg_prof && tid == 0) printf("[giant] len %d round %d: noconv\n", len, round);
-                break;
-            }
+            if (!conv) break;                    // k_chain_long runs it
             // Children lists of the converged forest: j is marked for i (t[j]
             // == i) iff a valid c in (j, i) has pprev[c] == j.  gptr = child
             // counts, val = list ends, gch = the lists.
             build_children();
+            __syncthreads();
+            GP(4);
             // No break is possible where a window holds <= max_skip mark
             // sources.  Elsewhere run the reference loop on the converged
             // values: the first anchor where it disagrees is pinned below.
@@ -2734,9 +2744,9 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                 if (mf != fo[t] || mj != gp[t]) atomicMin(&s_flag, (uint32_t)t);
             }
             __syncthreads();
+            GP(5);
             const uint32_t tf = s_flag;
             if (tf == 0x7fffffffu) {
-                if (a.lseg_prof && tid == 0) printf("[giant] len %d: settled after %d pins\n", len, round);
                 ok_seg = true;
                 break;
             }
@@ -2758,10 +2768,13 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                 fo[t] = mf; gp[t] = mj; glo[t] = (uint16_t)(glo[t] | 0x8000u);
             }
             __syncthreads();
+            GP(6);
+            if (a.gprof && tid == 0) atomicAdd(&a.gprof[11], 1ull);
         }
-        if (a.lseg_prof && tid == 0)
-            printf("[giant%s] len %d: %s, %d iterations, %.0f us\n", G ? "-hbm" : "", len, ok_seg ? "done" : "fallback", g_its,
-                   (double)(wall_clock64() - g_t0) / 100.0);
+        if (a.gprof && tid == 0) {
+            atomicAdd(&a.gprof[8], 1ull); atomicAdd(&a.gprof[9], (unsigned long long)len); atomicAdd(&a.gprof[10], (unsigned long long)g_its);
+            atomicAdd(&a.gprof[12], (unsigned long long)(wall_clock64() - g_t0)); if (!ok_seg) atomicAdd(&a.gprof[13], 1ull);
+        }
         if (!ok_seg) continue;
         if (tid == 0) s_best = 0;
         __syncthreads();
@@ -2774,14 +2787,28 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
             PP[s + t] = gp[t] >= 0 ? s + gp[t] : -1;
             best_merge(bf, bi, fo[t], s + t);
         }
-        if (bi >= 0) atomicMax(&s_best, best_key(bf, bi));
-        atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)pairs);
+        // one LDS / global atomic per wave, not per thread (same-address atomics serialize)
+        uint64_t bk = bi >= 0 ? best_key(bf, bi) : 0ull;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(bk, d, 64); bk = o > bk ? o : bk; }
+        pairs = wave_sum64(pairs);
+        if (lane_id() == 0) {
+            if (bk) atomicMax(&s_best, bk);
+            if (pairs) atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)pairs);
+        }
         __syncthreads();
         if (tid == 0) {
             atomicMax(a.rbest + r, s_best);
             a.lseg[q].w = LSEG_DONE;
         }
-        __syncthreads();
+        // LDS-only barrier: the next segment may reuse the LDS arrays, but the
+        // global stores above need not have landed (a full __syncthreads would
+        // wait for them)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        GP(7);
+#undef GP
     }
 }
 
