@@ -778,6 +778,10 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         for (int stg = 0; stg < 5; ++stg) {
             ca.giant_min = giant_min[pass];
             ca.giant_exact = pass == 0 ? 1u : 0u;
+            if (stg == 2) {   // longest-first order of the long segments (k_chain_giant and k_chain_long)
+                ProfScope ps(c, names[pass][stg]);
+                LCHK(launch_chain_stage(2, ca, 1, c->stream));
+            }
             // production only; the pin bitmap and the lo field bound the window (max_iter <= 5120)
             if (stg == 2 && ca.lazy && ca.giant_min != 0xffffffffu && ca.P.max_iter <= 5120 && K[MM2G_KNOB_GIANT]) {
                 ProfScope ps(c, pass ? "chain_giant_rescue" : "chain_giant");
@@ -794,6 +798,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                     LCHK(launch_chain_stage(8, ca, gblocks, c->stream));
                 }
             }
+            if (stg == 2) continue;   // launched above
             ProfScope ps(c, names[pass][stg]);
             LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));
         }

@@ -2500,7 +2500,23 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
-    for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
+    // LDS variant: workgroups take segments longest first (k_lseg_order) from a
+    // shared counter, so the long ones start early and no workgroup is left with
+    // a tail of them (static striding left the slowest workgroup ~2.7x the mean)
+    __shared__ uint32_t s_q;
+    for (uint32_t qi = blockIdx.x;; qi += gridDim.x) {
+        uint32_t q;
+        if constexpr (G) {
+            if (qi >= nl) break;
+            q = qi;
+        } else {
+            if (tid == 0) s_q = atomicAdd(&a.work[P.pass & 1], 1u);
+            __syncthreads();
+            const uint32_t t = s_q;
+            __syncthreads();
+            if (t >= nl) break;
+            q = a.lseg_order[t];
+        }
         const uint4 L = a.lseg[q];
         const int32_t s = (int32_t)L.y, e = (int32_t)L.z, len = e - s;
         if (len < (int32_t)a.giant_min || (G ? (len <= gcap || len > cap) : len > gcap)) continue;
