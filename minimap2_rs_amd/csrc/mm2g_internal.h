@@ -160,6 +160,7 @@ struct SortArgs {
     const uint32_t* abort = nullptr;
     uint32_t* rlist = nullptr;   // reads k_sort_read leaves to k_sort_radix ([n]), and their count (zeroed by k_sort_small)
     uint32_t* rcount = nullptr;
+    const uint32_t* order = nullptr;   // k_sort_read: block b sorts read order[b] (heaviest first); null = b
 };
 struct ChainArgs {
     uint32_t n;

@@ -1191,8 +1191,8 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
     __shared__ uint32_t s_goff[GOFF_LDS];
     extern __shared__ uint64_t dyn64[];
     uint32_t* dyn = (uint32_t*)dyn64;
-    const uint32_t r = blockIdx.x;
-    if (r >= a.n) return;
+    if (blockIdx.x >= a.n) return;
+    const uint32_t r = a.order ? a.order[blockIdx.x] : blockIdx.x;   // heaviest reads first
     const uint64_t base = a.a_off[r];
     const uint32_t A0 = (uint32_t)(a.a_off[r + 1] - base);
     if (A0 <= a.small_max) return;    // k_sort_small
@@ -2926,24 +2926,24 @@ __global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
 // order[t] = reads by descending anchor count (largest-first hand-out to the
 // chain waves).  Counting sort on log2 buckets of the anchor count keeps it one
 // cheap pass: exact LPT is not needed, only "heavy reads first".
+// Reads heaviest first (buckets of 512 anchors, descending): the hand-out order
+// of the per-read sort and of the chain work items (longest-processing-time
+// first, so the heaviest reads do not form the kernels' tails).
 __global__ __launch_bounds__(1024) void k_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order) {
-    __shared__ uint32_t hist[33], offs[33];
+    constexpr int NB = 1024;
+    __shared__ uint32_t hist[NB], s_sc[16];
     const int tid = threadIdx.x;
-    if (tid < 33) hist[tid] = 0;
+    hist[tid] = 0;
     __syncthreads();
-    for (uint32_t r = tid; r < n; r += 1024) {
-        const uint32_t c = a_cnt[r];
-        const int bk = c ? 32 - __builtin_clz(c) : 0;   // 0..32, heavier = larger
-        atomicAdd(&hist[32 - bk], 1u);
-    }
+    auto bucket = [](uint32_t c) -> int { const uint32_t b = c >> 9; return NB - 1 - (int)(b < (uint32_t)NB - 1 ? b : (uint32_t)NB - 1); };
+    for (uint32_t r = tid; r < n; r += 1024) atomicAdd(&hist[bucket(a_cnt[r])], 1u);
     __syncthreads();
-    if (tid == 0) { uint32_t run = 0; for (int b = 0; b < 33; ++b) { offs[b] = run; run += hist[b]; } }
+    uint32_t tot;
+    const uint32_t ex = block_excl_sum(hist[tid], tot, s_sc);
     __syncthreads();
-    for (uint32_t r = tid; r < n; r += 1024) {
-        const uint32_t c = a_cnt[r];
-        const int bk = c ? 32 - __builtin_clz(c) : 0;
-        order[atomicAdd(&offs[32 - bk], 1u)] = r;
-    }
+    hist[tid] = ex;
+    __syncthreads();
+    for (uint32_t r = tid; r < n; r += 1024) order[atomicAdd(&hist[bucket(a_cnt[r])], 1u)] = r;
 }
 
 // 6. dv inputs — paf_from_chain_with_primary (src/paf.rs:156-199): binary
