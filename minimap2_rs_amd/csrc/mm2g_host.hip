@@ -938,6 +938,12 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     int32_t* fb;
     ENSURE(c->fbuf, int32_t, A_cap, fb);    // the sort's per-key tags live here before the DP needs it
     sa.keys = keys; sa.cap_keys = c->keys.cap / 8;
+    // reads heaviest first (anchor counts from seed_count): the hand-out order of
+    // seed_write, the sort and the chain work items
+    uint32_t* rorder;
+    ENSURE(c->order, uint32_t, n, rorder);
+    LCHK(launch_read_order(n, a_cnt, rorder, c->stream));
+    sa.order = rorder;
     {
         ProfScope ps(c, "seed_write");
         LCHK(launch_seed_write(sa, grid_for(n), c->stream));
@@ -956,12 +962,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.abort = st32;
     so.meta = (uint32_t*)fb;
     so.rlist = rlist; so.rcount = rlist + n;
-    {   // heaviest reads first (also the chain stage's work-item order)
-        uint32_t* rorder;
-        ENSURE(c->order, uint32_t, n, rorder);
-        LCHK(launch_read_order(n, a_cnt, rorder, c->stream));
-        so.order = rorder;
-    }
+    so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     uint64_t* sprof = nullptr;
     if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 128)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 128, c->stream)); so.prof = sprof; }

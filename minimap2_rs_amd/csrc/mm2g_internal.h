@@ -134,6 +134,7 @@ struct SeedArgs {
     ReadOut* out;                         // m_kept
     uint32_t* a_part;                     // per read, SEED_PARTS-1 entries: anchors before part k (k = 1..)
     const uint32_t* abort = nullptr;      // batch status word (BS_*): kernels after the anchor scan exit on BS_ANCHORS
+    const uint32_t* order = nullptr;      // k_seed_write: reads heaviest first (null = batch order)
 };
 // seed_write splits each read's minimizers into this many contiguous parts
 // (whole 64-minimizer chunks), one wave each; seed_count records where they start

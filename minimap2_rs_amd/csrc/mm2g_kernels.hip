@@ -791,7 +791,7 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
     // one wave per (read, part): parts are contiguous runs of whole 64-minimizer
     // chunks, starting at the anchor counts seed_count recorded
     for (uint32_t wp = blockIdx.x * (blockDim.x >> 6) + wv; wp < a.n * (uint32_t)SEED_PARTS; wp += nwaves) {
-        const uint32_t r = wp / SEED_PARTS, part = wp % SEED_PARTS;
+        const uint32_t r = a.order ? (uint32_t)uni((int32_t)a.order[wp / SEED_PARTS]) : wp / SEED_PARTS, part = wp % SEED_PARTS;
         const uint64_t mb = uni64(a.mz_base[r]);
         const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
         const uint32_t nch = (m + 63) >> 6;
