@@ -1741,6 +1741,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     int32_t* tqs = (int32_t*)(krings + DP_NW * KRING);          // 3 classes x TQ segment starts
     uint8_t* tls = (uint8_t*)(tqs + DP_NW * 3 * TQ);            // their lengths
     int2* medbs = (int2*)(tls + DP_NW * 3 * TQ);
+    if (blockIdx.x * DP_NW >= (uint32_t)a.item_off[a.n]) return;   // no work item for this workgroup: skip the LUT load
     for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
     __syncthreads();
     const int lane = lane_id(), wv = wave_id();
@@ -1941,6 +1942,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
+    if (blockIdx.x * (blockDim.x >> 6) >= (uint32_t)a.item_off[a.n]) return;   // no work item: skip the LUT load
     for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
     __syncthreads();
     const int lane = lane_id();
@@ -2013,6 +2015,7 @@ __global__ __launch_bounds__(256) void k_chain_med(ChainArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
+    if (blockIdx.x * blockDim.x >= min(*a.mseg_n, a.mseg_cap)) return;   // no queue entry: skip the LUT load
     for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
     __syncthreads();
     const uint32_t qb = a.kl.qb;
@@ -2148,6 +2151,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
     uint32_t* rings = (uint32_t*)(smem + lut_bytes);
     uint64_t* rkeys = (uint64_t*)(rings + DP_NW * RING_WORDS);
     int2* rfps = (int2*)(rkeys + DP_NW * RK);
+    if (blockIdx.x * DP_NW >= min(*a.lseg_n, a.lseg_cap)) return;   // no long segment: skip the LUT load
     for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
     for (int i = threadIdx.x; i < DP_NW * RING_WORDS; i += blockDim.x) rings[i] = 0;
     __syncthreads();
