@@ -1815,6 +1815,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
         auto route = [&](bool emit, int32_t sl, int32_t el) {
             const int32_t len = el - sl;
             emit = emit && (int64_t)len * span >= (int64_t)fm;   // pruned: cannot hold the read's best f
+            if (!any(emit)) return;                               // nothing to route (the usual case when pruning)
             if (emit && len == 1) { F[sl] = span; PP[sl] = -1; best_merge(bf, bi, span, sl); }
             const bool c0 = emit && len == 2, c1 = emit && len >= 3 && len <= 4, c2 = emit && len >= 5 && len <= TINY;
             const uint64_t m0 = ballot(c0), m1 = ballot(c1), m2 = ballot(c2);
