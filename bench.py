@@ -279,7 +279,11 @@ def main():
     log(f"rank {rank}: index from {index_from} in {t_index:.1f}s, stats {idx.stats()}")
 
     # ---- reads: W+K distinct batches per rank, ASCII in host RAM ------------
-    n_batches = max(1, min(args.warmup + args.steps, args.max_batches))
+    # warmup: W steps, and at least one unit per context (each context's first
+    # unit allocates its workspaces; with W * P < S some would pay that in the timed region)
+    S_ctx = max(1, args.streams)
+    w_eff = max(args.warmup, -(-S_ctx // (args.shares if args.shares > 0 else S_ctx)))
+    n_batches = max(1, min(w_eff + args.steps, args.max_batches))
     t0 = time.time()
     batches = make_batches(gbuf, lens, args, rank, n_batches, thr)
     bases_per_batch = [int(b[1][-1]) for b in batches]
@@ -371,13 +375,13 @@ def main():
         if errs:
             raise errs[0]
 
-    run_steps(0, args.warmup)
+    run_steps(0, w_eff)
     for d in devs:
         d.prof_enable(True)
         d.prof_reset()
     barrier()
     t0 = time.perf_counter()
-    run_steps(args.warmup, args.warmup + args.steps)
+    run_steps(w_eff, w_eff + args.steps)
     barrier()
     elapsed = time.perf_counter() - t0
     prof = {}
@@ -386,7 +390,7 @@ def main():
             a0, c0 = prof.get(k, (0.0, 0))
             prof[k] = (a0 + ms, c0 + calls)
         d.prof_enable(False)
-    timed = [units[(s % n_batches) * P + k] for s in range(args.warmup, args.warmup + args.steps) for k in range(P)]
+    timed = [units[(s % n_batches) * P + k] for s in range(w_eff, w_eff + args.steps) for k in range(P)]
     cnt = {}
     for u in timed:
         for k, v in u["cnt"].items():
@@ -397,7 +401,7 @@ def main():
     # queue, wait for results (incl. post-processing), PAF formatting
     hm = np.array([u["host_ms"] for u in timed])
     host_ms = dict(zip(("set_reads", "map_enqueue", "results_wait", "format_paf"), [round(float(x), 3) for x in hm.mean(axis=0)]))
-    my_bases = sum(bases_per_batch[s % n_batches] for s in range(args.warmup, args.warmup + args.steps))
+    my_bases = sum(bases_per_batch[s % n_batches] for s in range(w_eff, w_eff + args.steps))
 
     # ---- extra: reads already resident in HBM (the round-1 headline) --------
     resident = None

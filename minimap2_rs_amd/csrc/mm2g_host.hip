@@ -183,7 +183,7 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
     if (hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) return;
     (void)hipFree(d);
-    double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0, nleg = 0;
+    double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0, nleg = 0, ktiny = 0, klong = 0, ksrch = 0;
     uint64_t t_lo = ~0ULL, t_hi = 0;
     uint32_t m = 0;
     std::vector<uint32_t> q0, q2, q3;
@@ -198,6 +198,7 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
         if ((p[9] >> 32) == 0xffffu) nleg += 1; else np += (double)(p[9] >> 32);
         t_lo = std::min(t_lo, p[10]); t_hi = std::max(t_hi, p[11]);
         q0.push_back((uint32_t)p[8]); q2.push_back((uint32_t)p[9]);
+        ktiny += (double)(uint32_t)p[14]; klong += (double)(p[14] >> 32); ksrch += (double)p[15];
     }
     if (!m) return;
     std::sort(q0.begin(), q0.end()); std::sort(q2.begin(), q2.end()); std::sort(q3.begin(), q3.end());
@@ -208,6 +209,8 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
     fprintf(stderr, "[sort_prof] reads=%u (whole-read radix %.0f) A0=%.0f A=%.0f nbig=%.2f windows=%.2f us/read: p1+kc=%.1f p2=%.1f gather=%.1f segs=%.1f chunk=%.1f rank=%.1f p4b/radix=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
             m, nleg, a0 / m, a2 / m, np / m, ph[7] / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
             ph[5] / m / 100, ph[6] / m / 100, tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
+    fprintf(stderr, "[sort_prof] keys per read in segments <= %u: %.0f, 17..64: %.0f, > 64: %.0f (%.2f other-chunk searches each)\n",
+            16u, ktiny / m, (a2 - ktiny - klong) / m, klong / m, klong > 0 ? ksrch / klong : 0.0);
 }
 
 // MM2G_SKETCH_PROF: phase times of k_sketch summed over each read's tiles

@@ -1384,6 +1384,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                 // above the cell-local lb <= 32 (rank, group, cell), so they compare
                 // by their low dwords.
                 const uint32_t* S32 = (const uint32_t*)S;
+                uint32_t pc_tiny = 0, pc_long = 0, pc_srch = 0;     // MM2G_KNOB_SORT_PROF segment classes
                 for (uint32_t i = tid; i < nwin; i += 1024) {
                     const uint64_t x = S[i];
                     uint32_t s, e;
@@ -1399,6 +1400,10 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                     }
                     const uint32_t xl = (uint32_t)x;
                     uint32_t rank = 0;
+                    if (pq) {
+                        if (L <= SEG_TINY) ++pc_tiny;
+                        else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
+                    }
                     if (L <= SEG_TINY) {
                         for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
                     } else {
@@ -1410,6 +1415,10 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                         }
                     }
                     O[oa + s + rank] = x & kmask;
+                }
+                if (pq) {
+                    const uint64_t v14 = wave_sum64(((uint64_t)pc_long << 32) | pc_tiny), v15 = wave_sum64(pc_srch);
+                    if (lane == 0) { atomicAdd((unsigned long long*)&pq[14], (unsigned long long)v14); atomicAdd((unsigned long long*)&pq[15], (unsigned long long)v15); }
                 }
                 __syncthreads();
                 SORT_PH(5);
