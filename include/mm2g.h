@@ -53,8 +53,9 @@ int mm2g_index_build_seqs(uint32_t n_seq, const char* const* names, const uint8_
                           int w, int k, int b, int flag, int n_threads, mm2g_index** out);
 /* The same builds on a GPU (reference sketching, bucket
  * sort by hash and p/h construction on `device`, S packed there too); the
- * result is identical to the host build (same .mmi bytes).  HPC (flag & 1) and
- * even k fall back to the host build inside the call. */
+ * result is identical to the host build (same .mmi bytes).  Even k is built on
+ * the device too (per-view warm-ups sized on the host, mm2g_ixbuild.hip); HPC
+ * (flag & 1) falls back to the host build inside the call. */
 int mm2g_index_build_fasta_gpu(const char* path, int w, int k, int b, int flag, int device, int n_threads, mm2g_index** out);
 int mm2g_index_build_seqs_gpu(uint32_t n_seq, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens,
                               int w, int k, int b, int flag, int device, int n_threads, mm2g_index** out);
@@ -280,7 +281,9 @@ enum {
     MM2G_IKNOB_IXCHUNK = 1,      /* GPU index build: bases per sketch view [65536]                            */
     MM2G_IKNOB_IXPROF = 2,       /* GPU index build: phase times to stderr [0]                                */
     MM2G_IKNOB_LOAD_THREADS = 3, /* .mmi load threads; 0 = min(32, cores) [0]                                 */
-    MM2G_IKNOB_COUNT = 4
+    MM2G_IKNOB_GPU_STRICT = 4,   /* tests: a GPU index build the device cannot do fails instead of falling
+                                    back to the host build [0]                                               */
+    MM2G_IKNOB_COUNT = 5
 };
 int mm2g_set_index_knob(int knob, int64_t value);
 

@@ -60,7 +60,7 @@ KNOBS = {"sort_small": 1, "seg_small": 2, "seg_chunk": 3, "giant_min": 4, "giant
          "giant_gblocks": 8, "filter": 9, "lazy": 10, "prune": 11, "giant": 12, "sketch_prof": 13, "sort_prof": 14,
          "lseg_prof": 15, "midhist_bins": 16, "sync_each": 17, "host_threads": 18, "ws_min": 19,
          "sort_lds_kb": 20, "stop_at": 21}
-INDEX_KNOBS = {"ixchunk": 1, "ixprof": 2, "load_threads": 3}
+INDEX_KNOBS = {"ixchunk": 1, "ixprof": 2, "load_threads": 3, "gpu_strict": 4}
 
 _VP = C.c_void_p
 _P64 = C.POINTER(C.c_uint64)

@@ -287,6 +287,7 @@ static int build_gpu_or_host(int device, const std::vector<const uint8_t*>& seqs
     bool unsupported = false;
     if (!build_index_gpu(device, seqs, lens, names, w, k, b, flag, I->h, err, unsupported)) {
         if (!unsupported) return set_err(MM2G_E_HIP, "%s", err.c_str());
+        if (g_index_knob[MM2G_IKNOB_GPU_STRICT].load()) return set_err(MM2G_E_UNSUP, "%s", err.c_str());
         if (!build_index(seqs, lens, names, w, k, b, flag, n_threads, I->h, err)) return set_err(MM2G_E_ARG, "%s", err.c_str());
     }
     *out = I.release();

@@ -3,11 +3,11 @@
 // (src/index.rs:69-109) run on the device.
 //
 //   1. contigs -> HBM; each contig is cut into views of IX_CHUNK bases plus a
-//      warm-up of 2(w+k)+64 bases before them.  k_sketch runs one wave per view
+//      warm-up before them (view_warmup below).  k_sketch runs one wave per view
 //      (SketchArgs view_*): the k-mer registers walk back into the contig (the
 //      reference never resets them), l and the w-slot window converge inside
-//      the warm-up (odd k: no symmetric k-mers), and only steps >= the view's
-//      own first base emit, so the views' emissions partition the contig's.
+//      the warm-up, and only steps >= the view's own first base emit, so the
+//      views' emissions partition the contig's.
 //   2. k_ix_compact: (hash, rid<<32 | pos<<1 | strand) pairs, contig order.
 //   3. two stable LSD radix sorts (rocPRIM): by value, then by hash -> sorted by
 //      (hash, value), which is post_process's order: per hash a run; runs of
@@ -17,9 +17,8 @@
 //      table are byte-identical with the host build (tests/test_gpu_parity.py).
 //   5. S, the 4-bit packed reference (src/index.rs:14-19), is packed on the
 //      device (k_pack4).
-// HPC (flag & 1) and even k are not built here (the caller falls back to the
-// host build): HPC spans need the TinyQueue branch, and symmetric k-mers (even
-// k only) can delay l's convergence past any fixed warm-up.
+// HPC (flag & 1) is not built here (the caller falls back to the host build):
+// its spans need the TinyQueue branch (src/sketch.rs:53-64).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -90,6 +89,50 @@ struct Dev {
     }
 };
 
+// Warm-up start of a view whose emissions begin at contig position c0.  The
+// sketch starts the view with l = 0 (src/sketch.rs:44,66-70: l counts the
+// non-symmetric ACGT k-mers since the last ambiguous base); the reference's l
+// there is unknown.  Both agree from the first ambiguous base on, and -- for
+// every comparison the reference makes, against k, w+k-1 and w+k -- from the
+// (w+k)-th non-symmetric k-mer on.  info and the w-slot window then follow
+// after w more steps.  Odd k has no symmetric k-mers, so a fixed 2(w+k)+64
+// bases always suffice; with even k a palindromic run ((AT)n, (ACGT)n, ...)
+// produces symmetric k-mers only, so the warm-up grows (doubling, down to the
+// contig start, where the sketch is exact) until it converges early enough.
+// The k-mer registers at vs come from the k-1 ACGT bases before it, as the
+// kernel's own walk-back computes them.
+int64_t view_warmup(const uint8_t* seq, int64_t c0, int w, int k) {
+    const int64_t cap = w + k;
+    int64_t warm = 2 * (w + k) + 64;
+    const uint64_t mask = (1ULL << (2 * k)) - 1;
+    const uint32_t shift1 = 2u * (uint32_t)(k - 1);
+    auto nt4h = [](uint8_t b) -> uint32_t {
+        const uint32_t c = b | 0x20u;
+        return c == 'a' ? 0u : c == 'c' ? 1u : c == 'g' ? 2u : c == 't' ? 3u : 4u;
+    };
+    for (;;) {
+        const int64_t vs = c0 > warm ? c0 - warm : 0;
+        if (vs == 0) return 0;
+        int64_t p = vs;
+        int need = k - 1;
+        while (need > 0 && p > 0) { --p; if (nt4h(seq[p]) < 4) --need; }
+        uint64_t kf = 0, kr = 0;
+        for (; p < vs; ++p) {
+            const uint32_t c = nt4h(seq[p]);
+            if (c < 4) { kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1); }
+        }
+        int64_t n = 0, conv = -1;
+        for (p = vs; p < c0 && conv < 0; ++p) {
+            const uint32_t c = nt4h(seq[p]);
+            if (c >= 4) { conv = p; break; }
+            kf = ((kf << 2) | c) & mask; kr = (kr >> 2) | ((uint64_t)(3 ^ c) << shift1);
+            if (kf != kr && ++n >= cap) conv = p;
+        }
+        if (conv >= 0 && conv + w + 2 <= c0) return vs;
+        warm *= 2;
+    }
+}
+
 inline int bit_width64(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
 inline size_t kroundup64(size_t x) { --x; x |= x >> 1; x |= x >> 2; x |= x >> 4; x |= x >> 8; x |= x >> 16; x |= x >> 32; return x + 1; }
 
@@ -113,7 +156,7 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     };
     if (w <= 0 || w >= 256 || k <= 0 || k > 28) { err = "invalid w/k (0 < w < 256, 0 < k <= 28)"; return false; }
     if (b < 1 || b > 30) { err = "invalid bucket bits"; return false; }
-    if ((flag & 1) || (k % 2) == 0) { unsupported = true; err = "GPU index build: HPC or even k (host build)"; return false; }
+    if (flag & 1) { unsupported = true; err = "GPU index build: HPC (host build)"; return false; }
     const size_t n = seqs.size();
     for (size_t i = 0; i < n; ++i)
         if (lens[i] >= (1ULL << 31)) { err = "sequences must be shorter than 2^31"; return false; }
@@ -141,7 +184,6 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
         if (lens[i]) IXCHK(hipMemcpyAsync(d_seq + idx.seq[i].offset, seqs[i], lens[i], hipMemcpyHostToDevice, st));
     int64_t chunk = IX_CHUNK;
     if (const int64_t v = g_index_knob[1].load()) chunk = std::max<int64_t>(256, v);   // MM2G_IKNOB_IXCHUNK (tests)
-    const int64_t warm = 2 * (w + k) + 64;
     std::vector<uint64_t> v_off, v_base, v_end;
     std::vector<uint32_t> v_len, v_pre, v_from, v_rid;
     std::vector<uint8_t> v_last;
@@ -149,7 +191,7 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     for (size_t r = 0; r < n; ++r) {
         const int64_t L = (int64_t)lens[r];
         for (int64_t c0 = 0; c0 < L; c0 += chunk) {
-            const int64_t vs = c0 > warm ? c0 - warm : 0, ve = std::min<int64_t>(L, c0 + chunk);
+            const int64_t vs = c0 ? view_warmup(seqs[r], c0, w, k) : 0, ve = std::min<int64_t>(L, c0 + chunk);
             v_off.push_back(idx.seq[r].offset + (uint64_t)vs);
             v_len.push_back((uint32_t)(ve - vs)); v_pre.push_back((uint32_t)vs); v_from.push_back((uint32_t)(c0 - vs));
             v_last.push_back(ve == L ? 1 : 0); v_rid.push_back((uint32_t)r);

@@ -332,7 +332,11 @@ def test_gpu_index_build(tmp_path, chunk):
     233-307) byte for byte (.mmi), with stats and calc_mid_occ (index.rs:
     111-141), on an hg38-shaped and an E. coli-shaped genome plus edge contigs:
     N runs across view boundaries, lowercase, contigs shorter than k, empty
-    contigs.  The product's host build must agree as well."""
+    contigs; even k (symmetric k-mers) with palindromic runs ((AT)n, (ACGT)n,
+    (TA)n in lowercase) that span view boundaries, so the per-view warm-up has
+    to grow past its default.  The build must run on the device
+    (MM2G_IKNOB_GPU_STRICT: no host fallback).  The product's host build must
+    agree as well."""
     rng = random.Random(11)
     names, lens, gbuf = simdata.genome("hg38", 0.0006, 5)
     seqs = [gbuf[int(o):int(o + l)].tobytes() for o, l in zip(np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)]
@@ -343,11 +347,17 @@ def test_gpu_index_build(tmp_path, chunk):
         s[st_:st_ + 60] = b"N" * 60
     seqs += [bytes(s), _rand_seq(rng, 9000, p_low=0.3), b"ACGTACGT", b"", _rand_seq(rng, 15, p_n=0.0), b"N" * 500 + _rand_seq(rng, 3000)]
     names += ["nruns", "lower", "short", "empty", "k15", "leadingN"]
+    pal = bytearray(_rand_seq(rng, 1000))
+    for unit, n in ((b"AT", 700), (b"ACGT", 350), (b"ta", 2200), (b"GC", 90)):
+        pal += unit * n + _rand_seq(rng, rng.randrange(200, 900))
+    pal += b"AT" * 5000                      # ends inside a palindromic run
+    seqs.append(bytes(pal)); names.append("palindromes")
     M.set_index_knob("ixchunk", chunk or 0)
+    M.set_index_knob("gpu_strict", 1)
     try:
         buf = np.frombuffer(b"".join(seqs), dtype=np.uint8)
         lv = np.array([len(x) for x in seqs], dtype=np.uint64)
-        for w, k in ((10, 15), (5, 11), (19, 19), (10, 27)):
+        for w, k in ((10, 15), (5, 11), (19, 19), (10, 27), (10, 16), (7, 8), (12, 28), (3, 2)):
             oi = O.OIndex.build_from_buffer(names, buf, lv, w=w, k=k, b=14, threads=4)
             ig = M.Index.build_from_buffer(names, buf, lv, w=w, k=k, b=14, threads=4, device=0)
             ih = M.Index.build_from_seqs(names, seqs, w=w, k=k, b=14, threads=4)
@@ -360,6 +370,7 @@ def test_gpu_index_build(tmp_path, chunk):
             assert _mmi_bytes(ih, str(tmp_path / "h.mmi")) == want, (w, k)
     finally:
         M.set_index_knob("ixchunk", 0)
+        M.set_index_knob("gpu_strict", 0)
 
 
 def test_cli_streaming_fastq(small_world, tmp_path):
