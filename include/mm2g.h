@@ -53,9 +53,11 @@ int mm2g_index_build_seqs(uint32_t n_seq, const char* const* names, const uint8_
                           int w, int k, int b, int flag, int n_threads, mm2g_index** out);
 /* The same builds on a GPU (reference sketching, bucket
  * sort by hash and p/h construction on `device`, S packed there too); the
- * result is identical to the host build (same .mmi bytes).  Even k is built on
- * the device too (per-view warm-ups sized on the host, mm2g_ixbuild.hip); HPC
- * (flag & 1) falls back to the host build inside the call. */
+ * result is identical to the host build (same .mmi bytes).  Odd and even k
+ * (per-view warm-ups sized on the host) and HPC (flag & 1: TinyQueue spans,
+ * src/sketch.rs:51-64, computed per base on the device) are built on the
+ * device; a device failure the build cannot handle (minimizer slot overflow)
+ * falls back to the host build inside the call unless MM2G_IKNOB_GPU_STRICT. */
 int mm2g_index_build_fasta_gpu(const char* path, int w, int k, int b, int flag, int device, int n_threads, mm2g_index** out);
 int mm2g_index_build_seqs_gpu(uint32_t n_seq, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens,
                               int w, int k, int b, int flag, int device, int n_threads, mm2g_index** out);

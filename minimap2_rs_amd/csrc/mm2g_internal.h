@@ -102,6 +102,10 @@ struct SketchArgs {
     const uint32_t* view_pre = nullptr;
     const uint32_t* emit_from = nullptr;
     const uint8_t* view_last = nullptr;
+    // HPC index build (flag & 1): per base of seq, the TinyQueue span of the
+    // k-mer ending there (src/sketch.rs:51-64; 256 = too long, no info).
+    // Null: every span is k (non-HPC, sketch.rs:66-70).
+    const uint16_t* hpc_span = nullptr;
     // Query reads in the device nt4 format (include/mm2g.h, "nt4 read batch"):
     // read r's 2-bit codes start at pk_words[pk_off[r]], its ambiguity bitmap
     // (if any) at pk_words[amb_off[r]] (U64MAX = none).  Null: ASCII `seq`.

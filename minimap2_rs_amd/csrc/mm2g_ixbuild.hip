@@ -17,8 +17,13 @@
 //      table are byte-identical with the host build (tests/test_gpu_parity.py).
 //   5. S, the 4-bit packed reference (src/index.rs:14-19), is packed on the
 //      device (k_pack4).
-// HPC (flag & 1) is not built here (the caller falls back to the host build):
-// its spans need the TinyQueue branch (src/sketch.rs:53-64).
+//   HPC (flag & 1, src/sketch.rs:51-64): the reference never advances i past a
+//      homopolymer run, so k-mers are the plain ones and only the
+//      spans change: span(i) = sum of skip_len over the last k ACGT bases since
+//      the last ambiguous base (TinyQueue), skip_len(j) = the run of base j's
+//      code starting at j, to the contig end.  k_hpc_skip / k_hpc_span compute
+//      them per base (u16, capped at 256: a span >= 256 gives no info) before
+//      the sketch, which reads them (SketchArgs::hpc_span).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -61,6 +66,46 @@ __global__ __launch_bounds__(256) void k_ix_compact(uint32_t n_views, const uint
         const uint32_t y = mz_y[b + i];
         hash[o + i] = x >> 8;
         val[o + i] = (rid << 32) | ((pre + (y >> 1)) << 1) | (uint64_t)(y & 1u);   // src/sketch.rs:72 (i not truncated)
+    }
+}
+
+// contig of global position i: the last r with coff[r] <= i (coff: n+1 offsets)
+__device__ __forceinline__ uint32_t contig_of(const uint64_t* coff, uint32_t n, uint64_t i) {
+    uint32_t lo = 0, hi = n;              // coff[lo] <= i < coff[hi]
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (coff[mid] <= i) lo = mid; else hi = mid; }
+    return lo;
+}
+
+// HPC skip_len (src/sketch.rs:53-58): the run of seq[i]'s code from i on, to
+// the contig end, capped at 256 (0 for an ambiguous base)
+__global__ __launch_bounds__(256) void k_hpc_skip(const uint8_t* seq, uint64_t total, const uint64_t* coff, uint32_t n,
+                                                  uint16_t* skip) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = nt4_dev(seq[i]);
+        if (c >= 4) { skip[i] = 0; continue; }
+        const uint64_t e = coff[contig_of(coff, n, i) + 1];
+        const uint64_t lim = e < i + 256 ? e : i + 256;
+        uint64_t t = i + 1;
+        while (t < lim && nt4_dev(seq[t]) == c) ++t;
+        skip[i] = (uint16_t)(t - i);
+    }
+}
+
+// HPC span (src/sketch.rs:59-61): TinyQueue holds the last k skip_lens since
+// the last ambiguous base (cleared there, :64), so span(i) is their sum over
+// j in (i-k, i] back to that base or the contig start; capped at 256
+__global__ __launch_bounds__(256) void k_hpc_span(const uint8_t* seq, uint64_t total, const uint64_t* coff, uint32_t n, int k,
+                                                  const uint16_t* skip, uint16_t* span) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (nt4_dev(seq[i]) >= 4) { span[i] = 0; continue; }
+        const uint64_t s0 = coff[contig_of(coff, n, i)];
+        uint32_t sum = 0;
+        for (uint64_t j = i, m = 0; m < (uint64_t)k && j >= s0; --j, ++m) {
+            if (nt4_dev(seq[j]) >= 4) break;
+            sum += skip[j];
+            if (j == 0) break;
+        }
+        span[i] = (uint16_t)(sum < 256u ? sum : 256u);
     }
 }
 
@@ -156,7 +201,6 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     };
     if (w <= 0 || w >= 256 || k <= 0 || k > 28) { err = "invalid w/k (0 < w < 256, 0 < k <= 28)"; return false; }
     if (b < 1 || b > 30) { err = "invalid bucket bits"; return false; }
-    if (flag & 1) { unsupported = true; err = "GPU index build: HPC (host build)"; return false; }
     const size_t n = seqs.size();
     for (size_t i = 0; i < n; ++i)
         if (lens[i] >= (1ULL << 31)) { err = "sequences must be shorter than 2^31"; return false; }
@@ -228,9 +272,25 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
         IXCHK(hipGetLastError());
         IXCHK(hipMemcpyAsync(idx.S.data(), d_S, nw * 4, hipMemcpyDeviceToHost, st));
     }
-    // ---- 3. sketch every view (one wave each)
+    // ---- 3. HPC spans (flag & 1), then sketch every view (one wave each)
+    uint16_t* d_span = nullptr;
+    if (flag & 1) {
+        std::vector<uint64_t> coff(n + 1, 0);
+        for (size_t i = 0; i < n; ++i) coff[i + 1] = coff[i] + lens[i];
+        uint64_t* d_coff = D.alloc<uint64_t>(n + 1);
+        uint16_t* d_skip = D.alloc<uint16_t>(total);
+        d_span = D.alloc<uint16_t>(total);
+        if (!d_coff || !d_skip || !d_span) { err = "hipMalloc(HPC spans) failed"; return false; }
+        IXCHK(hipMemcpyAsync(d_coff, coff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        const unsigned nb = (unsigned)std::min<uint64_t>((total + 255) / 256, 65536);
+        hipLaunchKernelGGL(k_hpc_skip, dim3(nb), dim3(256), 0, st, d_seq, total, d_coff, (uint32_t)n, d_skip);
+        IXCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_hpc_span, dim3(nb), dim3(256), 0, st, d_seq, total, d_coff, (uint32_t)n, k, d_skip, d_span);
+        IXCHK(hipGetLastError());
+    }
     SketchArgs sa{d_seq, nullptr, nv, w, k, d_vbase, d_vend, d_mx, d_my, d_cnt, d_ovf};
     sa.view_off = d_voff; sa.view_len = d_vlen; sa.view_pre = d_vpre; sa.emit_from = d_vfrom; sa.view_last = d_vlast;
+    sa.hpc_span = d_span;
     if (launch_sketch(sa, (int)std::min<uint32_t>((nv + 3) / 4, 4096u), st) != 0) { err = "k_sketch launch failed"; return false; }
     std::vector<uint32_t> cnt(nv);
     int32_t ovf = 0;

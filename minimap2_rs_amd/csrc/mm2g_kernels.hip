@@ -232,7 +232,7 @@ struct SeqNt4 {
     }
 };
 
-template <bool K32, typename Src>
+template <bool K32, typename Src, bool HPC = false>
 #ifndef SK_WPE
 #define SK_WPE 4            // waves per SIMD: caps k_sketch at 128 VGPRs
 #endif
@@ -357,7 +357,12 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
                             uint64_t h;
                             if (K32) h = hash64d<uint32_t>((uint32_t)km, (uint32_t)mask);
                             else h = hash64d<uint64_t>(km, mask);
-                            x = (h << 8) | (uint64_t)k;        // kmer_span == k whenever info is valid
+                            if constexpr (HPC) {               // TinyQueue span (sketch.rs:51-64, 72)
+                                const uint32_t sp = a.hpc_span[roff + (uint64_t)p];
+                                x = sp < 256u ? (h << 8) | (uint64_t)sp : U64MAX;
+                            } else {
+                                x = (h << 8) | (uint64_t)k;    // kmer_span == k whenever info is valid
+                            }
                             fl = 2;
                         }
                     }
@@ -3157,7 +3162,10 @@ int launch_sketch(const SketchArgs& a, int n_blocks, hipStream_t st) {
         if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqNt4>), dim3(n_blocks), dim3(256), lds, st, a);
         else hipLaunchKernelGGL((k_sketch<false, SeqNt4>), dim3(n_blocks), dim3(256), lds, st, a);
     } else {
-        if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqAscii>), dim3(n_blocks), dim3(256), lds, st, a);
+        if (a.hpc_span) {
+            if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqAscii, true>), dim3(n_blocks), dim3(256), lds, st, a);
+            else hipLaunchKernelGGL((k_sketch<false, SeqAscii, true>), dim3(n_blocks), dim3(256), lds, st, a);
+        } else if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqAscii>), dim3(n_blocks), dim3(256), lds, st, a);
         else hipLaunchKernelGGL((k_sketch<false, SeqAscii>), dim3(n_blocks), dim3(256), lds, st, a);
     }
     LAUNCH_CHECK();

@@ -334,7 +334,8 @@ def test_gpu_index_build(tmp_path, chunk):
     N runs across view boundaries, lowercase, contigs shorter than k, empty
     contigs; even k (symmetric k-mers) with palindromic runs ((AT)n, (ACGT)n,
     (TA)n in lowercase) that span view boundaries, so the per-view warm-up has
-    to grow past its default.  The build must run on the device
+    to grow past its default; HPC (flag 1: TinyQueue spans, sketch.rs:51-64)
+    with homopolymer runs up to 400 bases (spans >= 256 give no info).  The build must run on the device
     (MM2G_IKNOB_GPU_STRICT: no host fallback).  The product's host build must
     agree as well."""
     rng = random.Random(11)
@@ -352,22 +353,34 @@ def test_gpu_index_build(tmp_path, chunk):
         pal += unit * n + _rand_seq(rng, rng.randrange(200, 900))
     pal += b"AT" * 5000                      # ends inside a palindromic run
     seqs.append(bytes(pal)); names.append("palindromes")
+    # HPC spans: homopolymer runs of 2-400 bases (>= 256: no info), across view
+    # boundaries, broken by N, in lowercase, and at the contig end
+    hp = bytearray(_rand_seq(rng, 500))
+    for _ in range(60):
+        c = rng.choice(b"ACGTacgt")
+        hp += bytes([c]) * rng.choice((2, 3, 5, 9, 17, 40, 120, 255, 256, 257, 400))
+        if rng.random() < 0.2:
+            hp += b"N" * rng.randrange(1, 4) + bytes([c]) * rng.randrange(1, 30)
+        hp += _rand_seq(rng, rng.randrange(5, 300))
+    hp += b"G" * 300
+    seqs.append(bytes(hp)); names.append("homopolymers")
     M.set_index_knob("ixchunk", chunk or 0)
     M.set_index_knob("gpu_strict", 1)
     try:
         buf = np.frombuffer(b"".join(seqs), dtype=np.uint8)
         lv = np.array([len(x) for x in seqs], dtype=np.uint64)
-        for w, k in ((10, 15), (5, 11), (19, 19), (10, 27), (10, 16), (7, 8), (12, 28), (3, 2)):
-            oi = O.OIndex.build_from_buffer(names, buf, lv, w=w, k=k, b=14, threads=4)
-            ig = M.Index.build_from_buffer(names, buf, lv, w=w, k=k, b=14, threads=4, device=0)
-            ih = M.Index.build_from_seqs(names, seqs, w=w, k=k, b=14, threads=4)
-            assert ig.stats() == oi.stats() == ih.stats(), (w, k)
+        for w, k, fl in ((10, 15, 0), (5, 11, 0), (19, 19, 0), (10, 27, 0), (10, 16, 0), (7, 8, 0), (12, 28, 0), (3, 2, 0),
+                         (10, 15, 1), (5, 12, 1), (19, 19, 1), (12, 28, 1), (2, 3, 1)):
+            oi = O.OIndex.build_from_buffer(names, buf, lv, w=w, k=k, b=14, flag=fl, threads=4)
+            ig = M.Index.build_from_buffer(names, buf, lv, w=w, k=k, b=14, flag=fl, threads=4, device=0)
+            ih = M.Index.build_from_seqs(names, seqs, w=w, k=k, b=14, flag=fl, threads=4)
+            assert ig.stats() == oi.stats() == ih.stats(), (w, k, fl)
             for fr in (2e-4, 0.01, 0.5):
                 assert ig.calc_mid_occ(fr) == oi.mid_occ(fr) == ih.calc_mid_occ(fr)
             oi.save_mmi(str(tmp_path / "o.mmi"))
             want = open(str(tmp_path / "o.mmi"), "rb").read()
-            assert _mmi_bytes(ig, str(tmp_path / "g.mmi")) == want, (w, k)
-            assert _mmi_bytes(ih, str(tmp_path / "h.mmi")) == want, (w, k)
+            assert _mmi_bytes(ig, str(tmp_path / "g.mmi")) == want, (w, k, fl)
+            assert _mmi_bytes(ih, str(tmp_path / "h.mmi")) == want, (w, k, fl)
     finally:
         M.set_index_knob("ixchunk", 0)
         M.set_index_knob("gpu_strict", 0)
