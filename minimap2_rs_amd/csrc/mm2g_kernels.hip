@@ -931,6 +931,15 @@ constexpr int SORT_LDS = 157 * 1024;     // dynamic LDS of k_sort_read (one work
 #ifndef SORT_U
 #define SORT_U 8                          // keys per thread in flight in the block-wide passes over a read
 #endif
+#ifndef SORT_U1
+#define SORT_U1 SORT_U                    // ... in P1 (bitmaps only: few registers per key)
+#endif
+#ifndef SORT_U2
+#define SORT_U2 SORT_U                    // ... in P2
+#endif
+#ifndef SORT_UG
+#define SORT_UG SORT_U                    // ... in the window gathers
+#endif
 
 // 8 independent loads per thread, then fn(i, x) for each (i < n): hides HBM
 // latency in the block-wide passes of k_sort_read
@@ -1239,7 +1248,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
         // ---- P1: seen / seen-twice bitmaps
         for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
         __syncthreads();
-        block_pass8<SORT_U>(K, A0, [&](uint32_t, uint64_t x) {
+        block_pass8<SORT_U1>(K, A0, [&](uint32_t, uint64_t x) {
             const uint32_t c = cell_of(x), w = c >> 5, bit = 1u << (c & 31);
             if (atomicOr(&B1[w], bit) & bit) atomicOr(&B2[w], bit);   // seen before: seen twice
         });
@@ -1287,7 +1296,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
             // the bitmaps can be overwritten by the first window).
             uint64_t smx = 0;
             uint16_t* T16 = (uint16_t*)(a.meta + base);
-            block_pass8<SORT_U>(K, A0, [&](uint32_t i, uint64_t x) {
+            block_pass8<SORT_U2>(K, A0, [&](uint32_t i, uint64_t x) {
                 bool kept;
                 const uint32_t rk = rank_of(cell_of(x), kept);
                 if (kept) atomicAdd(&C[rk >> 1], 1u << ((rk & 1) << 4));
@@ -1351,7 +1360,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                 // window keys carry their rank in the top 16 bits: the rank rises
                 // with the key, so the order is unchanged, and a key's segment is
                 // one shift away
-                block_pass_km<SORT_U>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m) {
+                block_pass_km<SORT_UG>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m) {
                     const uint32_t rk = m;
                     if (m != 0xffffu && rk >= ra && rk < rb) {
                         const uint32_t sh = (rk & 1) << 4;

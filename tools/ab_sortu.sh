@@ -1,8 +1,13 @@
-# A/B: keys in flight per thread in the sort passes (U=8 default lib vs U=16 build), sort phase profile + 1-stream bench.
+# k_sort_read pass widths (SORT_U1 / SORT_U2 builds from tools/build_exp.sh): phase
+# profile (1 stream) and the sort kernel time, alternated on one box.
 set -e
 mkdir -p gpurun_out
-for v in base u16; do
-  if [ $v = u16 ]; then export MM2G_LIB=$PWD/minimap2_rs_amd/build/u16/libmm2g.so; fi
-  timeout -k 10 300 python3 bench.py --no-parity --resident-steps 0 --steps 1 --warmup 0 --streams 1 --knob sort_prof=1 > gpurun_out/sp_$v.json 2> gpurun_out/sp_$v.err
-  timeout -k 10 300 python3 bench.py --no-parity --resident-steps 0 --streams 1 > gpurun_out/s1_$v.json 2> gpurun_out/s1_$v.err
+: > gpurun_out/absu.txt
+for lib in ${LIBS:-- u1x16 u1x24 u12x16 -}; do
+  LIBV=""; [ "$lib" != "-" ] && LIBV="minimap2_rs_amd/build/libmm2g_$lib.so"
+  MM2G_LIB=$LIBV timeout -k 10 300 python bench.py --no-cpu --no-parity --resident-steps 0 --streams 1 --steps ${STEPS:-4} --warmup 1 --knob sort_prof=1 > gpurun_out/absu.json 2>gpurun_out/absu.err
+  echo "== $lib" >> gpurun_out/absu.txt
+  grep "sort_prof\] reads" gpurun_out/absu.err | tail -2 >> gpurun_out/absu.txt
+  python -c "
+import json;d=json.loads(open('gpurun_out/absu.json').read().strip().splitlines()[-1]);pk=d['extra']['per_kernel'];print('$lib', d['value'], d['ms_per_step'], 'sort_large', pk['sort_large']['ms_per_step'])" >> gpurun_out/absu.txt
 done
