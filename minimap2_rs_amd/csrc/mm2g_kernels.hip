@@ -1197,6 +1197,11 @@ DEVI void radix_range(uint64_t* src, uint64_t* dst, uint64_t* out, uint32_t A, u
     __syncthreads();
 }
 
+// GL: the group offsets stay in HBM (2 n_seq + 2 > GOFF_LDS).  A template
+// parameter rather than a pointer chosen at run time: a pointer that may be
+// LDS or global compiles to flat loads, and every flat load waits for all
+// outstanding global loads and stores (vmcnt(0)), which serialised P1/P2 per key.
+template <bool GL>
 __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t red[32];
@@ -1226,16 +1231,15 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
     uint64_t* O = a.tmp + base;       // sorted output
     const bool filt = a.cells != 0;
     const uint32_t ng = 2u * a.n_seq + 2u;
-    const uint32_t* goff = a.goff;
-    if (filt && ng <= (uint32_t)GOFF_LDS) {
-        for (uint32_t i = tid; i < ng; i += 1024) s_goff[i] = a.goff[i];
-        goff = s_goff;
+    if (!GL && filt) {
+        for (uint32_t i = tid; i < ng && i < (uint32_t)GOFF_LDS; i += 1024) s_goff[i] = a.goff[i];
     }
     if (tid == 0) { s_nbig = 0; s_kept = 0; }
     __syncthreads();
     // cell of a key (every group incl. the Q19 pseudo-group 2 * n_seq has cells)
     auto cell_of = [&](uint64_t x) -> uint32_t {
-        return goff[(uint32_t)(x >> gsh)] + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
+        const uint32_t g = (uint32_t)(x >> gsh);
+        return (GL ? a.goff[g] : s_goff[g]) + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
     };
     const uint32_t nw = (a.cells + 31) >> 5;
     const uint32_t LW = a.lds_words;
@@ -1248,10 +1252,26 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
         // ---- P1: seen / seen-twice bitmaps
         for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
         __syncthreads();
-        block_pass8<SORT_U1>(K, A0, [&](uint32_t, uint64_t x) {
-            const uint32_t c = cell_of(x), w = c >> 5, bit = 1u << (c & 31);
-            if (atomicOr(&B1[w], bit) & bit) atomicOr(&B2[w], bit);   // seen before: seen twice
-        });
+        // staged per group of SORT_U1 keys: all cells, then all first atomics
+        // (LDS round trips overlap instead of one chain per key)
+        for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U1) {
+            uint64_t x[SORT_U1];
+            uint32_t c[SORT_U1], old[SORT_U1];
+#pragma unroll
+            for (int u = 0; u < SORT_U1; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
+#pragma unroll
+            for (int u = 0; u < SORT_U1; ++u) c[u] = cell_of(x[u]);
+#pragma unroll
+            for (int u = 0; u < SORT_U1; ++u) {
+                const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
+                old[u] = i < A0 ? atomicOr(&B1[c[u] >> 5], 1u << (c[u] & 31)) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < SORT_U1; ++u) {
+                const uint32_t i = i0 + (uint32_t)u * 1024 + tid, bit = 1u << (c[u] & 31);
+                if (i < A0 && (old[u] & bit)) atomicOr(&B2[c[u] >> 5], bit);   // seen before: seen twice
+            }
+        }
         __syncthreads();
         // ---- KC (in place of B2) and the word prefix of its popcounts (in place of B1)
         const uint32_t per = (nw + 1023) >> 10;
@@ -1284,11 +1304,6 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
             uint64_t* S = dyn64;
             for (uint32_t i = tid; i < cw; i += 1024) C[i] = 0;
             __syncthreads();
-            auto rank_of = [&](uint32_t c, bool& kept) -> uint32_t {
-                const uint32_t w = c >> 5, b = c & 31, kw = B2[w];
-                kept = (kw >> b) & 1u;
-                return B1[w] + (uint32_t)__popc(kw & ((1u << b) - 1u));
-            };
             auto c16 = [&](uint32_t rk) -> uint32_t { return (C[rk >> 1] >> ((rk & 1) << 4)) & 0xffffu; };
             // ---- P2: counts per kept cell; the largest dropped key.  Each key's
             // kept-cell rank (0xffff = dropped) goes to the u16 tag array T16 in
@@ -1296,14 +1311,30 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
             // the bitmaps can be overwritten by the first window).
             uint64_t smx = 0;
             uint16_t* T16 = (uint16_t*)(a.meta + base);
-            block_pass8<SORT_U2>(K, A0, [&](uint32_t i, uint64_t x) {
-                bool kept;
-                const uint32_t rk = rank_of(cell_of(x), kept);
-                if (kept) atomicAdd(&C[rk >> 1], 1u << ((rk & 1) << 4));
-                else smx = x + 1 > smx ? x + 1 : smx;
-                T16[i] = kept ? (uint16_t)rk : (uint16_t)0xffffu;
-            });
-            smx = block_max64(smx, red);
+            // staged like P1: all cells, all bitmap reads, then counts and tags
+            for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U2) {
+                uint64_t x[SORT_U2];
+                uint32_t c[SORT_U2], kw[SORT_U2], pw[SORT_U2];
+#pragma unroll
+                for (int u = 0; u < SORT_U2; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
+#pragma unroll
+                for (int u = 0; u < SORT_U2; ++u) c[u] = cell_of(x[u]);
+#pragma unroll
+                for (int u = 0; u < SORT_U2; ++u) { kw[u] = B2[c[u] >> 5]; pw[u] = B1[c[u] >> 5]; }
+#pragma unroll
+                for (int u = 0; u < SORT_U2; ++u) {
+                    const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
+                    if (i < A0) {
+                        const uint32_t b = c[u] & 31;
+                        const bool kept = (kw[u] >> b) & 1u;
+                        const uint32_t rk = pw[u] + (uint32_t)__popc(kw[u] & ((1u << b) - 1u));
+                        if (kept) atomicAdd(&C[rk >> 1], 1u << ((rk & 1) << 4));
+                        else smx = x[u] + 1 > smx ? x[u] + 1 : smx;
+                        T16[i] = kept ? (uint16_t)rk : (uint16_t)0xffffu;
+                    }
+                }
+            }
+            smx = block_max64(smx, red);               // (its barriers also end the count atomics)
             // exclusive scan of the u16 counts, in place (offsets < A0 <= 65535)
             const uint32_t per2 = (cw + 1023) >> 10;
             const uint32_t ca = min(cw, (uint32_t)tid * per2), cb = min(cw, ca + per2);
@@ -1482,6 +1513,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
 // table, a key layout the 32-bit windows cannot hold, too many kept cells for
 // the LDS, or cell segments beyond SEG_RANK), with the bitmap singleton filter
 // when cells exist.  One workgroup per listed read (grid-stride over the list).
+template <bool GL>   // as k_sort_read: group offsets in HBM (true) or LDS, never a flat pointer
 __global__ __launch_bounds__(1024) void k_sort_radix(SortArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;
     __shared__ uint64_t red[32];
@@ -1495,13 +1527,12 @@ __global__ __launch_bounds__(1024) void k_sort_radix(SortArgs a) {
     const uint64_t rmask = (1ULL << a.rb) - 1;
     const bool filt = a.cells != 0;
     const uint32_t ng = 2u * a.n_seq + 2u;
-    const uint32_t* goff = a.goff;
-    if (filt && ng <= (uint32_t)GOFF_LDS) {
-        for (uint32_t i = tid; i < ng; i += 1024) s_goff[i] = a.goff[i];
-        goff = s_goff;
+    if (!GL && filt) {
+        for (uint32_t i = tid; i < ng && i < (uint32_t)GOFF_LDS; i += 1024) s_goff[i] = a.goff[i];
     }
     auto cell_of = [&](uint64_t x) -> uint32_t {
-        return goff[(uint32_t)(x >> gsh)] + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
+        const uint32_t g = (uint32_t)(x >> gsh);
+        return (GL ? a.goff[g] : s_goff[g]) + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
     };
     const uint32_t nw = (a.cells + 31) >> 5;
     uint32_t* B1 = dyn;
@@ -2244,8 +2275,11 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                         stb = st;
                         skv = i0 + 63;
                         const int32_t j = stb + lane;
-                        sk = 0;
-                        if (j < e) sk = j >= ring_lo ? rkey[j & (RK - 1)] : K[j];
+                        // two loads and a select, not a select of pointers (a flat
+                        // load would wait for every outstanding global load)
+                        const uint64_t sr = rkey[j & (RK - 1)];
+                        const uint64_t sg = (j < e && j < ring_lo) ? K[j] : 0;
+                        sk = j < e ? (j >= ring_lo ? sr : sg) : 0;
                     }
                     const int32_t j = stb + lane;
                     const int32_t pj = (int32_t)((sk >> qb) & rmask);
@@ -3212,11 +3246,13 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
         lds = std::min<size_t>(lds, (size_t)SORT_LDS);
         SortArgs b = a;
         b.lds_words = (uint32_t)(lds / 4);
-        hipLaunchKernelGGL(k_sort_read, dim3(a.n), dim3(1024), lds, st, b);
+        if (2u * b.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_read<true>, dim3(a.n), dim3(1024), lds, st, b);
+        else hipLaunchKernelGGL(k_sort_read<false>, dim3(a.n), dim3(1024), lds, st, b);
     } else {
         const size_t hb = (size_t)(RS_MAXP + 16) * RS_ND * 4;
         const size_t lds = std::min<size_t>(std::max<size_t>(bmb, hb), (size_t)SORT_LDS);
-        hipLaunchKernelGGL(k_sort_radix, dim3(std::min<uint32_t>(a.n, 512)), dim3(1024), lds, st, a);
+        if (2u * a.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_radix<true>, dim3(std::min<uint32_t>(a.n, 512)), dim3(1024), lds, st, a);
+        else hipLaunchKernelGGL(k_sort_radix<false>, dim3(std::min<uint32_t>(a.n, 512)), dim3(1024), lds, st, a);
     }
     LAUNCH_CHECK();
     return 0;
