@@ -20,11 +20,15 @@ mid_occ are outside the timed region.  The rate with reads already resident
 in HBM is reported in `extra`.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py
---gpus N): one process per GPU with its own reads (weak scaling, no
-collective on the data path); rank 0 builds the index once and the other
-ranks load its .mmi from /dev/shm; barrier + synchronize around the timed
-region, max-over-ranks time, value = all ranks' bases / that time; a
-sample of every rank's reads is checked against the oracle on rank 0.
+--gpus N, or plain `python bench.py --gpus N`, which starts the N rank
+processes itself before anything touches a GPU): one process per GPU with its
+own reads (weak scaling, no collective on the data path); rank 0 generates
+the reference once and shares it through /dev/shm, builds the index once and
+the other ranks load its .mmi from there; barrier + synchronize around the
+timed region, max-over-ranks time, value = all ranks' bases / that time; a
+sample of every rank's reads is checked against the oracle on rank 0.  A
+rank count that does not match --gpus, or more RCCL ranks than visible GPUs,
+is an error, never a silent 1-GPU run.
 
 Output: ONE JSON line on rank 0 with the driver contract fields plus
 "roofline" (dominant kernel, HIP events on the library stream) and
@@ -41,6 +45,7 @@ import json
 import os
 import socket
 import statistics
+import subprocess
 import sys
 import threading
 import time
@@ -52,6 +57,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_COPY_GBS = 6290.0          # measured copy bandwidth (same guide)
+VALU_INT32_OPS = 7.9e13        # 256 CU x 128 lanes/clk x 2.4 GHz
+OPS_PER_PAIR = 15              # int32 ops per DP pair evaluation
+SORT_CELL_MAX = 65535          # reads with more anchors take the large-read sort (k_sort_big)
 SORT_SMALL = 4096              # reads up to this many anchors are sorted by k_sort_small (mm2g_kernels.hip)
 
 # numpy view of mm2g_read_result (include/mm2g.h, 72 B)
@@ -87,6 +95,8 @@ def parse(argv=None):
     p.add_argument("--resident-steps", type=int, default=3, help="extra: steps re-mapping reads already in HBM")
     p.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
                    help="context knob for A/B runs (include/mm2g.h MM2G_KNOB_*), e.g. sort_prof=1")
+    p.add_argument("--index-knob", action="append", default=[], metavar="NAME=VALUE",
+                   help="process-wide index-build knob (include/mm2g.h MM2G_IKNOB_*), e.g. force_fallback=1")
     p.add_argument("--streams", type=int, default=4,
                    help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index")
     p.add_argument("--shares", type=int, default=2,
@@ -123,13 +133,80 @@ def reduce_step_time(dist, elapsed: float, n_bases: int, world: int, device):
     return float(tt.item()), float(bt.item())
 
 
-def count_devices(dist, world: int, gpu: int) -> int:
+def device_identity(gpu: int) -> str:
+    """A stable name of the GPU this rank drives (UUID where torch exposes it)."""
+    import torch
+    try:
+        pr = torch.cuda.get_device_properties(gpu)
+        u = getattr(pr, "uuid", None)
+        if u:
+            return str(u)
+        return f"{getattr(pr, 'pci_domain_id', '?')}:{getattr(pr, 'pci_bus_id', '?')}:{getattr(pr, 'pci_device_id', gpu)}"
+    except Exception:
+        return f"dev{gpu}"
+
+
+def count_devices(dist, world: int, ident) -> int:
     """Distinct (host, device) pairs over the ranks: n_gpus counts GPUs, not ranks."""
     if world <= 1:
         return 1
     got = [None] * world
-    dist.all_gather_object(got, (socket.gethostname(), gpu))
+    dist.all_gather_object(got, (socket.gethostname(), ident))
     return len(set(got))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def rank_env(argv_gpus: int, env=None):
+    """(rank, world, local_rank) from the launcher's environment, checked
+    against --gpus: a mismatch is an error, never a silent smaller run."""
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", str(rank)))
+    if world != argv_gpus:
+        raise SystemExit(f"bench.py: --gpus {argv_gpus} but the launcher started WORLD_SIZE={world} ranks; "
+                         f"run `python bench.py --gpus {argv_gpus}` (it starts the ranks itself) or "
+                         f"`python -m torch.distributed.run --nproc-per-node {argv_gpus} bench.py --gpus {argv_gpus}`")
+    return rank, world, local
+
+
+def spawn_ranks(n: int, argv, backend: str, ndev: int, cmd=None) -> int:
+    """`--gpus N` (N > 1) without a launcher: start the N rank processes of this
+    script as fresh children (this process never touches a GPU, so nothing is
+    exec'd from a GPU process), with the environment torch.distributed.run
+    gives them, and wait.  Rank 0 prints the line.  One failing rank stops the
+    others; the exit code is the first failure's."""
+    if backend == "nccl" and ndev < n:
+        raise SystemExit(f"bench.py: --gpus {n} needs {n} GPUs for {n} RCCL ranks, {ndev} visible "
+                         f"(MM2G_DIST_BACKEND=gloo rehearses {n} ranks on fewer GPUs)")
+    port = free_port()
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), MM2G_BENCH_SPAWNED="1")
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)]
+    procs = [subprocess.Popen(list(cmd) + list(argv), env=dict(base, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    log(f"started {n} rank processes (pids {[p.pid for p in procs]}, master 127.0.0.1:{port})")
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            c = p.poll()
+            if c is None:
+                continue
+            alive.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                log(f"rank process {p.pid} exited with {c}; stopping the others")
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
 
 
 def paf_lines_by_read(paf: bytes):
@@ -154,20 +231,29 @@ def bench_config_tag(args) -> str:
     return f"reads={args.reads},read_len={args.read_len},streams={max(1, args.streams)},shares={args.shares},scale={args.scale},preset={args.preset}"
 
 
-def pmc_traffic(kernel: str, tag: str):
+def pmc_traffic(kernel: str, hint: str, tag: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, tools/pmc_traffic.py: 2 x FETCH_SIZE +
     WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md §HBM) when they
-    were taken with this bench configuration on these kernel sources; else None."""
+    were taken with this bench configuration on these kernel sources; else
+    None.  Template instantiations are separate rows: `hint` picks the one the
+    mapping path runs (e.g. SeqNt4 for the query sketch).
+    -> (bytes per launch, row name) or (None, None)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             t = json.load(fh)
         if t.get("bench_config") != tag or t.get("kernels_sha") != kernel_sha():
-            return None
-        return t["kernels"][kernel]["hbm_bytes_per_launch"]
+            return None, None
+        rows = {k: v for k, v in t["kernels"].items() if k.split("<")[0] == kernel}
+        if len(rows) > 1 and hint:
+            rows = {k: v for k, v in rows.items() if hint in k}
+        if len(rows) != 1:
+            return None, None
+        (k, v), = rows.items()
+        return v["hbm_bytes_per_launch"], k
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 def host_threads(world: int) -> int:
@@ -202,21 +288,118 @@ def make_batches(gbuf, lens, args, rank, n_batches, threads):
         return list(ex.map(one, range(n_batches)))
 
 
+def shared_genome(args, dist, rank: int, world: int, thr: int, tag: str):
+    """The synthetic reference.  With several ranks, rank 0 generates it once and
+    shares it through /dev/shm (the others map the file read-only) instead of
+    every rank regenerating 3.1 Gb; if /dev/shm has no room, each rank generates
+    its own (the same seeded bytes)."""
+    from tools import simdata
+    if world <= 1:
+        return simdata.genome(args.preset, args.scale, args.ref_seed, threads=thr)
+    path = f"/dev/shm/mm2g_bench_{tag}.genome"
+    meta = [None]
+    gbuf = None
+    if rank == 0:
+        names, lens, gbuf = simdata.genome(args.preset, args.scale, args.ref_seed, threads=thr)
+        ok = True
+        try:
+            gbuf.tofile(path)
+        except OSError as e:
+            log(f"rank 0: reference to {path} failed ({e}); every rank generates its own")
+            ok = False
+        meta = [(names, [int(x) for x in lens], ok)]
+    dist.broadcast_object_list(meta, src=0)
+    names, lens_l, ok = meta[0]
+    lens = np.array(lens_l, dtype=np.int64)
+    if rank != 0:
+        if ok:
+            gbuf = np.memmap(path, dtype=np.uint8, mode="r", shape=(int(lens.sum()),))
+        else:
+            names, lens, gbuf = simdata.genome(args.preset, args.scale, args.ref_seed, threads=thr)
+    dist.barrier()
+    if rank == 0 and ok:
+        os.unlink(path)          # the ranks' mappings keep the pages until they exit
+    return names, lens, gbuf
+
+
+# slot (mm2g_prof name) -> (kernel symbol, instantiation hint for the PMC rows)
+KERNEL_SYMBOLS = {
+    "mz_base": ("k_mz_base", ""), "sketch": ("k_sketch", "SeqNt4"), "scan": ("k_excl_scan", ""),
+    "filter": ("k_filter", ""), "seed_count": ("k_seed_count", ""), "seed_write": ("k_seed_write", ""),
+    "sort_small": ("k_sort_small", ""), "sort_large": ("k_sort_read", ""), "sort_radix": ("k_sort_radix", ""),
+    "sort_big": ("k_sort_big", ""),
+    "chain_items": ("k_seg_items", ""), "chain_lb": ("k_chain_lb", ""), "chain_seg": ("k_chain_seg", ""),
+    "chain_med": ("k_chain_med", ""), "chain_lorder": ("k_lseg_order", ""), "chain_long": ("k_chain_long", ""),
+    "chain_giant": ("k_chain_giant", ""), "chain_fin": ("k_chain_fin", ""),
+    "chain_items_rescue": ("k_seg_items", ""), "chain_seg_rescue": ("k_chain_seg", ""), "chain_med_rescue": ("k_chain_med", ""),
+    "chain_lorder_rescue": ("k_lseg_order", ""), "chain_giant_rescue": ("k_chain_giant", ""),
+    "chain_long_rescue": ("k_chain_long", ""), "chain_fin_rescue": ("k_chain_fin", ""), "dv": ("k_dv", ""),
+}
+CHAIN_SLOTS = {k for k in KERNEL_SYMBOLS if k.startswith("chain_")}
+
+
+def alg_bytes(cnt: dict, res) -> dict:
+    """Algorithmic HBM bytes of every kernel slot over the mapped batches
+    (SURVEY.md §8d per-anchor terms).  cnt: summed
+    mm2g_batch_counters, res: the per-read results (RES_DTYPE).
+    Sorts are priced at 16 B per anchor (each key read once and written once),
+    whatever passes an implementation makes; chain kernels at 8 B of key in and
+    8 B of f/pprev out per anchor of the segments they process."""
+    n = len(res)
+    A, m, mk, L = cnt["anchors"], cnt["minimizers"], cnt["kept_minimizers"], cnt["bases"]
+    Adp = cnt.get("dp_anchors", A)
+    na = res["n_anchors"].astype(np.int64)
+    mapped = (res["flags"] & 1) != 0
+    cm = int(res["cm"][mapped].astype(np.int64).sum())
+    mdv = int(res["m_dv"][mapped].astype(np.int64).sum())
+    return {
+        "mz_base": 24 * n,
+        "sketch": (L + 3) // 4 + 12 * m,                 # nt4 codes in; (x 8 B, y 4 B) per minimizer out
+        "scan": 24 * n,                                   # two scans: u32 in, u64 out per read
+        "filter": 9 * m,                                  # x in, keep flag out
+        "seed_count": 9 * m + 16 * mk + 8 * m,            # keep+x in, 16 B table entry per kept, (n, poff) out
+        "seed_write": 12 * m + 16 * A,                    # (n, poff, y) in; 8 B position in + 8 B key out per anchor
+        "sort_small": 16 * int(na[(na > 1) & (na <= SORT_SMALL)].sum()),
+        "sort_large": 16 * int(na[(na > SORT_SMALL) & (na <= SORT_CELL_MAX)].sum()),
+        "sort_radix": 16 * int(na[na > SORT_CELL_MAX].sum()),
+        "sort_big": 16 * int(na[na > SORT_CELL_MAX].sum()),
+        "chain_items": 8 * n,
+        "chain_lb": 8 * Adp,
+        "chain_seg": 8 * Adp,
+        "chain_med": 16 * cnt.get("med_anchors", 0),
+        "chain_lorder": 0,
+        "chain_long": 16 * cnt.get("long_anchors", 0),
+        "chain_giant": 16 * cnt.get("giant_anchors", 0),
+        "chain_fin": 96 * n + 8 * cm,
+        "chain_items_rescue": 8 * n,
+        "chain_seg_rescue": 8 * cnt["rescued_anchors"],
+        "chain_med_rescue": 16 * cnt.get("med_anchors_rescue", 0),
+        "chain_lorder_rescue": 0,
+        "chain_giant_rescue": 16 * cnt.get("giant_anchors_rescue", 0),
+        "chain_long_rescue": 16 * cnt.get("long_anchors_rescue", 0),
+        "chain_fin_rescue": 96 * n,
+        "dv": 8 * cm + 4 * mdv,
+    }
+
+
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    backend = os.environ.get("MM2G_DIST_BACKEND", "nccl")   # gloo: rehearse more ranks than GPUs
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import torch
+        ndev = torch.cuda.device_count()       # counts devices without initialising HIP on this image
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:], backend, ndev))
+    rank, world, local = rank_env(args.gpus)
 
     import torch
     import torch.distributed as dist
 
-    # one process per GPU; MM2G_DIST_BACKEND=gloo rehearses the launch on fewer GPUs
-    backend = os.environ.get("MM2G_DIST_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > max(ndev, 1) and ndev >= 1:
+        raise SystemExit(f"bench.py: {world} RCCL ranks but {ndev} GPU(s) visible: one rank per GPU "
+                         f"(MM2G_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
     gpu = local % max(ndev, 1)
+    coll_seen = None
     if world > 1:
         torch.cuda.set_device(gpu)
         if backend == "nccl":
@@ -224,61 +407,36 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = "cuda" if backend == "nccl" else "cpu"
+    if world > 1:
+        one = torch.ones(1, dtype=torch.float64, device=red_dev)
+        dist.all_reduce(one)                  # the ranks the collective backend actually joined
+        coll_seen = int(one.item())
+        if coll_seen != world:
+            raise SystemExit(f"bench.py: {dist.get_backend()} all-reduce saw {coll_seen} ranks, expected {world}")
 
     import minimap2_rs_amd as M
     from minimap2_rs_amd import _lib as L
-    from tools import simdata
 
     lib = L.load()                               # libmm2g.so (fails loudly if missing)
     if lib.mm2g_device_count() <= 0:
         raise SystemExit("bench.py: no HIP device visible")
     thr = args.threads or host_threads(world)
-    n_gpus = count_devices(dist, world, gpu)
+    for kv in args.index_knob:
+        k, v = kv.split("=", 1)
+        M.set_index_knob(k, int(v))
+    ident = device_identity(gpu)
+    n_gpus = count_devices(dist, world, ident)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    # ---- reference + index (outside the timed region) ----------------------
+    # ---- reference, read batches, index (outside the timed region) ----------
+    tag = os.environ.get("MASTER_PORT", "0")
     t0 = time.time()
-    names, lens, gbuf = simdata.genome(args.preset, args.scale, args.ref_seed, threads=thr)
+    names, lens, gbuf = shared_genome(args, dist, rank, world, thr, tag)
     log(f"rank {rank}: reference {lens.sum() / 1e9:.3f} Gb, {len(lens)} contigs in {time.time() - t0:.1f}s")
-    t0 = time.time()
-    idx, index_from = None, "gpu build"
-    shm = f"/dev/shm/mm2g_bench_{os.environ.get('MASTER_PORT', '0')}.mmi"
-    if rank == 0 or world == 1:
-        # GPU index build (SURVEY.md §8f row 1; byte-identical to the oracle's, tests/test_gpu_parity.py)
-        idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr,
-                                        device=None if args.host_index else gpu)
-        index_from = "host build" if args.host_index else "gpu build"
-    if world > 1:
-        ok = False
-        if rank == 0:
-            try:
-                idx.save_to_mmi(shm)
-                ok = True
-            except Exception as e:   # no room in /dev/shm: every rank builds its own
-                log(f"rank 0: .mmi to {shm} failed ({e}); ranks build their own index")
-        flag = [None] * world
-        dist.all_gather_object(flag, ok)
-        if rank != 0:
-            if flag[0]:
-                idx = M.Index.load_from_mmi(shm)        # mapped, bucket-parallel load (SURVEY.md §8f row 2)
-                index_from = "rank 0's .mmi (/dev/shm)"
-            else:
-                idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr,
-                                                device=None if args.host_index else gpu)
-        dist.barrier()
-        if rank == 0 and ok:
-            os.unlink(shm)
-    t_index = time.time() - t0
-    t0 = time.time()
-    mid_host = idx.calc_mid_occ(2e-4)            # the reference's sort of all counts (index.rs:124-141)
-    t_mid_host = time.time() - t0
-    log(f"rank {rank}: index from {index_from} in {t_index:.1f}s, stats {idx.stats()}")
-
-    # ---- reads: W+K distinct batches per rank, ASCII in host RAM ------------
     # warmup: W steps, and at least one unit per context (each context's first
     # unit allocates its workspaces; with W * P < S some would pay that in the timed region)
     S_ctx = max(1, args.streams)
@@ -288,6 +446,38 @@ def main():
     batches = make_batches(gbuf, lens, args, rank, n_batches, thr)
     bases_per_batch = [int(b[1][-1]) for b in batches]
     log(f"rank {rank}: {n_batches} batches x {args.reads} reads generated in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    idx = None
+    shm = f"/dev/shm/mm2g_bench_{tag}.mmi"
+    if rank == 0 or world == 1:
+        # GPU index build (SURVEY.md §8f row 1; byte-identical to the oracle's, tests/test_gpu_parity.py)
+        idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr,
+                                        device=None if args.host_index else gpu)
+    if world > 1:
+        ok = False
+        if rank == 0:
+            try:
+                idx.save_to_mmi(shm)
+                ok = True
+            except Exception as e:   # no room in /dev/shm: every rank builds its own
+                log(f"rank 0: .mmi to {shm} failed ({e}); ranks build their own index")
+        flag = [ok]
+        dist.broadcast_object_list(flag, src=0)
+        if rank != 0:
+            if flag[0]:
+                idx = M.Index.load_from_mmi(shm)        # mapped, bucket-parallel load (SURVEY.md §8f row 2)
+            else:
+                idx = M.Index.build_from_buffer(names, gbuf, lens, w=10, k=15, b=14, flag=0, threads=thr,
+                                                device=None if args.host_index else gpu)
+        dist.barrier()
+        if rank == 0 and ok:
+            os.unlink(shm)
+    index_from, index_note = idx.origin               # what actually happened (mm2g_index_origin)
+    t_index = time.time() - t0
+    t0 = time.time()
+    mid_host = idx.calc_mid_occ(2e-4)            # the reference's sort of all counts (index.rs:124-141)
+    t_mid_host = time.time() - t0
+    log(f"rank {rank}: index from {index_from}{' (' + index_note + ')' if index_note else ''} in {t_index:.1f}s, stats {idx.stats()}")
 
     S = max(1, args.streams)
     devs = [M.Device(gpu) for _ in range(S)]
@@ -310,6 +500,7 @@ def main():
     devs[0].set_mid_occ(mid)
     for d in devs[1:]:
         d.share_index(devs[0], mid)
+    idx.release_tables()                         # the device copy is made: keep only names/lengths on the host
     log(f"rank {rank}: index upload {t_up:.1f}s ({S} contexts share it), mid_occ {mid} "
         f"(device {t_mid_dev * 1e3:.1f} ms, host sort {t_mid_host * 1e3:.0f} ms)")
 
@@ -435,39 +626,47 @@ def main():
     value = all_bases / elapsed / 1e9
     ms_per_step = elapsed / max(args.steps, 1) * 1e3
 
-    # ---- roofline of the dominant kernel (HIP events on the library stream) --
-    # Algorithmic bytes per launch.
-    A, Ar, m, mk = cnt["anchors"], cnt["rescued_anchors"], cnt["minimizers"], cnt["kept_minimizers"]
-    L_tot = cnt["bases"]
-    na = res_np["n_anchors"].astype(np.int64)
-    A_large = int(na[na > SORT_SMALL].sum())
-    A_small = int(na[(na > 1) & (na <= SORT_SMALL)].sum())
-    kernel_bytes = {   # slot -> (kernel symbol, algorithmic bytes over the timed steps)
-        "sketch": ("k_sketch", (L_tot + 3) // 4 + 12 * m),  # nt4 codes in; (x 8 B, y 4 B) per minimizer out
-        "filter": ("k_filter", 9 * m),                       # x in, keep flag out
-        "seed_count": ("k_seed_count", 9 * m + 16 * mk + 8 * m),   # keep+x in, 16 B table entry per kept, (n, poff) out
-        "seed_write": ("k_seed_write", 12 * m + 16 * A),     # (n, poff, y) in; 8 B position in + 8 B key out per anchor
-        "sort_small": ("k_sort_small", 16 * A_small),        # each 8 B key read once and written once
-        "sort_large": ("k_sort_read", 16 * A_large),
-        "chain_seg": ("k_chain_seg", 8 * A),                 # every key read once (segmenting)
-        "dv": ("k_dv", 0),
-    }
+    # ---- roofline of the dominant kernel (HIP events on the library streams) --
+    # Every kernel slot is priced (alg_bytes); the dominant one is the slot with
+    # the most device time over the timed region, whatever it is.
+    kb = alg_bytes(cnt, res_np)
     per_kernel = {}
     for name, (ms, calls) in prof.items():
         if calls > 0:
-            per_kernel[name] = {"ms_per_step": round(ms / args.steps, 4), "launches_per_step": calls / args.steps}
-    cand = {k: v for k, v in prof.items() if k in kernel_bytes and kernel_bytes[k][1] > 0 and v[1] > 0}
-    dom = max(cand, key=lambda k: cand[k][0])
-    d_ms, d_calls = cand[dom]
-    d_sym, d_bytes = kernel_bytes[dom]
+            b = kb.get(name)
+            avg_s = ms / 1e3 / calls
+            e = {"ms_per_step": round(ms / args.steps, 4), "launches_per_step": calls / args.steps}
+            if b is not None and avg_s > 0:
+                e["alg_GBps"] = round(b / calls / avg_s / 1e9, 2)
+                e["hbm_frac"] = round(b / calls / avg_s / 1e9 / HBM_PEAK_GBS, 5)
+            per_kernel[name] = e
+    timed_slots = {k: v for k, v in prof.items() if v[1] > 0}
+    dom = max(timed_slots, key=lambda k: timed_slots[k][0])
+    d_ms, d_calls = timed_slots[dom]
+    d_sym, d_hint = KERNEL_SYMBOLS.get(dom, (dom, ""))
+    d_bytes = kb.get(dom, 0)
     avg_s = d_ms / 1e3 / max(d_calls, 1)
     bytes_per_launch = d_bytes / max(d_calls, 1)
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic = pmc_traffic(d_sym, bench_config_tag(args))
+    traffic, traffic_row = pmc_traffic(d_sym, d_hint, bench_config_tag(args))
+    chain_ms = sum(v[0] for k, v in timed_slots.items() if k in CHAIN_SLOTS)
+    pair_peak = VALU_INT32_OPS / OPS_PER_PAIR
     roofline = {
-        "bound": "hbm", "kernel": d_sym, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+        "bound": "hbm", "kernel": d_sym, "slot": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_row": traffic_row,
         "avg_launch_ms": round(avg_s * 1e3, 4), "alg_bytes_per_launch": int(bytes_per_launch),
+        "share_of_kernel_time": round(d_ms / max(sum(v[0] for v in timed_slots.values()), 1e-9), 4),
+        # SURVEY.md §8d secondary figure: DP pair evaluations against the int32 VALU rate at 15 ops per pair
+        "compute": {"dp_pairs_per_step": cnt["dp_pairs"] / args.steps,
+                    "pairs_per_s_wall": round(cnt["dp_pairs"] / elapsed, 1) if world == 1 else None,
+                    "pairs_per_s_in_chain_kernels": round(cnt["dp_pairs"] / (chain_ms / 1e3), 1) if chain_ms > 0 else None,
+                    "peak_pairs_per_s": pair_peak,
+                    "frac_wall": round(cnt["dp_pairs"] / elapsed / pair_peak, 6) if world == 1 else None,
+                    "note": "peak = 7.9e13 int32 ops/s / 15 ops per pair (SURVEY.md §8d); chain-kernel time overlaps "
+                            "other contexts' kernels, so the in-kernel rate is a lower bound"},
+        "seed_lookup_floor_bytes_per_step": 128 * cnt["kept_minimizers"] // args.steps,
+        "seed_lookup_note": "a hashed-table probe reads at least one 128-B request per kept minimizer "
+                            "(MI355X_MICROARCH.md: 128-B requests), against 16 B of table entry priced as algorithmic",
     }
     # The same kernel on a quiet GPU: one context maps one batch's units one
     # after another (after the timed region), so its launches share the GPU with
@@ -479,25 +678,28 @@ def main():
         us0 = units[:P]
         d0.prof_reset()
         d0.prof_enable(True)
-        a_iso = 0
+        cnt_i = {}
+        res_i = []
         for u in us0:
             rb = batches[u["b"]][0]
             L.check(lib.mm2g_batch_set_reads(d0._h, rb.ctypes.data_as(C.c_void_p), u["offs"].ctypes.data_as(L._P64), u["n"]), "set_reads")
             L.check(lib.mm2g_batch_map(d0._h, C.byref(opts)), "batch_map")
             L.check(lib.mm2g_batch_results(d0._h, u["res"], u["n"]), "batch_results")
-            na_u = np.frombuffer(u["res"], dtype=RES_DTYPE, count=u["n"])["n_anchors"].astype(np.int64)
-            a_iso += int(na_u[na_u > SORT_SMALL].sum()) if dom == "sort_large" else 0
+            for k, v in d0.counters().items():
+                cnt_i[k] = cnt_i.get(k, 0) + v
+            res_i.append(np.frombuffer(u["res"], dtype=RES_DTYPE, count=u["n"]).copy())
         pi = d0.prof()
         d0.prof_enable(False)
         if dom in pi and pi[dom][1] > 0:
             i_ms, i_calls = pi[dom]
             i_avg = i_ms / 1e3 / i_calls
-            i_bytes = (16 * a_iso / i_calls) if dom == "sort_large" else bytes_per_launch
+            i_bytes = alg_bytes(cnt_i, np.concatenate(res_i)).get(dom, 0) / i_calls
             i_ach = i_bytes / i_avg / 1e9
             iso = {"kernel": d_sym, "avg_launch_ms": round(i_avg * 1e3, 4), "alg_bytes_per_launch": int(i_bytes),
                    "achieved": round(i_ach, 3), "frac": round(i_ach / HBM_PEAK_GBS, 6),
                    "note": "one context, one batch's units mapped back to back after the timed region (no other kernels on the GPU)"}
     # whole-path algorithmic bytes (SURVEY.md §8d B(read) summed) over the step time
+    A, Ar, mk, L_tot = cnt["anchors"], cnt["rescued_anchors"], cnt["kept_minimizers"], cnt["bases"]
     B_path = (L_tot + 3) // 4 + 16 * mk + 48 * A + 24 * Ar
     path_gbs = B_path / elapsed / 1e9 if world == 1 else None
     dp_pairs_s = cnt["dp_pairs"] / elapsed if world == 1 else None
@@ -532,7 +734,12 @@ def main():
                             f"{args.reads}x{args.read_len // 1000} kb ONT reads per GPU per step, from host RAM "
                             f"(nt4 pack + H2D + map + PAF in the timed region)",
                 "reads_per_gpu_step": args.reads, "read_len": args.read_len, "ref_bases": int(lens.sum()),
-                "distinct_batches": n_batches, "mid_occ": mid, "ranks": world,
+                "distinct_batches": n_batches, "mid_occ": mid,
+                "ranks": world, "distinct_devices": n_gpus,
+                "collective_backend": (dist.get_backend() if world > 1 else None),
+                "collective_world_seen": coll_seen if world > 1 else 1,
+                "launch": ("self-spawned ranks" if os.environ.get("MM2G_BENCH_SPAWNED") else
+                           ("torch.distributed.run" if world > 1 else "single process")),
                 "parallelism": f"reads sharded x{world} (index replicated), {S} streams per GPU, {P} units per batch",
             },
             "roofline": roofline,
@@ -546,7 +753,7 @@ def main():
                 "path_alg_GBps": round(path_gbs, 3) if path_gbs else None,
                 "path_frac_of_8TBps": round(path_gbs / HBM_PEAK_GBS, 6) if path_gbs else None,
                 "dp_pairs_per_s": dp_pairs_s,
-                "index_build_s": round(t_index, 3), "index_from": index_from,
+                "index_build_s": round(t_index, 3), "index_from": index_from, "index_fallback_reason": index_note,
                 "index_upload_s": round(t_up, 3),
                 "mid_occ_device_ms": round(t_mid_dev * 1e3, 2), "mid_occ_host_sort_ms": round(t_mid_host * 1e3, 1),
                 "pack_threads_per_context": pack_thr,
@@ -624,11 +831,26 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
         oi.align_buffer(rnames, cat, offs, out, mid_occ=mid, threads=thr)
         cpu_lines = {ln.split(b"\t", 1)[0].decode(): ln for ln in open(out, "rb").read().splitlines()}
     paf_same = cpu_lines == gpu_paf
+    # paf.rs:178's binary_search as rustc 1.52-1.81 compiles it (the device and the
+    # oracle default follow >= 1.82): how many sampled reads would change
+    O.set_binary_search(True)
+    try:
+        with tempfile.TemporaryDirectory() as td:
+            out = os.path.join(td, "cpu_pre182.paf")
+            oi.align_buffer(rnames, cat, offs, out, mid_occ=mid, threads=thr)
+            pre_lines = {ln.split(b"\t", 1)[0].decode(): ln for ln in open(out, "rb").read().splitlines()}
+    finally:
+        O.set_binary_search(False)
+    bs_diff = sum(1 for k in set(cpu_lines) | set(pre_lines) if cpu_lines.get(k) != pre_lines.get(k))
     panics = int(((rec[:, 0] & 8) != 0).sum())
     parity = {"reads": len(seqs), "ranks_sampled": world, "identical": bool(paf_same and not diff),
               "paf_lines_identical": bool(paf_same), "gpu_lines": len(gpu_paf), "cpu_lines": len(cpu_lines),
               "per_read_outcome_identical": not diff, "per_read_outcome_diffs": diff[:10],
               "cpu_panics": panics,
+              "rustc_binary_search": {"assumed": ">= 1.82 (base/size halving)",
+                                      "reads_whose_paf_differs_under_1_52_to_1_81": bs_diff,
+                                      "note": "k = 15 is odd: minimizer positions are strictly increasing, so both std "
+                                              "algorithms agree (DESIGN.md §2); tests/golden/binsearch_even_k.json pins both at k = 16"},
               "note": "per-read outcome = chain flags, anchors, score, cm, q/t ranges, rid, strand; it covers the reads "
                       "on which the reference panics (Q19), which have no PAF line on either side"}
     cpu = None
@@ -652,7 +874,10 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
                          f"(their chaining cost is paid, only the PAF line is missing)",
                "runs_s": [round(x, 3) for x in t1],
                "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-               "all_cores": {"value": round(vN, 9), "cores": thr, "runs_s": [round(x, 3) for x in tN]}}
+               "all_cores": {"value": round(vN, 9), "cores": thr, "runs_s": [round(x, 3) for x in tN],
+                             "note": f"{thr} threads: the process's CPU affinity / OMP_NUM_THREADS share "
+                                     f"({len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else '?'} "
+                                     f"CPUs in the affinity set of {os.cpu_count()} on the host)"}}
     oi.close()
     return cpu, parity
 

@@ -76,6 +76,19 @@ int mm2g_index_seq(const mm2g_index* idx, uint32_t rid, const char** name, uint3
 /* Index::get (src/index.rs:143-154): *kind = 0 none, 1 Single, 2 Multi;
  * returns the number of positions (copies up to cap into out). */
 int64_t mm2g_index_get(const mm2g_index* idx, uint64_t minier, int* kind, uint64_t* out, int64_t cap);
+/* How this index came to be (the reference has one path, build_index_from_fasta
+ * src/index.rs:427-475, or load_from_mmi :361-424): returns an MM2G_IX_* value;
+ * *note (may be NULL) receives why a GPU build ran on the host, else NULL. */
+#define MM2G_IX_HOST 1          /* mm2g_index_build_fasta / _seqs                      */
+#define MM2G_IX_GPU 2           /* mm2g_index_build_*_gpu, built on the device          */
+#define MM2G_IX_GPU_FALLBACK 3  /* a GPU build the device could not do, built on the host */
+#define MM2G_IX_MMI 4           /* mm2g_index_load_mmi                                  */
+int mm2g_index_origin(const mm2g_index* idx, const char** note);
+/* Free the host hash tables and S of an index whose device copies are made
+ * (per GPU process only names, lengths and (w, k) are needed afterwards, for
+ * PAF and dv).  Later save/get/calc_mid_occ/upload calls fail with
+ * MM2G_E_STATE; stats keep their values. */
+int mm2g_index_release_tables(mm2g_index* idx);
 
 /* ---------------------------------------------------------------- device
  * One context per (host thread, device). */
@@ -85,6 +98,10 @@ void mm2g_ctx_destroy(mm2g_ctx* ctx);
  * array (DESIGN.md "Index layout").  mid_occ as computed by the caller
  * (main.rs:196-197: max(calc_mid_occ(-f), 10)). */
 int mm2g_ctx_upload_index(mm2g_ctx* ctx, const mm2g_index* idx, int32_t mid_occ);
+/* The same for n contexts (normally one per GPU: `mm2rs align --devices`):
+ * the host layout is built once and the devices' copies are made in parallel
+ * host threads. */
+int mm2g_ctx_upload_index_many(mm2g_ctx* const* ctxs, int n, const mm2g_index* idx, int32_t mid_occ);
 /* Use the device index of `src` (same device) in `dst` without another copy:
  * several contexts — one per host thread, each with its own stream and batch
  * buffers — map concurrently against one index in HBM. */
@@ -115,7 +132,7 @@ void mm2g_map_opts_default(mm2g_map_opts* o);
 #define MM2G_R_RESCUED 2   /* rescue_long_join re-ran the DP with bw_long     */
 #define MM2G_R_DV_FOUND 4  /* first chain position found among minimizers     */
 #define MM2G_R_PANIC 8     /* reference panics: chain on an odd-rid contig (Q19) */
-#define MM2G_R_EMPTY 16    /* empty read (reference asserts, src/sketch.rs:40) */
+#define MM2G_R_EMPTY 16    /* empty read (reference asserts, src/sketch.rs:30) */
 typedef struct {
     int32_t flags;
     int32_t n_anchors;
@@ -285,7 +302,8 @@ enum {
     MM2G_IKNOB_LOAD_THREADS = 3, /* .mmi load threads; 0 = min(32, cores) [0]                                 */
     MM2G_IKNOB_GPU_STRICT = 4,   /* tests: a GPU index build the device cannot do fails instead of falling
                                     back to the host build [0]                                               */
-    MM2G_IKNOB_COUNT = 5
+    MM2G_IKNOB_FORCE_FALLBACK = 5, /* tests: GPU index builds take the host fallback (MM2G_IX_GPU_FALLBACK) [0] */
+    MM2G_IKNOB_COUNT = 6
 };
 int mm2g_set_index_knob(int knob, int64_t value);
 
@@ -296,9 +314,11 @@ int mm2g_prof_get(mm2g_ctx* ctx, int i, const char** name, double* ms, int64_t* 
 int mm2g_prof_reset(mm2g_ctx* ctx);
 /* Batch counters for roofline accounting: [0]=bases [1]=minimizers
  * [2]=kept minimizers [3]=anchors [4]=rescued anchors [5]=dp pair evaluations
- * [6]=anchors entering the DP (after the sort's singleton filter).
+ * [6]=anchors entering the DP (after the sort's singleton filter); anchors in
+ * the DP's long segments below the giant-kernel size [7] / from it on [8] and
+ * in its medium segments [9] of pass 0, and [10], [11], [12] of the rescue pass.
  * Copies min(n, MM2G_N_COUNTERS) values; returns how many. */
-#define MM2G_N_COUNTERS 7
+#define MM2G_N_COUNTERS 13
 int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus

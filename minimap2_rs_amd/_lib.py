@@ -60,7 +60,9 @@ KNOBS = {"sort_small": 1, "seg_small": 2, "seg_chunk": 3, "giant_min": 4, "giant
          "giant_gblocks": 8, "filter": 9, "lazy": 10, "prune": 11, "giant": 12, "sketch_prof": 13, "sort_prof": 14,
          "lseg_prof": 15, "midhist_bins": 16, "sync_each": 17, "host_threads": 18, "ws_min": 19,
          "sort_lds_kb": 20, "stop_at": 21}
-INDEX_KNOBS = {"ixchunk": 1, "ixprof": 2, "load_threads": 3, "gpu_strict": 4}
+INDEX_KNOBS = {"ixchunk": 1, "ixprof": 2, "load_threads": 3, "gpu_strict": 4, "force_fallback": 5}
+# mm2g_index_origin values
+INDEX_ORIGINS = {1: "host build", 2: "gpu build", 3: "gpu build fell back to the host build", 4: ".mmi load"}
 
 _VP = C.c_void_p
 _P64 = C.POINTER(C.c_uint64)
@@ -88,6 +90,9 @@ SIGNATURES = {
     "mm2g_ctx_create": (C.c_int, [C.c_int, C.POINTER(_VP)]),
     "mm2g_ctx_destroy": (None, [_VP]),
     "mm2g_ctx_upload_index": (C.c_int, [_VP, _VP, C.c_int32]),
+    "mm2g_ctx_upload_index_many": (C.c_int, [C.POINTER(_VP), C.c_int, _VP, C.c_int32]),
+    "mm2g_index_origin": (C.c_int, [_VP, C.POINTER(C.c_char_p)]),
+    "mm2g_index_release_tables": (C.c_int, [_VP]),
     "mm2g_map_opts_default": (None, [C.POINTER(MapOpts)]),
     "mm2g_batch_set_reads": (C.c_int, [_VP, C.c_void_p, _P64, C.c_uint32]),
     "mm2g_batch_map": (C.c_int, [_VP, C.POINTER(MapOpts)]),

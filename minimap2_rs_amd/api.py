@@ -154,6 +154,18 @@ class Index:
         except Exception:
             pass
 
+    @property
+    def origin(self) -> Tuple[str, Optional[str]]:
+        """How the index was made (``mm2g_index_origin``): ("gpu build" | "host build" |
+        "gpu build fell back to the host build" | ".mmi load", reason of a fallback or None)."""
+        note = C.c_char_p()
+        o = check(load().mm2g_index_origin(self._h, C.byref(note)), "index_origin")
+        return L.INDEX_ORIGINS.get(o, f"unknown ({o})"), (note.value.decode() if note.value else None)
+
+    def release_tables(self) -> None:
+        """Free the host hash tables once the device copies exist (``mm2g_index_release_tables``)."""
+        check(load().mm2g_index_release_tables(self._h), "release_tables")
+
     def stats(self) -> Tuple[int, float, float, int]:
         a, d = C.c_uint64(), C.c_uint64()
         b, c = C.c_double(), C.c_double()
@@ -214,6 +226,14 @@ class Device:
     def upload_index(self, index: Index, mid_occ: int) -> None:
         check(load().mm2g_ctx_upload_index(self._h, index._h, mid_occ), "upload_index")
         self.index = index
+
+    @staticmethod
+    def upload_index_many(devs: Sequence["Device"], index: Index, mid_occ: int) -> None:
+        """One index copy per context (normally one per GPU), made in parallel host threads."""
+        arr = (C.c_void_p * max(len(devs), 1))(*[d._h.value for d in devs])
+        check(load().mm2g_ctx_upload_index_many(arr, len(devs), index._h, mid_occ), "upload_index_many")
+        for d in devs:
+            d.index = index
 
     def share_index(self, other: "Device", mid_occ: int) -> None:
         """Map against `other`'s device index (same GPU) without another copy."""
@@ -385,9 +405,10 @@ class Device:
         return out[: 6 * n].reshape(n, 6)
 
     def counters(self) -> dict:
-        buf = (C.c_uint64 * 7)()
-        check(load().mm2g_batch_counters(self._h, buf, 7), "counters")
-        keys = ["bases", "minimizers", "kept_minimizers", "anchors", "rescued_anchors", "dp_pairs", "dp_anchors"]
+        keys = ["bases", "minimizers", "kept_minimizers", "anchors", "rescued_anchors", "dp_pairs", "dp_anchors",
+                "long_anchors", "giant_anchors", "med_anchors", "long_anchors_rescue", "giant_anchors_rescue", "med_anchors_rescue"]
+        buf = (C.c_uint64 * len(keys))()
+        check(load().mm2g_batch_counters(self._h, buf, len(keys)), "counters")
         return dict(zip(keys, list(buf)))
 
 

@@ -37,7 +37,17 @@ static int set_err(int code, const char* fmt, ...) {
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return set_err(MM2G_E_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); } while (0)
 #define LCHK(x) do { int e_ = (x); if (e_ != 0) return set_err(MM2G_E_HIP, "kernel launch %s: %s", #x, hipGetErrorString((hipError_t)e_)); } while (0)
 
-struct mm2g_index { HostIndex h; };
+struct mm2g_index {
+    HostIndex h;
+    int origin = 0;              // MM2G_IX_* (mm2g_index_origin)
+    std::string origin_note;     // why a GPU build ran on the host instead
+    bool released = false;       // mm2g_index_release_tables: the hash tables and S are freed
+    uint64_t st_keys = 0, st_total = 0; double st_occ = 0, st_spacing = 0;   // stats kept across the release
+};
+static int need_tables(const mm2g_index* idx) {
+    if (idx->released) return set_err(MM2G_E_STATE, "index tables were released (mm2g_index_release_tables)");
+    return 0;
+}
 
 // ------------------------------------------------------------------ device buffers
 struct DevBuf {
@@ -59,6 +69,11 @@ static int ensure(DevBuf& b, size_t n, T** out) {
 #define ENSURE(buf, T, n, ptr) do { int e_ = ensure<T>(buf, (n), &(ptr)); if (e_) return e_; } while (0)
 
 struct ProfSlot { std::string name; double ms = 0; int64_t calls = 0; };
+// Batch status block (u64 words, device + pinned copy): [0] BS_* bits | dv
+// overflow, [1] filter-table entries, [2] anchors, [3] minimizers, [4] anchors
+// in the DP, [8 + 3 pass ..] anchors in long (< / >= giant_min) and medium
+// segments of each DP pass (k_lseg_order)
+constexpr int STAT_WORDS = 16;
 
 // pinned host staging of one read batch (header + nt4 words), double-buffered
 struct Stage { uint64_t* p = nullptr; uint64_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; };
@@ -112,7 +127,7 @@ struct mm2g_ctx {
     DevBuf dstat;                          // batch status block (BS_* word, workspace needs, counters)
     DevBuf chain_rdoff;                    // mm2g_chain_batch: prefix sums of the caller's qlen
     uint64_t cap_tab = 0, cap_A = 0;       // filter-table entries / anchors the workspaces hold
-    uint64_t* h_stat = nullptr;            // pinned copy of dstat (8 u64)
+    uint64_t* h_stat = nullptr;            // pinned copy of dstat (STAT_WORDS u64)
     hipEvent_t ev_done = nullptr;          // end of the queued batch
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, collected = false, stop_after_sort = false, dv_separate = false;
@@ -262,6 +277,7 @@ int mm2g_index_build_fasta(const char* path, int w, int k, int b, int flag, int 
     for (auto& r : recs) { seqs.push_back((const uint8_t*)r.seq.data()); lens.push_back(r.seq.size()); names.push_back(r.name); }
     std::unique_ptr<mm2g_index> I(new mm2g_index());
     if (!build_index(seqs, lens, &names, w, k, b, flag, n_threads, I->h, err)) return set_err(MM2G_E_ARG, "%s", err.c_str());
+    I->origin = MM2G_IX_HOST;
     *out = I.release();
     return 0;
 }
@@ -276,19 +292,33 @@ int mm2g_index_build_seqs(uint32_t n_seq, const char* const* names, const uint8_
     std::unique_ptr<mm2g_index> I(new mm2g_index());
     std::string err;
     if (!build_index(s, l, names ? &nm : nullptr, w, k, b, flag, n_threads, I->h, err)) return set_err(MM2G_E_ARG, "%s", err.c_str());
+    I->origin = MM2G_IX_HOST;
     *out = I.release();
     return 0;
 }
 
+// The GPU index build; where the device cannot do it (minimizer slot overflow,
+// or MM2G_IKNOB_FORCE_FALLBACK in tests) the host builds the same index and the
+// index records it (mm2g_index_origin: MM2G_IX_GPU_FALLBACK and the reason).
 static int build_gpu_or_host(int device, const std::vector<const uint8_t*>& seqs, const std::vector<uint64_t>& lens,
                              const std::vector<std::string>* names, int w, int k, int b, int flag, int n_threads, mm2g_index** out) {
     std::unique_ptr<mm2g_index> I(new mm2g_index());
     std::string err;
     bool unsupported = false;
-    if (!build_index_gpu(device, seqs, lens, names, w, k, b, flag, I->h, err, unsupported)) {
+    bool ok;
+    if (g_index_knob[MM2G_IKNOB_FORCE_FALLBACK].load()) {
+        ok = false; unsupported = true; err = "GPU index build: host fallback forced (MM2G_IKNOB_FORCE_FALLBACK)";
+    } else {
+        ok = build_index_gpu(device, seqs, lens, names, w, k, b, flag, I->h, err, unsupported);
+    }
+    I->origin = MM2G_IX_GPU;
+    if (!ok) {
         if (!unsupported) return set_err(MM2G_E_HIP, "%s", err.c_str());
         if (g_index_knob[MM2G_IKNOB_GPU_STRICT].load()) return set_err(MM2G_E_UNSUP, "%s", err.c_str());
+        const std::string why = err;
         if (!build_index(seqs, lens, names, w, k, b, flag, n_threads, I->h, err)) return set_err(MM2G_E_ARG, "%s", err.c_str());
+        I->origin = MM2G_IX_GPU_FALLBACK;
+        I->origin_note = why;
     }
     *out = I.release();
     return 0;
@@ -318,11 +348,13 @@ int mm2g_index_load_mmi(const char* path, mm2g_index** out) {
     std::unique_ptr<mm2g_index> I(new mm2g_index());
     std::string err;
     if (!load_mmi(path, I->h, err)) return set_err(MM2G_E_IO, "%s", err.c_str());
+    I->origin = MM2G_IX_MMI;
     *out = I.release();
     return 0;
 }
 int mm2g_index_save_mmi(const mm2g_index* idx, const char* path) {
     if (!idx || !path) return set_err(MM2G_E_ARG, "null argument");
+    if (int e = need_tables(idx)) return e;
     std::string err;
     if (!save_mmi(idx->h, path, err)) return set_err(MM2G_E_IO, "%s", err.c_str());
     return 0;
@@ -331,12 +363,14 @@ void mm2g_index_free(mm2g_index* idx) { delete idx; }
 int mm2g_index_stats(const mm2g_index* idx, uint64_t* n_keys, double* avg_occ, double* avg_spacing, uint64_t* total_len) {
     if (!idx) return set_err(MM2G_E_ARG, "null index");
     uint64_t a, d; double b, c;
-    idx->h.stats(a, b, c, d);
+    if (idx->released) { a = idx->st_keys; b = idx->st_occ; c = idx->st_spacing; d = idx->st_total; }
+    else idx->h.stats(a, b, c, d);
     if (n_keys) *n_keys = a; if (avg_occ) *avg_occ = b; if (avg_spacing) *avg_spacing = c; if (total_len) *total_len = d;
     return 0;
 }
 int mm2g_index_calc_mid_occ(const mm2g_index* idx, float frac, int32_t* out) {
     if (!idx || !out) return set_err(MM2G_E_ARG, "null argument");
+    if (int e = need_tables(idx)) return e;
     *out = idx->h.calc_mid_occ(frac);
     return 0;
 }
@@ -353,10 +387,26 @@ int mm2g_index_seq(const mm2g_index* idx, uint32_t rid, const char** name, uint3
 }
 int64_t mm2g_index_get(const mm2g_index* idx, uint64_t minier, int* kind, uint64_t* out, int64_t cap) {
     if (!idx || !kind) return set_err(MM2G_E_ARG, "null argument");
+    if (int e = need_tables(idx)) return e;
     const uint64_t* pos; size_t n; uint64_t single;
     idx->h.get(minier, *kind, pos, n, single);
     for (size_t i = 0; i < n && (int64_t)i < cap; ++i) out[i] = pos[i];
     return (int64_t)n;
+}
+
+int mm2g_index_origin(const mm2g_index* idx, const char** note) {
+    if (!idx) return set_err(MM2G_E_ARG, "null index");
+    if (note) *note = idx->origin_note.empty() ? nullptr : idx->origin_note.c_str();
+    return idx->origin;
+}
+int mm2g_index_release_tables(mm2g_index* idx) {
+    if (!idx) return set_err(MM2G_E_ARG, "null index");
+    if (idx->released) return 0;
+    idx->h.stats(idx->st_keys, idx->st_occ, idx->st_spacing, idx->st_total);
+    std::vector<HostBucket>().swap(idx->h.B);
+    std::vector<uint32_t>().swap(idx->h.S);
+    idx->released = true;
+    return 0;
 }
 
 // ------------------------------------------------------------------ context
@@ -369,7 +419,7 @@ int mm2g_ctx_create(int device, mm2g_ctx** out) {
     std::unique_ptr<mm2g_ctx> c(new mm2g_ctx());
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipHostMalloc((void**)&c->h_stat, 8 * sizeof(uint64_t), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c->h_stat, STAT_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
     for (auto& S : c->stage) HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
     for (int k = 0; k < MM2G_KNOB_COUNT; ++k) c->knob[k] = knob_default(k);
@@ -389,34 +439,42 @@ void mm2g_ctx_destroy(mm2g_ctx* c) {
     delete c;
 }
 
-int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
-    if (!c || !idx) return set_err(MM2G_E_ARG, "null argument");
-    HIPCHK(hipSetDevice(c->device));
+// The index in the device layout's input form: per distinct key (key, off, n)
+// with Singles inline (IxEntry), and the positions of the Multis.  Built once
+// per upload call, however many devices receive it.
+struct FlatIndex { std::vector<uint64_t> keys, pos; std::vector<uint32_t> offs, ns; };
+static int flatten_index(const mm2g_index* idx, FlatIndex& F) {
+    if (int e = need_tables(idx)) return e;
     const HostIndex& H = idx->h;
     if (H.max_len >= (1u << 31)) return set_err(MM2G_E_UNSUP, "reference sequences must be shorter than 2^31");
-    std::vector<uint64_t> keys, pos; std::vector<uint32_t> offs, ns;
-    H.flatten(keys, offs, ns, pos);
-    if (pos.size() >= (1ULL << 32)) return set_err(MM2G_E_UNSUP, "more than 2^32 index positions");
     if (H.n_seq >= IX_INLINE) return set_err(MM2G_E_UNSUP, "2^31 or more reference sequences");
-    for (size_t t = 0; t < keys.size(); ++t)          // Singles: the position inline (IxEntry)
-        if (ns[t] == 1) { const uint64_t p = pos[offs[t]]; offs[t] = (uint32_t)p; ns[t] = IX_INLINE | (uint32_t)(p >> 32); }
-    const uint64_t nk = keys.size();
+    H.flatten(F.keys, F.offs, F.ns, F.pos);
+    if (F.pos.size() >= (1ULL << 32)) return set_err(MM2G_E_UNSUP, "more than 2^32 index positions");
+    for (size_t t = 0; t < F.keys.size(); ++t)          // Singles: the position inline (IxEntry)
+        if (F.ns[t] == 1) { const uint64_t p = F.pos[F.offs[t]]; F.offs[t] = (uint32_t)p; F.ns[t] = IX_INLINE | (uint32_t)(p >> 32); }
+    return 0;
+}
+
+static int upload_flat(mm2g_ctx* c, const HostIndex& H, const FlatIndex& F, int32_t mid_occ) {
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t nk = F.keys.size();
     uint32_t l2 = 1;
     while ((1ULL << l2) < 2 * std::max<uint64_t>(nk, 1)) ++l2;     // load factor <= 0.5
     if (l2 > 31) return set_err(MM2G_E_UNSUP, "index too large for the device table");
+    c->mapped = false;
     IxEntry* tab; uint64_t* dpos;
     c->dix = std::make_shared<mm2g_ctx::DevIndex>();    // a fresh copy (contexts sharing the old one keep it)
     ENSURE(c->dix->tab, IxEntry, (size_t)1 << l2, tab);
-    ENSURE(c->dix->ix_pos, uint64_t, pos.size(), dpos);
+    ENSURE(c->dix->ix_pos, uint64_t, F.pos.size(), dpos);
     HIPCHK(hipMemsetAsync(tab, 0xff, sizeof(IxEntry) << l2, c->stream));
-    if (!pos.empty()) HIPCHK(hipMemcpyAsync(dpos, pos.data(), pos.size() * 8, hipMemcpyHostToDevice, c->stream));
+    if (!F.pos.empty()) HIPCHK(hipMemcpyAsync(dpos, F.pos.data(), F.pos.size() * 8, hipMemcpyHostToDevice, c->stream));
     DevBuf dk, doff, dn;
     uint64_t* k_; uint32_t* o_; uint32_t* n_;
     ENSURE(dk, uint64_t, nk, k_); ENSURE(doff, uint32_t, nk, o_); ENSURE(dn, uint32_t, nk, n_);
     if (nk) {
-        HIPCHK(hipMemcpyAsync(k_, keys.data(), nk * 8, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(o_, offs.data(), nk * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(n_, ns.data(), nk * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(k_, F.keys.data(), nk * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(o_, F.offs.data(), nk * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(n_, F.ns.data(), nk * 4, hipMemcpyHostToDevice, c->stream));
     }
     LCHK(launch_ix_build(k_, o_, n_, nk, tab, l2, c->stream));
     // singleton-filter cells: per group (fwd, rev) a guard cell, ceil(len / 2^CELL_SHIFT) cells, a guard cell
@@ -445,10 +503,36 @@ int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
     return 0;
 }
 
+int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
+    if (!c || !idx) return set_err(MM2G_E_ARG, "null argument");
+    FlatIndex F;
+    if (int e = flatten_index(idx, F)) return e;
+    return upload_flat(c, idx->h, F, mid_occ);
+}
+
+// One flatten, then every context's copy (normally one per GPU) in its own
+// host thread: the H2D copies and table builds of the devices overlap.
+int mm2g_ctx_upload_index_many(mm2g_ctx* const* ctxs, int n, const mm2g_index* idx, int32_t mid_occ) {
+    if (!ctxs || n < 0 || !idx) return set_err(MM2G_E_ARG, "null argument");
+    for (int i = 0; i < n; ++i) if (!ctxs[i]) return set_err(MM2G_E_ARG, "null context %d", i);
+    FlatIndex F;
+    if (int e = flatten_index(idx, F)) return e;
+    std::vector<int> rc(n, 0);
+    std::vector<std::string> msg(n);
+    std::vector<std::thread> th;
+    for (int i = 0; i < n; ++i)
+        th.emplace_back([&, i] { rc[i] = upload_flat(ctxs[i], idx->h, F, mid_occ); if (rc[i]) msg[i] = g_err; });
+    for (auto& t : th) t.join();
+    for (int i = 0; i < n; ++i)
+        if (rc[i]) return set_err(rc[i], "device %d: %s", ctxs[i]->device, msg[i].c_str());
+    return 0;
+}
+
 int mm2g_ctx_share_index(mm2g_ctx* dst, const mm2g_ctx* src, int32_t mid_occ) {
     if (!dst || !src) return set_err(MM2G_E_ARG, "null argument");
     if (!src->have_index) return set_err(MM2G_E_STATE, "source context has no index");
     if (dst->device != src->device) return set_err(MM2G_E_ARG, "contexts are on different devices");
+    dst->mapped = false;
     dst->dix = src->dix;
     dst->log2cap = src->log2cap;
     dst->hidx = src->hidx;
@@ -508,6 +592,7 @@ int mm2g_ctx_index_mid_occ(mm2g_ctx* c, float frac, int32_t* out) {
 int mm2g_ctx_set_mid_occ(mm2g_ctx* c, int32_t mid_occ) {
     if (!c) return set_err(MM2G_E_ARG, "null argument");
     c->mid_occ = mid_occ;
+    c->mapped = false;      // a mapped batch's anchors used the old mid_occ
     return 0;
 }
 
@@ -530,16 +615,18 @@ int64_t mm2g_nt4_pack(const uint8_t* seq, const uint64_t* offs, uint32_t n_reads
 
 // Record the batch geometry and queue the H2D copy of the staged buffer
 // (header + nt4 words) on the context stream.
-static int stage_commit(mm2g_ctx* c, Stage& S, uint32_t n, uint64_t total_words) {
+static int stage_commit(mm2g_ctx* c, Stage& S, uint32_t n, uint64_t total_words, std::vector<uint64_t>& ro, uint32_t mx) {
+    c->mapped = false;
     uint64_t* d;
     ENSURE(c->rd_dev, uint64_t, total_words, d);
     HIPCHK(hipMemcpyAsync(d, S.p, total_words * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipEventRecord(S.ev, c->stream));
     S.pending = true;
     c->st_next ^= 1;
+    c->h_rd_off.swap(ro);
+    c->max_read_len = mx;
     c->d_rd_off = d; c->d_pk_off = d + n + 1; c->d_amb_off = d + 2 * (size_t)n + 1; c->d_words = d + 3 * (size_t)n + 1;
     c->n_reads = n; c->total_bases = c->h_rd_off[n];
-    c->mapped = false;
     c->sk1.exact = c->sk2.exact = false;
     return 0;
 }
@@ -559,17 +646,19 @@ static int stage_acquire(mm2g_ctx* c, uint64_t words, Stage** out) {
     return 0;
 }
 
-static int check_offsets(mm2g_ctx* c, const uint64_t* offs, uint32_t n) {
-    c->h_rd_off.assign((size_t)n + 1, 0);
-    uint32_t mx = 0;
+// Validates the offsets into `ro` (relative, n+1) and the longest read; the
+// context takes them only in stage_commit, so a failed call leaves the
+// previous batch's geometry intact.
+static int check_offsets(const uint64_t* offs, uint32_t n, std::vector<uint64_t>& ro, uint32_t& mx) {
+    ro.assign((size_t)n + 1, 0);
+    mx = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (offs[i + 1] < offs[i]) return set_err(MM2G_E_ARG, "offsets must be non-decreasing");
         const uint64_t L = offs[i + 1] - offs[i];
         if (L >= (1ULL << 31)) return set_err(MM2G_E_UNSUP, "reads must be shorter than 2^31");
         mx = std::max<uint32_t>(mx, (uint32_t)L);
-        c->h_rd_off[i + 1] = c->h_rd_off[i] + L;
+        ro[i + 1] = ro[i] + L;
     }
-    c->max_read_len = mx;
     return 0;
 }
 
@@ -578,16 +667,17 @@ int mm2g_batch_set_reads(mm2g_ctx* c, const uint8_t* seq, const uint64_t* offs, 
     HIPCHK(hipSetDevice(c->device));
     static const uint64_t zero = 0;
     if (!n_reads) offs = &zero;
-    if (int e = check_offsets(c, offs, n_reads)) return e;
+    std::vector<uint64_t> ro; uint32_t mx;
+    if (int e = check_offsets(offs, n_reads, ro, mx)) return e;
     const uint64_t hdr = 3 * (uint64_t)n_reads + 1;
     Stage* S;
     if (int e = stage_acquire(c, hdr + nt4_words_bound(offs, n_reads), &S)) return e;
     uint64_t* h = S->p;
-    memcpy(h, c->h_rd_off.data(), ((size_t)n_reads + 1) * 8);
+    memcpy(h, ro.data(), ((size_t)n_reads + 1) * 8);
     const int64_t nw = nt4_pack(seq, offs, n_reads, h + n_reads + 1, h + 2 * (size_t)n_reads + 1, h + hdr, S->cap - hdr,
                                 (int)c->knob[MM2G_KNOB_HOST_THREADS]);
     if (nw < 0) return set_err(MM2G_E_NOMEM, "nt4 staging too small");
-    return stage_commit(c, *S, n_reads, hdr + (uint64_t)nw);
+    return stage_commit(c, *S, n_reads, hdr + (uint64_t)nw, ro, mx);
 }
 
 int mm2g_batch_set_reads_nt4(mm2g_ctx* c, const mm2g_nt4_batch* b) {
@@ -602,18 +692,19 @@ int mm2g_batch_set_reads_nt4(mm2g_ctx* c, const mm2g_nt4_batch* b) {
         if (b->amb_off[r] != ~0ULL && b->amb_off[r] + (L + 63) / 64 > b->n_words) return set_err(MM2G_E_ARG, "read %u: bitmap beyond n_words", r);
         offs[r + 1] = offs[r] + L;
     }
-    if (int e = check_offsets(c, offs.data(), n)) return e;
+    std::vector<uint64_t> ro; uint32_t mx;
+    if (int e = check_offsets(offs.data(), n, ro, mx)) return e;
     const uint64_t hdr = 3 * (uint64_t)n + 1;
     Stage* S;
     if (int e = stage_acquire(c, hdr + b->n_words, &S)) return e;
     uint64_t* h = S->p;
-    memcpy(h, c->h_rd_off.data(), ((size_t)n + 1) * 8);
+    memcpy(h, ro.data(), ((size_t)n + 1) * 8);
     if (n) {
         memcpy(h + n + 1, b->pk_off, (size_t)n * 8);
         memcpy(h + 2 * (size_t)n + 1, b->amb_off, (size_t)n * 8);
     }
     if (b->n_words) memcpy(h + hdr, b->words, b->n_words * 8);
-    return stage_commit(c, *S, n, hdr + b->n_words);
+    return stage_commit(c, *S, n, hdr + b->n_words, ro, mx);
 }
 
 // Sketch the resident batch into sk's slots (one slot of L+16 per read, or the
@@ -698,7 +789,8 @@ static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_
 // arrays requested): no segment pruning, no lazy windows.
 static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const ChainKParams& P0, float gap, int npass, int32_t mdx1,
                      int32_t mdy1, int32_t bw_long, uint64_t A_cap, const uint64_t* a_off, const uint32_t* a_cnt, uint64_t* keys,
-                     uint64_t* ktmp, const uint32_t* cnt2, const uint64_t* smax, ReadOut* out, const uint32_t* abort, bool full) {
+                     uint64_t* ktmp, const uint32_t* cnt2, const uint64_t* smax, ReadOut* out, const uint32_t* abort, bool full,
+                     unsigned long long* stat = nullptr) {
     int32_t *fb, *pb;
     ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
     build_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1);
@@ -779,6 +871,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
             HIPCHK(hipMemsetAsync(gprof, 0, 16 * 8, c->stream));
         }
         ca.gprof = gprof;
+        ca.seg_stat = stat ? stat + 8 + 3 * pass : nullptr;
         for (int stg = 0; stg < 5; ++stg) {
             ca.giant_min = giant_min[pass];
             ca.giant_exact = pass == 0 ? 1u : 0u;
@@ -839,6 +932,30 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     return 0;
 }
 
+// The anchor workspace of a batch: keys, sorted keys, f (the sort's tags
+// first), pprev and the DP marks, 28 B per anchor (x 1.25 slack), kept across
+// batches.  The first estimate is 3 anchors per base (C3 has 2): about 10 GB
+// per context for a 100 Mb batch.  When HBM cannot hold that, the batch's exact
+// anchor count (the scan's total; one synchronisation) is used instead, so a
+// batch whose anchors fit is never refused for the estimate.
+static int reserve_anchor_ws(mm2g_ctx* c, const unsigned long long* st, uint64_t& A_cap) {
+    auto grab = [&](uint64_t n) -> int {
+        uint64_t* p64; int32_t* p32;
+        if (int e = ensure<uint64_t>(c->keys, n, &p64)) return e;
+        if (int e = ensure<uint64_t>(c->keys_tmp, n, &p64)) return e;
+        if (int e = ensure<int32_t>(c->fbuf, n, &p32)) return e;
+        if (int e = ensure<int32_t>(c->ppbuf, n, &p32)) return e;
+        if (int e = ensure<int32_t>(c->tmark, n, &p32)) return e;
+        return 0;
+    };
+    if (grab(A_cap) == 0) return 0;
+    unsigned long long tot = 0;
+    HIPCHK(hipMemcpyAsync(&tot, st + 2, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->cap_A = A_cap = std::max<uint64_t>((uint64_t)tot, 1);
+    return grab(A_cap);
+}
+
 // Queue the whole path for the resident batch on the context stream (no host
 // synchronisation): sketch -> filter -> lookup -> anchors -> sort -> chain ->
 // dv, then the per-read results and the status block to pinned host memory.
@@ -865,10 +982,10 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     ReadOut* out;
     ENSURE(c->outb, ReadOut, n + 1, out);
     unsigned long long* st;
-    ENSURE(c->dstat, unsigned long long, 8, st);
+    ENSURE(c->dstat, unsigned long long, STAT_WORDS, st);
     uint32_t* st32 = (uint32_t*)st;
     HIPCHK(hipMemsetAsync(out, 0, sizeof(ReadOut) * (n + 1), c->stream));
-    HIPCHK(hipMemsetAsync(st, 0, 64, c->stream));
+    HIPCHK(hipMemsetAsync(st, 0, STAT_WORDS * 8, c->stream));
     if (c->h_out_cap < (size_t)n + 1) {
         HIPCHK(hipStreamSynchronize(c->stream));   // a previous batch's copy may still target it
         if (c->h_out) (void)hipHostFree(c->h_out);
@@ -877,7 +994,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         c->h_out_cap = (size_t)n + 1;
     }
     if (n == 0) {
-        HIPCHK(hipMemcpyAsync(c->h_stat, st, 64, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_stat, st, STAT_WORDS * 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipEventRecord(c->ev_done, c->stream));
         c->mapped = true;
         return 0;
@@ -932,15 +1049,15 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     }
     c->cap_A = std::max<uint64_t>(c->cap_A, 3 * c->total_bases + 65536);
     if (c->knob[MM2G_KNOB_WS_MIN] > 0 && !c->redo) c->cap_A = (uint64_t)c->knob[MM2G_KNOB_WS_MIN];   // tests: force the re-map
-    const uint64_t A_cap = c->cap_A;
+    uint64_t A_cap = c->cap_A;
     {
         ProfScope ps(c, "scan");
         LCHK(launch_excl_scan(a_cnt, n, a_off, 0, 0, o->k, A_cap, st32, BS_ANCHORS, 2, c->stream));
     }
-    uint64_t *keys, *ktmp;
-    ENSURE(c->keys, uint64_t, A_cap, keys); ENSURE(c->keys_tmp, uint64_t, A_cap, ktmp);
-    int32_t* fb;
-    ENSURE(c->fbuf, int32_t, A_cap, fb);    // the sort's per-key tags live here before the DP needs it
+    if (int e = reserve_anchor_ws(c, st, A_cap)) return e;
+    uint64_t* keys = (uint64_t*)c->keys.p;
+    uint64_t* ktmp = (uint64_t*)c->keys_tmp.p;
+    int32_t* fb = (int32_t*)c->fbuf.p;      // the sort's per-key tags live here before the DP needs it
     sa.keys = keys; sa.cap_keys = c->keys.cap / 8;
     // reads heaviest first (anchor counts from seed_count): the hand-out order of
     // seed_write, the sort and the chain work items
@@ -995,7 +1112,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
         P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
         if (int e = run_chain(c, n, c->d_rd_off, P, 0.01f * 0.8f * (float)o->k, stop_at == 3 ? 1 : 2, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
-                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug))
+                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug, st))
             return e;
         // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
         const bool sep = (H.w != o->w || H.k != o->k);
@@ -1013,7 +1130,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     }
     LCHK(launch_batch_sums(n, mz_cnt, cnt2, st, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_out, out, (size_t)n * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_stat, st, 64, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_stat, st, STAT_WORDS * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipEventRecord(c->ev_done, c->stream));
     c->mapped = true;
     return 0;
@@ -1100,6 +1217,7 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     }
     for (int t = 0; t < 6; ++t) c->counters[t] = cnt[t];
     c->counters[6] = c->h_stat[4];    // anchors left after the sort's singleton filter (the DP input)
+    for (int t = 0; t < 6; ++t) c->counters[7 + t] = c->h_stat[8 + t];   // anchors per chain kernel class and pass
     return 0;
 }
 
@@ -1159,10 +1277,10 @@ int mm2g_batch_sketch(mm2g_ctx* c, int w, int k, uint32_t rid, uint64_t* out_off
     B.exact = false;
     int32_t* ovf;
     unsigned long long* st;
-    ENSURE(c->dstat, unsigned long long, 8, st);
+    ENSURE(c->dstat, unsigned long long, STAT_WORDS, st);
     ovf = (int32_t*)st + 1;
     for (int it = 0;; ++it) {
-        HIPCHK(hipMemsetAsync(st, 0, 64, c->stream));
+        HIPCHK(hipMemsetAsync(st, 0, STAT_WORDS * 8, c->stream));
         if (int e = run_sketch(c, w, k, B, ovf)) return e;
         int32_t o = 0;
         HIPCHK(hipMemcpyAsync(&o, ovf, 4, hipMemcpyDeviceToHost, c->stream));
@@ -1215,7 +1333,10 @@ int64_t mm2g_seed_batch(mm2g_ctx* c, const mm2g_map_opts* o, uint64_t* a_off, ui
     if (!c || !o || !a_off) return set_err(MM2G_E_ARG, "null argument");
     if (!c->have_index) return set_err(MM2G_E_STATE, "no index uploaded");
     HIPCHK(hipSetDevice(c->device));
-    const bool same = c->mapped && c->stop_after_sort && !memcmp(&c->last_opts, o, sizeof *o);
+    const mm2g_map_opts& L = c->last_opts;    // field by field: no struct padding in the comparison
+    const bool same = c->mapped && c->stop_after_sort && L.w == o->w && L.k == o->k && L.max_gap == o->max_gap && L.bw == o->bw &&
+                      L.bw_long == o->bw_long && L.min_cnt == o->min_cnt && L.min_chain_score == o->min_chain_score &&
+                      L.mask_level == o->mask_level && L.pri_ratio == o->pri_ratio && L.best_n == o->best_n;
     if (!same)
         if (int e = map_enqueue(c, o, true)) return e;
     if (int e = wait_batch(c)) return e;
@@ -1432,6 +1553,8 @@ int mm2g_prof_reset(mm2g_ctx* c) {
 int64_t mm2g_debug_chain_stats(mm2g_ctx* c, uint32_t* out6, uint32_t n) {
     if (!c) return set_err(MM2G_E_ARG, "null context");
     if (!c->mapped || !c->h_out) return set_err(MM2G_E_STATE, "call mm2g_batch_results first");
+    HIPCHK(hipSetDevice(c->device));
+    if (int e = wait_batch(c)) return e;        // h_out is filled by an async copy
     if (out6)
         for (uint32_t i = 0; i < n && i < c->n_reads; ++i) {
             const ReadOut& o = c->h_out[i];

@@ -206,6 +206,7 @@ struct ChainArgs {
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
     const uint32_t* abort = nullptr;
     unsigned long long* gprof = nullptr;   // MM2G_LSEG_PROF: k_chain_giant phase sums (16 counters)
+    unsigned long long* seg_stat = nullptr;   // k_lseg_order: anchors in long (< / >= giant_min) and medium segments
 };
 struct DvArgs {
     uint32_t n;

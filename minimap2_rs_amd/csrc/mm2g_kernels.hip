@@ -2176,19 +2176,37 @@ __global__ __launch_bounds__(256) void k_chain_med(ChainArgs a) {
     }
 }
 
-// long segments by descending length (largest-first hand-out to k_chain_long)
-__global__ __launch_bounds__(1024) void k_lseg_order(const uint32_t* lseg_n, uint32_t cap, const uint4* lseg, uint32_t* order) {
+// long segments by descending length (largest-first hand-out to k_chain_long);
+// also the anchors each chain kernel gets (roofline accounting, mm2g_batch_counters):
+// seg_stat[0] long segments below giant_min, [1] from giant_min on, [2] medium segments
+__global__ __launch_bounds__(1024) void k_lseg_order(ChainArgs a) {
     __shared__ uint32_t hist[33], offs[33];
+    __shared__ unsigned long long ssum[3][16];
     const int tid = threadIdx.x;
-    const uint32_t n = min(*lseg_n, cap);
+    const uint32_t n = min(*a.lseg_n, a.lseg_cap);
+    const uint4* lseg = a.lseg;
+    uint32_t* order = a.lseg_order;
     if (tid < 33) hist[tid] = 0;
     __syncthreads();
+    unsigned long long s_lo = 0, s_hi = 0, s_med = 0;
     for (uint32_t q = tid; q < n; q += 1024) {
         const uint32_t c = lseg[q].z - lseg[q].y;
         atomicAdd(&hist[32 - (32 - __builtin_clz(c | 1))], 1u);
+        if (c >= a.giant_min) s_hi += c; else s_lo += c;
+    }
+    if (a.seg_stat) {
+        const uint32_t nm = min(*a.mseg_n, a.mseg_cap);
+        for (uint32_t q = tid; q < nm; q += 1024) s_med += a.mseg[q].z - a.mseg[q].y;
+        s_lo = wave_sum64(s_lo); s_hi = wave_sum64(s_hi); s_med = wave_sum64(s_med);
+        if (lane_id() == 0) { ssum[0][tid >> 6] = s_lo; ssum[1][tid >> 6] = s_hi; ssum[2][tid >> 6] = s_med; }
     }
     __syncthreads();
     if (tid == 0) { uint32_t run = 0; for (int b = 0; b < 33; ++b) { offs[b] = run; run += hist[b]; } }
+    if (a.seg_stat && tid < 3) {
+        unsigned long long t = 0;
+        for (int w = 0; w < 16; ++w) t += ssum[tid][w];
+        a.seg_stat[tid] = t;
+    }
     __syncthreads();
     for (uint32_t q = tid; q < n; q += 1024) {
         const uint32_t c = lseg[q].z - lseg[q].y;
@@ -3284,7 +3302,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     switch (stage) {
     case 0: hipLaunchKernelGGL(k_chain_seg, dim3(blocks), dim3(DP_NW * 64), seg_lds(a.P.lut_n), st, a); break;
     case 1: hipLaunchKernelGGL(k_chain_med, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
-    case 2: hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, (const uint32_t*)a.lseg_n, a.lseg_cap, (const uint4*)a.lseg, a.lseg_order); break;
+    case 2: hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, a); break;
     case 3: hipLaunchKernelGGL(k_chain_long, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a); break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;

@@ -5,14 +5,17 @@
 //               [-n] [-m] [-M] [-p] [-N] [-x preset] [-a] [-o out]
 //   mm2rs anchors <ref> <reads.fa> [-w] [-k] [-H]       (main.rs:160-171)
 //   mm2rs chain <ref> <reads.fa> [-w] [-k] [-r 5000] [-H] (main.rs:172-186)
-// Extra flags: -t threads (host index build), --device N, --batch-bases N,
-// --streams N (contexts in the align pipeline), --first-only (map only the
-// first record, exactly as the reference does), --cpu-index.
+// Extra flags: -t threads (host index build), --device N, --devices 0,1,..,
+// --batch-bases N, --streams N (contexts per GPU in the align pipeline),
+// --first-only (map only the first record, exactly as the reference does),
+// --cpu-index.
 // Unlike the reference, align maps every record of <reads> (FASTA or FASTQ),
-// streaming: a reader fills batches, N contexts (HIP streams, one shared
-// device index) map them concurrently -- batch k+1's upload and sketch overlap
-// batch k's chaining -- and a writer emits PAF in input order.  The output is
-// the per-read concatenation of what the reference prints for each read alone.
+// streaming: a reader fills batches, N contexts per GPU (HIP streams, one
+// device index per GPU, the GPUs' copies uploaded in parallel) pull them from
+// one queue -- batch k+1's upload and sketch overlap batch k's chaining, and
+// reads shard over the GPUs of --devices -- and a writer emits PAF in input
+// order.  The output is the per-read concatenation of what the reference
+// prints for each read alone (src/main.rs:189-230), whatever the device count.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -32,7 +35,7 @@ static void usage() {
             "Usage: mm2rs index <fasta> [-w 10] [-k 15] [-b 14] [-H] [-d out.mmi] [-t threads] [--device N] [--cpu-index]\n"
             "       mm2rs align <ref.mmi|ref.fa> <reads.fa> [-w 10] [-k 15] [-H] [-f 2e-4] [-g 5000] [-r bw[,bw_long]]\n"
             "                   [-n 3] [-m 40] [-M 0.5] [-p 0.8] [-N 5] [-x map-ont|map-hifi|lr:hq|sr] [-a] [-o out]\n"
-            "                   [-t threads] [--device N] [--batch-bases N] [--first-only]\n");
+            "                   [-t threads] [--device N | --devices 0,1,..] [--streams N] [--batch-bases N] [--first-only]\n");
 }
 
 static bool ends_with(const std::string& s, const char* suf) {
@@ -51,6 +54,7 @@ int main(int argc, char** argv) {
     mm2g_map_opts mo; mm2g_map_opts_default(&mo);
     long long batch_bases = 256LL << 20;
     int n_streams = 4;
+    std::vector<int> devices;
     for (int i = 2; i < argc; ++i) {
         std::string a = argv[i];
         auto nxt = [&]() -> std::string { if (i + 1 >= argc) { usage(); exit(2); } return std::string(argv[++i]); };
@@ -72,6 +76,19 @@ int main(int argc, char** argv) {
         else if (a == "-o") out = nxt();
         else if (a == "-t") threads = atoi(nxt().c_str());
         else if (a == "--device") device = atoi(nxt().c_str());
+        else if (a == "--devices") {   // comma-separated device ids; a device may repeat (one index copy each)
+            devices.clear();
+            const std::string v = nxt();
+            for (size_t p = 0; p <= v.size();) {
+                size_t q = v.find(',', p);
+                if (q == std::string::npos) q = v.size();
+                const std::string t = v.substr(p, q - p);
+                char* e; const long d = strtol(t.c_str(), &e, 10);
+                if (t.empty() || *e || d < 0) { fprintf(stderr, "error: --devices expects a list like 0,1,2\n"); return 2; }
+                devices.push_back((int)d);
+                p = q + 1;
+            }
+        }
         else if (a == "--batch-bases") batch_bases = atoll(nxt().c_str());
         else if (a == "--streams") n_streams = std::max(1, atoi(nxt().c_str()));
         else if (a == "--first-only") first_only = true;
@@ -79,6 +96,7 @@ int main(int argc, char** argv) {
         else if (!a.empty() && a[0] == '-' && a.size() > 1) { fprintf(stderr, "error: unknown option %s\n", a.c_str()); usage(); return 2; }
         else pos.push_back(a);
     }
+    if (!devices.empty()) device = devices[0];
     if (cmd == "index") {   // main.rs:150-159
         if (pos.size() != 1) { usage(); return 2; }
         const int flag = hpc ? 1 : 0;
@@ -87,6 +105,9 @@ int main(int argc, char** argv) {
         const int st0 = gpu ? mm2g_index_build_fasta_gpu(pos[0].c_str(), w, k, b, flag, device, threads, &idx)
                             : mm2g_index_build_fasta(pos[0].c_str(), w, k, b, flag, threads, &idx);
         if (st0 != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
+        const char* why = nullptr;
+        if (mm2g_index_origin(idx, &why) == MM2G_IX_GPU_FALLBACK)
+            fprintf(stderr, "warning: the GPU index build fell back to the host build (%s); the index is the same\n", why ? why : "?");
         uint64_t nk, tl; double ao, as; uint32_t n_seq;
         mm2g_index_stats(idx, &nk, &ao, &as, &tl);
         mm2g_index_params(idx, nullptr, nullptr, nullptr, nullptr, &n_seq);
@@ -131,15 +152,30 @@ int main(int argc, char** argv) {
                                                      : mm2g_index_build_fasta(ref.c_str(), w, k, 14, hpc ? 1 : 0, threads, &idx);
     }
     if (st != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
-    // calc_mid_occ (main.rs:196-197) on the device table once it is uploaded
+    {
+        const char* why = nullptr;
+        if (mm2g_index_origin(idx, &why) == MM2G_IX_GPU_FALLBACK)
+            fprintf(stderr, "warning: the GPU index build fell back to the host build (%s); the index is the same\n", why ? why : "?");
+    }
+    if (devices.empty() || dbg_cmd) devices.assign(1, device);
+    {
+        const int nd = mm2g_device_count();
+        for (int d : devices)
+            if (d >= nd) { fprintf(stderr, "Error: device %d out of range (%d devices visible)\n", d, nd); return 1; }
+    }
+    // one index copy per listed device, uploaded in parallel; calc_mid_occ
+    // (main.rs:196-197) on the first device's table
     int32_t mid_occ = 10;
-    mm2g_ctx* ctx = nullptr;
-    if (mm2g_ctx_create(device, &ctx) != 0 || mm2g_ctx_upload_index(ctx, idx, mid_occ) != 0 ||
-        mm2g_ctx_index_mid_occ(ctx, frac, &mid_occ) != 0) {
+    std::vector<mm2g_ctx*> heads(devices.size(), nullptr);
+    for (size_t i = 0; i < devices.size(); ++i)
+        if (mm2g_ctx_create(devices[i], &heads[i]) != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
+    if (mm2g_ctx_upload_index_many(heads.data(), (int)heads.size(), idx, mid_occ) != 0 ||
+        mm2g_ctx_index_mid_occ(heads[0], frac, &mid_occ) != 0) {
         fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1;
     }
     if (mid_occ < 10) mid_occ = 10;                        // main.rs:197
-    mm2g_ctx_set_mid_occ(ctx, mid_occ);
+    for (mm2g_ctx* h : heads) mm2g_ctx_set_mid_occ(h, mid_occ);
+    mm2g_ctx* ctx = heads[0];
     if (dbg_cmd) {   // anchors / chain of the first read (read_fasta_first, main.rs:92-103)
         mm2g::SeqStream in; std::string err;
         mm2g::FastaRecord rec;
@@ -174,17 +210,20 @@ int main(int argc, char** argv) {
                 printf("end:   x=0x%016llx y=0x%016llx\n", (unsigned long long)xy[2 * en], (unsigned long long)xy[2 * en + 1]);
             }
         }
-        mm2g_ctx_destroy(ctx);
+        for (mm2g_ctx* h : heads) mm2g_ctx_destroy(h);
         mm2g_index_free(idx);
         return 0;
     }
-    // ---- streaming align: reader -> N mapping contexts -> in-order writer
-    std::vector<mm2g_ctx*> ctxs{ctx};
-    for (int i = 1; i < n_streams; ++i) {
-        mm2g_ctx* c2 = nullptr;
-        if (mm2g_ctx_create(device, &c2) != 0 || mm2g_ctx_share_index(c2, ctx, mid_occ) != 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1; }
-        ctxs.push_back(c2);
-    }
+    // ---- streaming align: reader -> N mapping contexts per GPU -> in-order writer
+    std::vector<mm2g_ctx*> ctxs;
+    for (int i = 0; i < n_streams; ++i)      // interleaved over the GPUs, so each starts working at once
+        for (size_t d = 0; d < heads.size(); ++d) {
+            mm2g_ctx* c2 = heads[d];
+            if (i > 0 && (mm2g_ctx_create(devices[d], &c2) != 0 || mm2g_ctx_share_index(c2, heads[d], mid_occ) != 0)) {
+                fprintf(stderr, "Error: %s\n", mm2g_last_error()); return 1;
+            }
+            ctxs.push_back(c2);
+        }
     mm2g::SeqStream in; std::string err;
     if (!in.open(pos[1].c_str(), err)) { fprintf(stderr, "Error: %s\n", err.c_str()); return 1; }
     FILE* fo = stdout;
@@ -242,7 +281,7 @@ int main(int argc, char** argv) {
                 std::vector<const char*> nm(n);
                 for (uint32_t i = 0; i < n; ++i) {
                     nm[i] = B->names[i].c_str();
-                    if (B->res[i].flags & MM2G_R_EMPTY) fprintf(stderr, "warning: read %s is empty (the reference asserts on it, src/sketch.rs:40); skipped\n", nm[i]);
+                    if (B->res[i].flags & MM2G_R_EMPTY) fprintf(stderr, "warning: read %s is empty (the reference asserts on it, src/sketch.rs:30); skipped\n", nm[i]);
                     if (B->res[i].flags & MM2G_R_PANIC) fprintf(stderr, "warning: read %s: the reference panics here (index out of bounds: rid 2147483647, DESIGN.md Q19); no PAF line\n", nm[i]);
                 }
                 const int64_t need = mm2g_format_paf(idx, B->res.data(), nm.data(), n, nullptr, 0);

@@ -743,8 +743,18 @@ struct PafRecord {
     bool panic = false;   // the reference would panic here (idx.seq[rid0] out of bounds)
 };
 
+// paf.rs:178 `mini_pos.binary_search(&first)`.  Cargo.lock version 4 bounds
+// the reference's rustc only from below (>= 1.78), and std changed the
+// algorithm in 1.82.  mini_pos is strictly increasing for odd k (no symmetric
+// k-mers: every position is emitted once, in order), where both versions give
+// the same answer; with even k a symmetric k-mer keeps l at w+k-1 for several
+// steps, the first-window tie emission (sketch.rs:79-82) repeats, and mini_pos
+// can hold duplicates and go backwards.  There the two versions
+// can disagree; the device (k_dv) follows >= 1.82, the oracle either one.
+static int g_binsearch_pre182 = 0;   // orc_set_binary_search(1): the 1.52-1.81 algorithm
+
 // Rust >= 1.82 slice::binary_search_by (base/size halving, no early exit)
-static bool rust_binary_search(const std::vector<int32_t>& v, int32_t target, size_t& idx) {
+static bool rust_binary_search_182(const std::vector<int32_t>& v, int32_t target, size_t& idx) {
     size_t size = v.size();
     if (size == 0) { idx = 0; return false; }
     size_t base = 0;
@@ -756,6 +766,26 @@ static bool rust_binary_search(const std::vector<int32_t>& v, int32_t target, si
     if (v[base] == target) { idx = base; return true; }
     idx = base + (v[base] < target ? 1 : 0);
     return false;
+}
+
+// Rust 1.52-1.81 slice::binary_search_by: midpoint of [left, right), early
+// return on Equal
+static bool rust_binary_search_pre182(const std::vector<int32_t>& v, int32_t target, size_t& idx) {
+    size_t size = v.size(), left = 0, right = size;
+    while (left < right) {
+        const size_t mid = left + size / 2;
+        const int32_t y = v[mid];
+        if (y < target) left = mid + 1;        // cmp == Less
+        else if (y > target) right = mid;      // cmp == Greater
+        else { idx = mid; return true; }
+        size = right - left;
+    }
+    idx = left;
+    return false;
+}
+
+static bool rust_binary_search(const std::vector<int32_t>& v, int32_t target, size_t& idx) {
+    return g_binsearch_pre182 ? rust_binary_search_pre182(v, target, idx) : rust_binary_search_182(v, target, idx);
 }
 
 // paf.rs:130-222
@@ -1056,7 +1086,7 @@ long long orc_align_fasta(void* idx, const char* reads_fa, const char* out_path,
     for (const auto& r : recs) {
         if (max_reads > 0 && nr >= max_reads) break;
         nr++;
-        if (r.seq.empty()) continue;   // reference asserts (sketch.rs:40); skipped here
+        if (r.seq.empty()) continue;   // reference asserts (sketch.rs:30); skipped here
         align_one(*I, mid_occ, o, r.name, (const uint8_t*)r.seq.data(), r.seq.size(), lines, counts ? &rc : nullptr);
     }
     auto t1 = std::chrono::steady_clock::now();
@@ -1072,6 +1102,16 @@ long long orc_align_fasta(void* idx, const char* reads_fa, const char* out_path,
 }
 
 void orc_set_quiet(int q) { g_quiet = q != 0; }
+// paf.rs:178's binary_search as rustc 1.52-1.81 (1) or >= 1.82 (0, default) compiles it
+void orc_set_binary_search(int pre182) { g_binsearch_pre182 = pre182 != 0; }
+// the two algorithms on a caller array (tests): returns found, *idx = Ok / Err index
+int orc_binary_search(const int32_t* v, uint64_t n, int32_t target, int pre182, uint64_t* idx) {
+    std::vector<int32_t> a(v, v + n);
+    size_t i = 0;
+    const bool f = pre182 ? rust_binary_search_pre182(a, target, i) : rust_binary_search_182(a, target, i);
+    *idx = i;
+    return f ? 1 : 0;
+}
 
 // build_index_from_fasta (src/index.rs:427-475) on in-memory records
 // (bench.py: avoids a multi-GB FASTA round trip for the hg38-shaped genome).
@@ -1106,7 +1146,7 @@ long long orc_align_seqs(void* idx, int n, const char* const* names, const uint8
         for (;;) {
             const int r = next.fetch_add(1);
             if (r >= n) break;
-            if (lens[r] == 0) continue;   // reference asserts (sketch.rs:40)
+            if (lens[r] == 0) continue;   // reference asserts (sketch.rs:30)
             align_one(*I, mid_occ, o, names ? std::string(names[r]) : std::string("*"), seqs[r], (size_t)lens[r], per[r], &rcs[t]);
         }
     };

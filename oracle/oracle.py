@@ -64,6 +64,9 @@ def lib() -> C.CDLL:
         L.orc_align_seqs.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, _P64, C.c_char_p, C.POINTER(C.c_int),
                                      C.POINTER(C.c_float), C.c_int, C.c_int, _P64, C.POINTER(C.c_double)]
         L.orc_set_quiet.argtypes = [C.c_int]
+        L.orc_set_binary_search.argtypes = [C.c_int]
+        L.orc_binary_search.restype = C.c_int
+        L.orc_binary_search.argtypes = [C.POINTER(C.c_int32), C.c_uint64, C.c_int32, C.c_int, _P64]
         L.orc_align_records.restype = C.c_longlong
         L.orc_align_records.argtypes = [C.c_void_p, C.c_int, C.c_void_p, _P64, C.POINTER(C.c_int), C.POINTER(C.c_float), C.c_int,
                                         C.c_int, C.POINTER(C.c_int32)]
@@ -232,6 +235,20 @@ def align_records(oi: "OIndex", seqs, mid_occ: int = -1, threads: int = 4, w: in
 
 def set_quiet(q: bool = True) -> None:
     lib().orc_set_quiet(1 if q else 0)
+
+
+def set_binary_search(pre182: bool) -> None:
+    """paf.rs:178's `binary_search` as rustc 1.52-1.81 (True) or >= 1.82 (False, the default) compiles it."""
+    lib().orc_set_binary_search(1 if pre182 else 0)
+
+
+def binary_search(v, target: int, pre182: bool = False):
+    """Rust slice::binary_search of `target` in the i32 array v: ("Ok", i) or ("Err", i)."""
+    a = np.ascontiguousarray(v, dtype=np.int32)
+    out = np.zeros(1, np.uint64)
+    f = lib().orc_binary_search(a.ctypes.data_as(C.POINTER(C.c_int32)), len(a), int(target), 1 if pre182 else 0,
+                                out.ctypes.data_as(_P64))
+    return ("Ok" if f else "Err", int(out[0]))
 
 
 def _seq_views(names, buf: np.ndarray, lens, starts=None):

@@ -115,3 +115,37 @@ def test_cli_usage_errors():
     mm2rs = os.path.join(ROOT, "minimap2_rs_amd", "build", "mm2rs")
     assert subprocess.run([mm2rs], capture_output=True).returncode != 0
     assert subprocess.run([mm2rs, "index", "/nonexistent.fa"], capture_output=True).returncode != 0
+
+
+def test_index_origin_and_forced_fallback(tmp_path):
+    """mm2g_index_origin tells how an index was made; a GPU build the device
+    cannot do falls back to the host build and says so (forced here by
+    MM2G_IKNOB_FORCE_FALLBACK, which returns before any device call, so this
+    runs without a GPU).  The fallback index equals the host build byte for
+    byte; released tables refuse later use but keep the stats."""
+    import numpy as np
+    import minimap2_rs_amd as M
+    from tools import simdata
+    names, lens, g = simdata.genome("small", 1.0, 11)
+    ih = M.Index.build_from_buffer(names, g, lens, threads=2)
+    assert ih.origin == ("host build", None)
+    M.set_index_knob("force_fallback", 1)
+    try:
+        ig = M.Index.build_from_buffer(names, g, lens, threads=2, device=0)
+    finally:
+        M.set_index_knob("force_fallback", 0)
+    kind, why = ig.origin
+    assert kind == "gpu build fell back to the host build" and "forced" in why
+    ig.save_to_mmi(str(tmp_path / "g.mmi"))
+    ih.save_to_mmi(str(tmp_path / "h.mmi"))
+    assert open(tmp_path / "g.mmi", "rb").read() == open(tmp_path / "h.mmi", "rb").read()
+    im = M.Index.load_from_mmi(str(tmp_path / "g.mmi"))
+    assert im.origin == (".mmi load", None)
+    st = im.stats()
+    im.release_tables()
+    assert im.stats() == st
+    with pytest.raises(M.Mm2gError if hasattr(M, "Mm2gError") else Exception):
+        im.calc_mid_occ(2e-4)
+    with pytest.raises(Exception):
+        im.save_to_mmi(str(tmp_path / "x.mmi"))
+    assert im.seq(0)[1] == int(lens[0])

@@ -9,6 +9,7 @@ checker.  PAF lines of reads whose chain lies on an odd rid are absent: the
 reference panics there."""
 import json
 import os
+import tempfile
 
 import numpy as np
 import pytest
@@ -188,3 +189,54 @@ def test_mmi_load_mapped_parallel(world, tmp_path, monkeypatch):
         cut.write_bytes(raw[:n])
         with pytest.raises(RuntimeError):
             M.Index.load_from_mmi(str(cut))
+
+
+def test_rust_binary_search_versions():
+    """paf.rs:178's `binary_search` as rustc 1.52-1.81 and >= 1.82 compile it:
+    identical on sorted arrays once the reference walks back to the first equal
+    element; on unsorted arrays they disagree (hand-traced: [5,1,3,2,4,0] for 3
+    is Err(4) with base/size halving, Err(6) with the early-exit midpoint)."""
+    assert O.binary_search([5, 1, 3, 2, 4, 0], 3) == ("Err", 4)
+    assert O.binary_search([5, 1, 3, 2, 4, 0], 3, pre182=True) == ("Err", 6)
+    assert O.binary_search([1, 3, 3, 3, 3], 3) == ("Ok", 4)
+    assert O.binary_search([1, 3, 3, 3, 3], 3, pre182=True) == ("Ok", 2)
+    rng = np.random.default_rng(4)
+    for _ in range(300):
+        v = np.sort(rng.integers(0, 50, size=int(rng.integers(0, 40))))
+        t = int(rng.integers(-2, 52))
+        a, b = O.binary_search(v, t), O.binary_search(v, t, pre182=True)
+        assert a[0] == b[0]
+        if a[0] == "Ok":
+            first = lambda i: int(np.searchsorted(v, v[i]))   # paf.rs:180 walks back to the first equal
+            assert first(a[1]) == first(b[1])
+        else:
+            assert a[1] == b[1] == int(np.searchsorted(v, t))
+
+
+def test_binary_search_exposure_even_k():
+    """Reads whose dv depends on the reference's rustc (tests/golden/
+    make_binsearch.py): with k = 16 their dv sketch's positions are not
+    increasing, and the oracle reproduces both recorded PAF lines under the
+    matching setting.  With odd k (every preset) positions are strictly
+    increasing and the setting changes nothing (bench.py counts it)."""
+    doc = json.load(open(os.path.join(GOLD, "binsearch_even_k.json")))
+    assert doc["cases"]
+    for c in doc["cases"]:
+        mv = O.sketch(c["read"].encode(), doc["w"], doc["k"])
+        pos = ((mv[:, 1] >> np.uint64(1)) & np.uint64(0xffffffff)).astype(np.int64)
+        assert np.any(np.diff(pos) <= 0)
+        ref = c["ref"].encode()
+        oi = O.OIndex.build_from_buffer([doc["ref_name"]], np.frombuffer(ref, np.uint8), np.array([len(ref)], np.uint64),
+                                        w=doc["w"], k=doc["k"], b=14, flag=0, threads=2)
+        q = c["read"].encode()
+        offs = np.array([0, len(q)], np.uint64)
+        try:
+            for pre, want in ((False, c["paf_rust_ge_1_82"]), (True, c["paf_rust_1_52_to_1_81"])):
+                O.set_binary_search(pre)
+                with tempfile.TemporaryDirectory() as td:
+                    p = os.path.join(td, "o.paf")
+                    oi.align_buffer([doc["read_name"]], np.frombuffer(q, np.uint8), offs, p, w=doc["w"], k=doc["k"], mid_occ=10000, threads=1)
+                    assert open(p).read().rstrip("\n") == want
+        finally:
+            O.set_binary_search(False)
+        assert c["paf_rust_ge_1_82"] != c["paf_rust_1_52_to_1_81"]

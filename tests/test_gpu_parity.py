@@ -375,6 +375,7 @@ def test_gpu_index_build(tmp_path, chunk):
             ig = M.Index.build_from_buffer(names, buf, lv, w=w, k=k, b=14, flag=fl, threads=4, device=0)
             ih = M.Index.build_from_seqs(names, seqs, w=w, k=k, b=14, flag=fl, threads=4)
             assert ig.stats() == oi.stats() == ih.stats(), (w, k, fl)
+            assert ig.origin == ("gpu build", None) and ih.origin == ("host build", None)
             for fr in (2e-4, 0.01, 0.5):
                 assert ig.calc_mid_occ(fr) == oi.mid_occ(fr) == ih.calc_mid_occ(fr)
             oi.save_mmi(str(tmp_path / "o.mmi"))
@@ -384,6 +385,27 @@ def test_gpu_index_build(tmp_path, chunk):
     finally:
         M.set_index_knob("ixchunk", 0)
         M.set_index_knob("gpu_strict", 0)
+
+
+def test_cli_align_devices(small_world, tmp_path):
+    """`mm2rs align --devices 0,0[,0]`: one index copy per listed device
+    (uploaded in parallel), reads pulled from one queue by every device's
+    contexts, PAF written in input order -- byte-identical to the oracle CLI
+    (the multi-GPU drop-in; one GPU here, so the device repeats)."""
+    import subprocess
+    ref, reads, rnames, rseqs = small_world
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mm2rs = os.path.join(root, "minimap2_rs_amd", "build", "mm2rs")
+    cpu = os.path.join(root, "oracle", "build", "mm2rs-cpu")
+    mmi = str(tmp_path / "ref.mmi")
+    subprocess.run([mm2rs, "index", ref, "-d", mmi], check=True, capture_output=True)
+    want = subprocess.run([cpu, "align", ref, reads], check=True, capture_output=True, text=True).stdout
+    for devs, streams in (("0,0", "2"), ("0,0,0", "1")):
+        got = subprocess.run([mm2rs, "align", mmi, reads, "--devices", devs, "--streams", streams, "--batch-bases", "15000"],
+                             check=True, capture_output=True, text=True).stdout
+        assert got == want and want.count("\n") > 50, devs
+    bad = subprocess.run([mm2rs, "align", mmi, reads, "--devices", "0,99"], capture_output=True, text=True)
+    assert bad.returncode != 0 and "out of range" in bad.stderr
 
 
 def test_cli_streaming_fastq(small_world, tmp_path):

@@ -3,6 +3,7 @@ oracle -- nt4 read input, mm2g_seed_batch (build_anchors_filtered),
 mm2g_chain_batch (chain_dp_all / rescue_long_join on caller anchors) -- plus
 the workspace re-map and the wide-gap envelope of the sort's singleton filter.
 All calls go through libmm2g.so; the oracle is only the checker."""
+import os
 import random
 
 import numpy as np
@@ -151,3 +152,19 @@ def test_chain_batch_rejects(dev):
         dev.chain_batch([a[::-1].copy()], [1000], M.chain_params(15, chn_pen_skip=0.5))
     with pytest.raises(Mm2gError):
         dev.chain_batch([a[::-1].copy()], [1000], M.chain_params(15, min_cnt=1))
+
+
+def test_dv_binary_search_even_k(dev):
+    """Even-k reads whose dv depends on the reference's rustc (tests/golden/
+    binsearch_even_k.json): the device follows paf.rs:178's binary_search as
+    rustc >= 1.82 compiles it."""
+    import json
+    doc = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "binsearch_even_k.json")))
+    for c in doc["cases"]:
+        idx = M.Index.build_from_seqs([doc["ref_name"]], [c["ref"].encode()], w=doc["w"], k=doc["k"], b=14, flag=0, threads=2)
+        dev.set_debug(False)
+        dev.upload_index(idx, 10000)
+        dev.set_reads([c["read"].encode()])
+        res = dev.map(M.map_opts(w=doc["w"], k=doc["k"]))
+        assert dev.paf([doc["read_name"]], res).rstrip("\n") == c["paf_rust_ge_1_82"]
+    dev.set_debug(True)

@@ -128,3 +128,90 @@ def test_shard_cuts_balanced(lens, world):
 def test_batches_distinct_per_rank_and_step():
     seeds = {bench.batch_seed(3, r, b) for r in range(8) for b in range(40)}
     assert len(seeds) == 8 * 40 and bench.batch_seed(3, 0, 0) == 3
+
+
+_RANK_SCRIPT = r'''
+import os, sys, json
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+t = torch.ones(1)
+dist.all_reduce(t)
+out = {"rank": int(os.environ["RANK"]), "local": int(os.environ["LOCAL_RANK"]), "world": dist.get_world_size(),
+       "seen": int(t.item()), "addr": os.environ["MASTER_ADDR"], "argv": sys.argv[1:],
+       "spawned": os.environ.get("MM2G_BENCH_SPAWNED")}
+with open(os.path.join(sys.argv[1], "rank%d.json" % out["rank"]), "w") as fh:
+    json.dump(out, fh)
+dist.destroy_process_group()
+sys.exit(int(os.environ.get("FAIL_RANK", "-1")) == out["rank"] and 3 or 0)
+'''
+
+
+def test_self_spawn_starts_every_rank(tmp_path, monkeypatch):
+    """`bench.py --gpus N` without a launcher starts N rank processes itself
+    (here a stand-in rank script over gloo): every rank joins the collective
+    and sees the launcher environment torch.distributed.run would give it."""
+    import json
+    import sys
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT)
+    monkeypatch.delenv("FAIL_RANK", raising=False)
+    rc = bench.spawn_ranks(3, [str(tmp_path), "--gpus", "3"], "gloo", 0, cmd=[sys.executable, str(script)])
+    assert rc == 0
+    got = [json.loads((tmp_path / f"rank{r}.json").read_text()) for r in range(3)]
+    assert [g["rank"] for g in got] == [0, 1, 2] and [g["local"] for g in got] == [0, 1, 2]
+    assert all(g["world"] == 3 and g["seen"] == 3 and g["addr"] == "127.0.0.1" and g["spawned"] == "1" for g in got)
+    assert all(g["argv"] == [str(tmp_path), "--gpus", "3"] for g in got)
+
+
+def test_self_spawn_failing_rank_fails_the_run(tmp_path, monkeypatch):
+    import sys
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT)
+    monkeypatch.setenv("FAIL_RANK", "1")
+    rc = bench.spawn_ranks(2, [str(tmp_path)], "gloo", 0, cmd=[sys.executable, str(script)])
+    assert rc == 3
+
+
+def test_more_rccl_ranks_than_gpus_is_an_error():
+    with pytest.raises(SystemExit) as e:
+        bench.spawn_ranks(2, [], "nccl", 1)
+    assert "2 GPUs" in str(e.value.code) or "needs 2" in str(e.value.code)
+
+
+def test_rank_count_must_match_gpus():
+    assert bench.rank_env(1, {}) == (0, 1, 0)
+    assert bench.rank_env(4, {"WORLD_SIZE": "4", "RANK": "2", "LOCAL_RANK": "2"}) == (2, 4, 2)
+    with pytest.raises(SystemExit):
+        bench.rank_env(8, {})                     # --gpus 8 in one process: never a silent 1-GPU run
+    with pytest.raises(SystemExit):
+        bench.rank_env(2, {"WORLD_SIZE": "4", "RANK": "0"})
+
+
+def _genome_worker(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank), "WORLD_SIZE": str(world)})
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import hashlib
+        args = bench.parse(["--preset", "ecoli", "--scale", "0.05"])
+        names, lens, g = bench.shared_genome(args, dist, rank, world, 2, f"t{port}")
+        q.put((rank, names, [int(x) for x in lens], hashlib.sha256(bytes(g)).hexdigest(), type(g).__name__))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shared_genome_one_generator(tmp_path):
+    """Rank 0 generates the reference once; the other ranks map it from /dev/shm
+    and see the same bytes (the file is gone once every rank has it)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_genome_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got[0][1:4] == got[1][1:4] and sum(got[0][2]) > 0
+    assert got[1][4] == "memmap"
+    assert not os.path.exists(f"/dev/shm/mm2g_bench_t{port}.genome")

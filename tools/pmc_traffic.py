@@ -9,7 +9,7 @@ FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction: FETCH_SIZE counts
 half the bytes of wide coalesced reads (TCC_EA0_RDREQ x 64 B for 128-B
 requests), so HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE.  Infinity-Cache hits
 are counted, not excluded (same section).  bench.py reads the result as the
-roofline's `traffic` for its dominant kernel.
+roofline's `traffic` for its dominant kernel (the instantiation that ran).
 """
 from __future__ import annotations
 
@@ -38,7 +38,9 @@ def per_kernel(path: str, counter: str):
         for row in csv.DictReader(fh):
             if row["Counter_Name"] != counter:
                 continue
-            name = row["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].strip()
+            # template instantiations stay apart (k_sketch<true, SeqNt4, false> of the
+            # query path vs k_sketch<..., SeqAscii, ...> of the index build)
+            name = row["Kernel_Name"].replace("void ", "", 1).split("(")[0].strip()
             acc[name].append(float(row["Counter_Value"]) * 1024.0)
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
