@@ -198,7 +198,7 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
     if (hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) return;
     (void)hipFree(d);
-    double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0, nleg = 0, ktiny = 0, klong = 0, ksrch = 0;
+    double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0, nleg = 0, nbigp = 0, ktiny = 0, klong = 0, ksrch = 0;
     uint64_t t_lo = ~0ULL, t_hi = 0;
     uint32_t m = 0;
     std::vector<uint32_t> q0, q2, q3;
@@ -210,7 +210,9 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
         for (int k = 0; k < 8; ++k) ph[k] += (double)p[k];
         tot += (double)(p[11] - p[10]);
         a0 += (double)p[8]; a2 += (double)(uint32_t)p[9];
-        if ((p[9] >> 32) == 0xffffu) nleg += 1; else np += (double)(p[9] >> 32);
+        if ((p[9] >> 32) == 0xffffu) nleg += 1;
+        else if ((p[9] >> 32) == 0xfffeu) nbigp += 1;
+        else np += (double)(p[9] >> 32);
         t_lo = std::min(t_lo, p[10]); t_hi = std::max(t_hi, p[11]);
         q0.push_back((uint32_t)p[8]); q2.push_back((uint32_t)p[9]);
         ktiny += (double)(uint32_t)p[14]; klong += (double)(p[14] >> 32); ksrch += (double)p[15];
@@ -221,8 +223,8 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
     fprintf(stderr, "[sort_prof] A0 q10/50/90/99/max=%u/%u/%u/%u/%u  A q10/50/90/99/max=%u/%u/%u/%u/%u  kept cells q10/50/90/99/max=%u/%u/%u/%u/%u\n",
             Q(q0, .1), Q(q0, .5), Q(q0, .9), Q(q0, .99), q0.back(), Q(q2, .1), Q(q2, .5), Q(q2, .9), Q(q2, .99), q2.back(),
             Q(q3, .1), Q(q3, .5), Q(q3, .9), Q(q3, .99), q3.back());
-    fprintf(stderr, "[sort_prof] reads=%u (whole-read radix %.0f) A0=%.0f A=%.0f nbig=%.2f windows=%.2f us/read: p1+kc=%.1f p2=%.1f gather=%.1f segs=%.1f chunk=%.1f rank=%.1f p4b/radix=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
-            m, nleg, a0 / m, a2 / m, np / m, ph[7] / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
+    fprintf(stderr, "[sort_prof] reads=%u (whole-read radix %.0f, bucket path %.0f) A0=%.0f A=%.0f nbig=%.2f windows=%.2f us/read: p1+kc=%.1f p2=%.1f gather=%.1f segs=%.1f chunk=%.1f rank=%.1f p4b/radix=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
+            m, nleg, nbigp, a0 / m, a2 / m, np / m, ph[7] / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
             ph[5] / m / 100, ph[6] / m / 100, tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
     fprintf(stderr, "[sort_prof] keys per read in segments <= %u: %.0f, 17..64: %.0f, > 64: %.0f (%.2f other-chunk searches each)\n",
             16u, ktiny / m, (a2 - ktiny - klong) / m, klong / m, klong > 0 ? ksrch / klong : 0.0);
@@ -867,8 +869,8 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         ca.lseg_prof = K[MM2G_KNOB_LSEG_PROF] ? 1u : 0u;
         unsigned long long* gprof = nullptr;
         if (ca.lseg_prof) {
-            HIPCHK(hipMalloc(&gprof, 16 * 8));
-            HIPCHK(hipMemsetAsync(gprof, 0, 16 * 8, c->stream));
+            HIPCHK(hipMalloc(&gprof, 32 * 8));
+            HIPCHK(hipMemsetAsync(gprof, 0, 32 * 8, c->stream));
         }
         ca.gprof = gprof;
         ca.seg_stat = stat ? stat + 8 + 3 * pass : nullptr;
@@ -899,8 +901,8 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
             ProfScope ps(c, names[pass][stg]);
             LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));
         }
-        if (gprof) {   // k_chain_giant phase sums (wall clock, 100 MHz)
-            unsigned long long g[16];
+        if (gprof) {   // k_chain_giant phase sums (wall clock, 100 MHz); k_chain_long per-anchor cycles
+            unsigned long long g[32];
             HIPCHK(hipMemcpyAsync(g, gprof, sizeof g, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
             (void)hipFree(gprof);
@@ -909,6 +911,10 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                             "setup %.0f eval %.0f changed %.0f improve %.0f children %.0f markcheck %.0f pin %.0f write %.0f\n",
                     pass, g[8], g[9], g[10], g[11], g[13], g[12] / 100.0, g[0] / 100.0, g[1] / 100.0, g[2] / 100.0, g[3] / 100.0,
                     g[4] / 100.0, g[5] / 100.0, g[6] / 100.0, g[7] / 100.0);
+            const double na = (double)std::max<unsigned long long>(g[16], 1);
+            fprintf(stderr, "[long_prof] pass %d: %llu anchors in long segments, %llu settled by the simple/shortcut step, %llu exact "
+                            "(%llu 64-lane window steps in all); shader cycles per anchor: st %.0f simple %.0f exact %.0f tail %.0f total %.0f\n",
+                    pass, g[16], g[17], g[19], g[18], g[20] / na, g[21] / na, g[22] / na, g[23] / na, (g[20] + g[21] + g[22] + g[23]) / na);
         }
         if (ca.lseg_prof) {   // the slowest long segments of this pass
             uint32_t nl = 0;
@@ -1074,7 +1080,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     //    it is off in debug mode (full anchor/DP arrays for the parity tests).
     uint32_t* cnt2; uint64_t* smax; uint32_t* rlist;
     ENSURE(c->cnt2, uint32_t, n, cnt2);
-    ENSURE(c->rlist, uint32_t, n + 1, rlist);
+    ENSURE(c->rlist, uint32_t, n + 2, rlist);
     ENSURE(c->smax, uint64_t, n, smax);
     const bool filt = !c->debug && !stop_after_sort && K[MM2G_KNOB_FILTER] && std::max(mdx0, mdx1) <= (1 << CELL_SHIFT);
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
@@ -1082,7 +1088,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
                 (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_SEG_SMALL], SEG_THREAD)), nullptr};
     so.abort = st32;
     so.meta = (uint32_t*)fb;
-    so.rlist = rlist; so.rcount = rlist + n;
+    so.rlist = rlist; so.rcount = rlist + n; so.rwork = rlist + n + 1;
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     uint64_t* sprof = nullptr;
@@ -1098,7 +1104,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         LCHK(launch_sort_read(1, so, c->stream));
     }
     {
-        ProfScope ps(c, "sort_radix");
+        ProfScope ps(c, so.cells ? "sort_big" : "sort_radix");   // reads k_sort_read listed: buckets (filter on) or radix
         LCHK(launch_sort_read(2, so, c->stream));
     }
     if (sprof) dump_sort_prof(c, sprof, n);

@@ -166,6 +166,7 @@ struct SortArgs {
     uint32_t* rlist = nullptr;   // reads k_sort_read leaves to k_sort_radix ([n]), and their count (zeroed by k_sort_small)
     uint32_t* rcount = nullptr;
     const uint32_t* order = nullptr;   // k_sort_read: block b sorts read order[b] (heaviest first); null = b
+    uint32_t* rwork = nullptr;         // k_sort_big: next list entry to take (zeroed by k_sort_small)
 };
 struct ChainArgs {
     uint32_t n;

@@ -860,7 +860,7 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
 constexpr int SORT_SMALL = 4096;
 
 __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.rcount = 0;   // k_sort_read's list for k_sort_radix
+    if (blockIdx.x == 0 && threadIdx.x == 0) { *a.rcount = 0; if (a.rwork) *a.rwork = 0; }   // k_sort_read's list for k_sort_radix / k_sort_big
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t s[SORT_SMALL];
     const uint32_t r = blockIdx.x;
@@ -1585,6 +1585,316 @@ __global__ __launch_bounds__(1024) void k_sort_radix(SortArgs a) {
     }
 }
 
+// inclusive max-scan over a 1024-thread block (all threads call it: it holds barriers)
+DEVI uint32_t block_incl_max(uint32_t v, uint32_t* sc) {
+    const int lane = lane_id(), wv = wave_id();
+    uint32_t x = wave_incl_scan(v, [](uint32_t p, uint32_t q) { return p > q ? p : q; });
+    __syncthreads();
+    if (lane == 63) sc[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) { const uint32_t q = sc[t]; pre = (t < wv && q > pre) ? q : pre; }
+    return x > pre ? x : pre;
+}
+// inclusive min-scan over a 1024-thread block
+DEVI uint32_t block_incl_min(uint32_t v, uint32_t* sc) {
+    const int lane = lane_id(), wv = wave_id();
+    uint32_t x = wave_incl_scan(v, [](uint32_t p, uint32_t q) { return p < q ? p : q; });
+    __syncthreads();
+    if (lane == 63) sc[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0xffffffffu;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) { const uint32_t q = sc[t]; pre = (t < wv && q < pre) ? q : pre; }
+    return x < pre ? x : pre;
+}
+
+// ---- large reads: every read k_sort_read lists while the singleton filter is
+// on (A0 > 65535 -- the 100 kb reads of C5 --, key layouts over 48 bits, more
+// kept cells or bigger cell segments than its LDS windows hold).  Cell buckets
+// through HBM instead of one LDS window pass per window over the whole read:
+//   P1/KC  as k_sort_read: seen / seen-twice bitmaps, kept cells, their ranks.
+//   P2     counts per bucket of 2^bsh consecutive kept cells (u32, top of the
+//          LDS; bsh is the smallest shift that gives <= BIG_NB_MAX buckets) and
+//          the largest dropped key; scanned to bucket starts.
+//   P3     scatter of the kept keys to O by bucket (LDS atomics hand out the
+//          slots).  A bucket is a union of whole cells, so bucket order is key
+//          order: O then holds every bucket in place, each one unsorted.
+//   P4     windows of whole buckets (<= W keys), read from O into LDS in one
+//          coalesced pass: every 64-key chunk is sorted by a wave (a chunk that
+//          spans buckets keeps each bucket in its slot range, since all keys of
+//          bucket b are below bucket b+1's); a key's rank inside its bucket is
+//          its chunk position plus a binary search per other chunk of the
+//          bucket (<= 16 keys: a direct count).  Bucket bounds of a slot come
+//          from a bucket-start bitmap and its word-level max / min scans.  The
+//          window is written back in place.
+//   big    buckets over SEG_RANK keys: the LSD radix on their HBM range (K is
+//          scratch once P3 has read it).
+// Traffic per key: 8 B (P1) + 8 (P2) + 16 (P3) + 16 (P4) = 48 B, against
+// ~9 passes of the whole-read radix.  One block per listed read, taken from a
+// work counter (the list is roughly heaviest first: k_sort_read defers in its
+// heaviest-first order).
+constexpr uint32_t BIG_NB_MAX = 16384;
+template <bool GL>
+__global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;
+    __shared__ uint64_t red[32];
+    __shared__ uint32_t s_sc[16], s_read, s_nbig;
+    __shared__ uint2 s_big[BIG_MAX];
+    __shared__ uint32_t s_goff[GOFF_LDS];
+    extern __shared__ uint64_t dyn64[];
+    uint32_t* dyn = (uint32_t*)dyn64;
+    const int tid = threadIdx.x, lane = lane_id();
+    const uint32_t nlist = *a.rcount;
+    const uint32_t qb = a.qb, gsh = a.qb + a.rb;
+    const uint64_t rmask = (1ULL << a.rb) - 1;
+    const uint32_t ng = 2u * a.n_seq + 2u;
+    if (!GL) {
+        for (uint32_t i = tid; i < ng && i < (uint32_t)GOFF_LDS; i += 1024) s_goff[i] = a.goff[i];
+    }
+    auto cell_of = [&](uint64_t x) -> uint32_t {
+        const uint32_t g = (uint32_t)(x >> gsh);
+        return (GL ? a.goff[g] : s_goff[g]) + 1u + (uint32_t)(((x >> qb) & rmask) >> CELL_SHIFT);
+    };
+    const uint32_t nw = (a.cells + 31) >> 5;
+    const uint32_t LW = a.lds_words;
+    uint32_t* B1 = dyn;
+    uint32_t* B2 = dyn + nw;
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) s_read = atomicAdd(a.rwork, 1u);
+        __syncthreads();
+        const uint32_t li = (uint32_t)uni((int32_t)s_read);
+        if (li >= nlist) break;
+        const uint32_t r = a.rlist[li];
+        const uint64_t base = a.a_off[r];
+        const uint32_t A0 = (uint32_t)(a.a_off[r + 1] - base);
+        uint64_t* K = a.keys + base;
+        uint64_t* O = a.tmp + base;
+        uint64_t* const pq = a.prof ? a.prof + (uint64_t)r * 16 : nullptr;
+        if (pq && tid == 0) pq[10] = pq[12] = wall_clock64();
+#define BIG_PH(k) do { if (pq && tid == 0) { const uint64_t t_ = wall_clock64(); pq[k] += t_ - pq[12]; pq[12] = t_; } } while (0)
+        // ---- P1: seen / seen-twice bitmaps (staged: all cells, then all atomics)
+        for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U1) {
+            uint64_t x[SORT_U1];
+            uint32_t c[SORT_U1], old[SORT_U1];
+#pragma unroll
+            for (int u = 0; u < SORT_U1; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
+#pragma unroll
+            for (int u = 0; u < SORT_U1; ++u) c[u] = cell_of(x[u]);
+#pragma unroll
+            for (int u = 0; u < SORT_U1; ++u) {
+                const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
+                old[u] = i < A0 ? atomicOr(&B1[c[u] >> 5], 1u << (c[u] & 31)) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < SORT_U1; ++u) {
+                const uint32_t i = i0 + (uint32_t)u * 1024 + tid, bit = 1u << (c[u] & 31);
+                if (i < A0 && (old[u] & bit)) atomicOr(&B2[c[u] >> 5], bit);
+            }
+        }
+        __syncthreads();
+        // ---- KC (in place of B2) and the word prefix of its popcounts (in place of B1)
+        const uint32_t per = (nw + 1023) >> 10;
+        const uint32_t wa = min(nw, (uint32_t)tid * per), wb = min(nw, wa + per);
+        uint32_t loc = 0;
+        for (uint32_t w = wa; w < wb; ++w) {
+            const uint32_t b1 = B1[w];
+            const uint32_t nb = (b1 << 1) | (w ? B1[w - 1] >> 31 : 0u) | (b1 >> 1) | (w + 1 < nw ? B1[w + 1] << 31 : 0u);
+            const uint32_t kc = b1 & (B2[w] | nb);
+            B2[w] = kc;
+            loc += (uint32_t)__popc(kc);
+        }
+        uint32_t nkc;
+        uint32_t run = block_excl_sum(loc, nkc, s_sc);
+        for (uint32_t w = wa; w < wb; ++w) { B1[w] = run; run += (uint32_t)__popc(B2[w]); }
+        BIG_PH(0);
+        if (pq && tid == 0) pq[13] = nkc;
+        // buckets of 2^bsh kept cells; their counts (then ends) CNT[0..NB] at the top of the LDS
+        const uint32_t nbmax = min(BIG_NB_MAX, LW - 2 * nw - 64);
+        uint32_t bsh = 0;
+        while (((nkc + (1u << bsh) - 1) >> bsh) > nbmax) ++bsh;
+        const uint32_t NB = (nkc + (1u << bsh) - 1) >> bsh;
+        const uint32_t cofs = (LW - NB - 1) & ~1u;
+        uint32_t* CNT = dyn + cofs;
+        for (uint32_t i = tid; i <= NB; i += 1024) CNT[i] = 0;
+        __syncthreads();
+        // ---- P2: counts per bucket, the largest dropped key
+        uint64_t smx = 0;
+        for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U2) {
+            uint64_t x[SORT_U2];
+            uint32_t c[SORT_U2], kw[SORT_U2], pw[SORT_U2];
+#pragma unroll
+            for (int u = 0; u < SORT_U2; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
+#pragma unroll
+            for (int u = 0; u < SORT_U2; ++u) c[u] = cell_of(x[u]);
+#pragma unroll
+            for (int u = 0; u < SORT_U2; ++u) { kw[u] = B2[c[u] >> 5]; pw[u] = B1[c[u] >> 5]; }
+#pragma unroll
+            for (int u = 0; u < SORT_U2; ++u) {
+                const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
+                if (i < A0) {
+                    const uint32_t b = c[u] & 31;
+                    if ((kw[u] >> b) & 1u) atomicAdd(&CNT[(pw[u] + (uint32_t)__popc(kw[u] & ((1u << b) - 1u))) >> bsh], 1u);
+                    else smx = x[u] + 1 > smx ? x[u] + 1 : smx;
+                }
+            }
+        }
+        smx = block_max64(smx, red);               // (its barriers also end the count atomics)
+        // exclusive scan of the counts in place: CNT[b] = start of bucket b
+        const uint32_t per2 = (NB + 1023) >> 10;
+        const uint32_t ca = min(NB, (uint32_t)tid * per2), cb = min(NB, ca + per2);
+        uint32_t l2 = 0;
+        for (uint32_t i = ca; i < cb; ++i) l2 += CNT[i];
+        uint32_t A;
+        uint32_t o = block_excl_sum(l2, A, s_sc);
+        for (uint32_t i = ca; i < cb; ++i) { const uint32_t v = CNT[i]; CNT[i] = o; o += v; }
+        if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; s_nbig = 0; }
+        __syncthreads();
+        BIG_PH(1);
+        // ---- P3: scatter of the kept keys by bucket; CNT[b] turns into bucket b's end
+        for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U2) {
+            uint64_t x[SORT_U2];
+            uint32_t c[SORT_U2], kw[SORT_U2], pw[SORT_U2];
+#pragma unroll
+            for (int u = 0; u < SORT_U2; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
+#pragma unroll
+            for (int u = 0; u < SORT_U2; ++u) c[u] = cell_of(x[u]);
+#pragma unroll
+            for (int u = 0; u < SORT_U2; ++u) { kw[u] = B2[c[u] >> 5]; pw[u] = B1[c[u] >> 5]; }
+#pragma unroll
+            for (int u = 0; u < SORT_U2; ++u) {
+                const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
+                const uint32_t b = c[u] & 31;
+                if (i < A0 && ((kw[u] >> b) & 1u)) {
+                    const uint32_t bk = (pw[u] + (uint32_t)__popc(kw[u] & ((1u << b) - 1u))) >> bsh;
+                    O[CK(atomicAdd(&CNT[bk], 1u), A0)] = x[u];
+                }
+            }
+        }
+        __syncthreads();
+        BIG_PH(2);
+        // ---- P4: windows of whole buckets.  LDS below CNT: S[W] keys, then the
+        // bucket-start bitmap SB and its word scans LS / NS (W/32 + 2 words each).
+        auto bstart = [&](uint32_t b) -> uint32_t { return b ? CNT[b - 1] : 0u; };
+        const uint32_t W = (((cofs - 16) * 32u) / 67u) & ~63u;
+        uint64_t* S = dyn64;
+        uint32_t* SB = dyn + 2 * W;
+        uint32_t* LS = SB + (W >> 5) + 2;
+        uint32_t* NS = LS + (W >> 5) + 2;
+        auto radix_big = [&](uint32_t s0, uint32_t e0) {   // block-wide; keys of O[s0, e0) sorted in place
+            __syncthreads();
+            radix_range(O + s0, K + s0, O + s0, e0 - s0, qb, dyn, red);
+        };
+        uint32_t ba = 0;
+        while (ba < NB) {
+            const uint32_t oa = bstart(ba);
+            if (CNT[ba] - oa > W) {                 // one bucket beyond a window: radix in HBM
+                radix_big(oa, CNT[ba]);
+                if (pq && tid == 0) pq[7] += 1;
+                ba = ba + 1;
+                continue;
+            }
+            uint32_t lo = ba + 1, hi = NB;          // last bb with bstart(bb) <= oa + W
+            while (lo < hi) { const uint32_t mid = (lo + hi + 1) >> 1; if (bstart(mid) - oa <= W) lo = mid; else hi = mid - 1; }
+            const uint32_t bb = lo;
+            const uint32_t nwin = bstart(bb) - oa;
+            const uint32_t nwd = (nwin + 31) >> 5;
+            __syncthreads();
+            block_pass8<SORT_UG>(O + oa, nwin, [&](uint32_t i, uint64_t x) { S[i] = x; });
+            for (uint32_t q = tid; q < nwd; q += 1024) SB[q] = 0;
+            __syncthreads();
+            for (uint32_t b = ba + tid; b < bb; b += 1024) { const uint32_t p = bstart(b) - oa; atomicOr(&SB[p >> 5], 1u << (p & 31)); }
+            __syncthreads();
+            // LS[q]: last bucket start in words <= q; NS[q]: first bucket start in words >= q (NS[nwd] = nwin)
+            for (uint32_t q0 = 0; q0 < nwd; q0 += 1024) {
+                const uint32_t q = q0 + tid;
+                const uint32_t m = q < nwd ? SB[q] : 0u;
+                uint32_t v = m ? q * 32 + 31 - (uint32_t)__builtin_clz(m) : 0u;
+                v = block_incl_max(v, s_sc);
+                const uint32_t carry = q0 ? LS[q0 - 1] : 0u;
+                if (q < nwd) LS[q] = v > carry ? v : carry;
+                __syncthreads();
+            }
+            for (uint32_t q0 = 0; q0 < nwd; q0 += 1024) {      // suffix min, from the end
+                const uint32_t q = nwd - 1 - (q0 + tid);
+                const bool ok = q0 + tid < nwd;
+                const uint32_t m = ok ? SB[q] : 0u;
+                uint32_t v = m ? q * 32 + (uint32_t)__builtin_ctz(m) : nwin;
+                v = block_incl_min(v, s_sc);
+                const uint32_t carry = q0 ? NS[nwd - q0] : nwin;
+                if (ok) NS[q] = v < carry ? v : carry;
+                __syncthreads();
+            }
+            if (tid == 0) NS[nwd] = nwin;
+            __syncthreads();
+            auto seg_of = [&](uint32_t i, uint32_t& s0, uint32_t& e0) {
+                const uint32_t q = i >> 5, bi = i & 31;
+                const uint32_t m = SB[q];
+                const uint32_t le = bi == 31 ? 0xffffffffu : ((2u << bi) - 1u);
+                const uint32_t lo_m = m & le, hi_m = m & ~le;
+                s0 = lo_m ? q * 32 + 31 - (uint32_t)__builtin_clz(lo_m) : LS[q ? q - 1 : 0];
+                e0 = hi_m ? q * 32 + (uint32_t)__builtin_ctz(hi_m) : NS[q + 1];
+            };
+            // A: sort every 64-key chunk holding a bucket of 17..SEG_RANK keys
+            const uint32_t nch = (nwin + 63) >> 6;
+            for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 16) {
+                const uint32_t i = q * 64 + (uint32_t)lane;
+                const bool v = i < nwin;
+                uint32_t s0 = 0, e0 = 0;
+                if (v) seg_of(i, s0, e0);
+                if (any(v && e0 - s0 > SEG_TINY && e0 - s0 <= SEG_RANK)) {
+                    uint64_t x = v ? S[i] : U64MAX;
+                    wave_bitonic64_np(x);
+                    if (v) S[i] = x;
+                }
+            }
+            __syncthreads();
+            BIG_PH(4);
+            // B: ranks inside the buckets, written back in place; buckets over
+            // SEG_RANK keys go back unsorted and are radix-sorted below
+            for (uint32_t i = tid; i < nwin; i += 1024) {
+                const uint64_t x = S[i];
+                uint32_t s0, e0;
+                seg_of(i, s0, e0);
+                const uint32_t L = e0 - s0;
+                if (L > SEG_RANK) {
+                    O[oa + i] = x;
+                    if (i == s0) { const uint32_t slot = atomicAdd(&s_nbig, 1u); if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s0, oa + e0); }
+                    continue;
+                }
+                uint32_t rank = 0;
+                if (L <= SEG_TINY) {
+                    for (uint32_t j = s0; j < e0; ++j) { const uint64_t y = S[j]; rank += (y < x || (y == x && j < i)) ? 1u : 0u; }
+                } else {
+                    const uint32_t co = i >> 6;
+                    rank = i - max(s0, co << 6);
+                    for (uint32_t c = s0 >> 6; c <= (e0 - 1) >> 6; ++c) {
+                        if (c == co) continue;
+                        rank += count_below(S, max(s0, c << 6), min(e0, (c << 6) + 64), x, c < co);
+                    }
+                }
+                O[oa + s0 + rank] = x;
+            }
+            __syncthreads();
+            BIG_PH(5);
+            if (pq && tid == 0) pq[7] += 1;
+            // a window holds fewer than W / SEG_RANK such buckets (<= BIG_MAX)
+            const uint32_t nbig = s_nbig;
+            for (uint32_t t = 0; t < nbig; ++t) radix_big(s_big[t].x, s_big[t].y);
+            __syncthreads();
+            if (tid == 0) s_nbig = 0;
+            BIG_PH(6);
+            ba = bb;
+        }
+        if (pq && tid == 0) { pq[8] = A0; pq[9] = (0xfffeULL << 32) | A; pq[11] = wall_clock64(); }
+#undef BIG_PH
+    }
+}
+
 // ============================================================================
 // 5. CHAIN DP — chain_dp_all (src/lchain.rs:59-91) + the fallback chain
 // (lchain.rs:162-173) + chain_qrange/trange (178-200) + the rescue test of
@@ -2215,6 +2525,13 @@ __global__ __launch_bounds__(1024) void k_lseg_order(ChainArgs a) {
 }
 
 // ---- 5b. one long segment per wave, wave-cooperative (heaviest first)
+// PROF (MM2G_KNOB_LSEG_PROF): shader-clock cycles of each phase of the
+// per-anchor step, summed over the pass's long segments into a.gprof[16..31]:
+// [16] anchors, [17] settled by the simple / chain-shortcut step, [19] taken
+// through the exact loop, [18] 64-predecessor window steps of both paths;
+// cycles of [20] the st window, [21] the simple / shortcut attempt, [22] the
+// exact loop, [23] the register shift + ring store.
+template <bool PROF>
 __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     extern __shared__ __align__(16) unsigned char smem[];
@@ -2265,6 +2582,8 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
         int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
         bool try_simple = true;
         int32_t next_try = 0, backoff = 16;     // after a failed simple attempt: retry at next_try (backoff 16..128)
+        uint64_t pc_st = 0, pc_simple = 0, pc_exact = 0, pc_tail = 0, pn_done = 0, pn_exact = 0, tp = 0;
+#define LP(acc) do { if (PROF) { const uint64_t t_ = clock64(); acc += t_ - tp; tp = t_; } } while (0)
         uint64_t nk = (s + lane < e) ? K[s + lane] : 0;
         for (int32_t i0 = s; i0 < e; i0 += 64) {
             const uint64_t ak = nk;
@@ -2284,6 +2603,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 wf = shr1_dpp(wf, span); wpp = shr1_dpp(wpp, -1);
             }
             for (int32_t i = ib; i < ie; ++i) {
+                if (PROF) tp = clock64();
                 const uint64_t ki = rdl64(ak, i - i0);
                 const int32_t pi = (int32_t)((ki >> qb) & rmask);
                 const int32_t qi = (int32_t)(ki & qmask);
@@ -2310,6 +2630,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 const int32_t lo = st > i - P.max_iter ? st : i - P.max_iter;
                 int32_t max_f = span, max_j = -1, n_skip = 0;
                 bool marks = false;
+                LP(pc_st);
                 // Simple path: n_skip only rises on a marked target, and every mark
                 // comes from a valid j with pprev[j] >= lo.  With <= max_skip such
                 // sources in the whole window no break can happen, so (f[i], pprev[i])
@@ -2377,6 +2698,8 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     if (done) backoff = 16;
                     else { next_try = i + backoff; backoff = backoff < 128 ? 2 * backoff : 128; }
                 }
+                LP(pc_simple);
+                if (PROF) { pn_done += done ? 1u : 0u; pn_exact += done ? 0u : 1u; }
                 if (!done)
                 for (int32_t jtop = i - 1; jtop >= lo; jtop -= 64) {
                     const int32_t j = jtop - lane;
@@ -2484,6 +2807,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                         wave_lds_sync();
                     }
                 }
+                LP(pc_exact);
                 // clear this i's marks (all targets lie in [lo, i-1])
                 if (marks) {
                     const int32_t w0 = lo >> 5, w1 = (i - 1) >> 5;
@@ -2495,6 +2819,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 }
                 if (lane == 0) rfp[i & (RK - 1)] = make_int2(max_f, max_j);
                 wp = shr1_dpp(wp, pi); wq = shr1_dpp(wq, qi); wf = shr1_dpp(wf, max_f); wpp = shr1_dpp(wpp, max_j);
+                LP(pc_tail);
             }
             wave_lds_sync();
             // flush f/pprev of the block; segment best (last index with max f)
@@ -2510,8 +2835,15 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
             atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)cpairs);
             atomicAdd(&a.out[r].n_noniso, (uint32_t)(e - s - 1));
             atomicAdd(&a.out[r].n_steps, n_steps);
+            if (PROF && a.gprof) {
+                atomicAdd(&a.gprof[16], (unsigned long long)(e - s - 1)); atomicAdd(&a.gprof[17], (unsigned long long)pn_done);
+                atomicAdd(&a.gprof[18], (unsigned long long)n_steps); atomicAdd(&a.gprof[19], (unsigned long long)pn_exact);
+                atomicAdd(&a.gprof[20], (unsigned long long)pc_st); atomicAdd(&a.gprof[21], (unsigned long long)pc_simple);
+                atomicAdd(&a.gprof[22], (unsigned long long)pc_exact); atomicAdd(&a.gprof[23], (unsigned long long)pc_tail);
+            }
         }
     }
+#undef LP
 }
 
 // ---- 5b'. giant segments (production only): chain_dp_all (lchain.rs:73-90)
@@ -3266,6 +3598,12 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
         b.lds_words = (uint32_t)(lds / 4);
         if (2u * b.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_read<true>, dim3(a.n), dim3(1024), lds, st, b);
         else hipLaunchKernelGGL(k_sort_read<false>, dim3(a.n), dim3(1024), lds, st, b);
+    } else if (a.cells) {       // the singleton filter is on: every listed read takes the bucket path
+        SortArgs b = a;
+        b.lds_words = (uint32_t)(SORT_LDS / 4);
+        const unsigned grid = std::min<uint32_t>(a.n, 1024);
+        if (2u * b.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_big<true>, dim3(grid), dim3(1024), (size_t)SORT_LDS, st, b);
+        else hipLaunchKernelGGL(k_sort_big<false>, dim3(grid), dim3(1024), (size_t)SORT_LDS, st, b);
     } else {
         const size_t hb = (size_t)(RS_MAXP + 16) * RS_ND * 4;
         const size_t lds = std::min<size_t>(std::max<size_t>(bmb, hb), (size_t)SORT_LDS);
@@ -3286,7 +3624,7 @@ int chain_max_blocks(int lut_n, int which) {
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     hipError_t e = which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_seg, DP_NW * 64, seg_lds(lut_n))
-                   : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_long, DP_NW * 64, chain_lds(lut_n))
+                   : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_long<false>, DP_NW * 64, chain_lds(lut_n))
                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_med, 256, lut_lds(lut_n));
     if (e != hipSuccess) return 0;
     return ncu * (per > 0 ? per : 1);
@@ -3303,7 +3641,10 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 0: hipLaunchKernelGGL(k_chain_seg, dim3(blocks), dim3(DP_NW * 64), seg_lds(a.P.lut_n), st, a); break;
     case 1: hipLaunchKernelGGL(k_chain_med, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 2: hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(k_chain_long, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a); break;
+    case 3:
+        if (a.lseg_prof) hipLaunchKernelGGL(k_chain_long<true>, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
+        else hipLaunchKernelGGL(k_chain_long<false>, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
+        break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
     case 7: hipLaunchKernelGGL(k_chain_giant<false>, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
