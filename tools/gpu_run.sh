@@ -14,6 +14,7 @@
 #   pmc     FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic.json
 #   sq      one SQ counter pass (stall shares, LDS bank conflicts), 1 stream
 #   ab      alternate bench runs of knob sets: AB="sort_lds_kb=157|sort_lds_kb=128" N=3
+#   abdir   alternate quick bench runs of whole trees (same box): DIRS=". .ab/r02" N=2
 # Outputs: gpurun_out/<TAG>/ (TAG defaults to "run").
 set -euo pipefail
 STEPS_ARG=${1:?steps}
@@ -83,6 +84,14 @@ for S in "${STEPS[@]}"; do
           timeout -k 10 300 python -u bench.py $QUIET --steps ${ABSTEPS:-12} $KA $BARGS > "$OUT/ab_${j}_$i.json" 2> "$OUT/ab_${j}_$i.err"
           echo "[$K] $(line "$OUT/ab_${j}_$i.json")" | tee -a "$OUT/ab.txt"
           j=$((j + 1))
+        done
+      done ;;
+    abdir)
+      for i in $(seq 1 ${N:-2}); do
+        for D in ${DIRS:?DIRS=". .ab/r02"}; do
+          nm=$(echo "$D" | tr -c 'a-zA-Z0-9\n' '_')
+          (cd "$D" && timeout -k 10 300 python -u bench.py $QUIET --steps ${ABSTEPS:-16} $BARGS) > "$OUT/abd_${nm}_$i.json" 2> "$OUT/abd_${nm}_$i.err"
+          echo "[$D] $(line "$OUT/abd_${nm}_$i.json")" | tee -a "$OUT/abdir.txt"
         done
       done ;;
     *) echo "unknown step $S"; exit 2 ;;
