@@ -911,10 +911,11 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                             "setup %.0f eval %.0f changed %.0f improve %.0f children %.0f markcheck %.0f pin %.0f write %.0f\n",
                     pass, g[8], g[9], g[10], g[11], g[13], g[12] / 100.0, g[0] / 100.0, g[1] / 100.0, g[2] / 100.0, g[3] / 100.0,
                     g[4] / 100.0, g[5] / 100.0, g[6] / 100.0, g[7] / 100.0);
-            const double na = (double)std::max<unsigned long long>(g[16], 1);
-            fprintf(stderr, "[long_prof] pass %d: %llu anchors in long segments, %llu settled by the simple/shortcut step, %llu exact "
-                            "(%llu 64-lane window steps in all); shader cycles per anchor: st %.0f simple %.0f exact %.0f tail %.0f total %.0f\n",
-                    pass, g[16], g[17], g[19], g[18], g[20] / na, g[21] / na, g[22] / na, g[23] / na, (g[20] + g[21] + g[22] + g[23]) / na);
+            const double np_ = (double)std::max<unsigned long long>(g[17] + g[19], 1);
+            fprintf(stderr, "[long_prof] pass %d: %llu anchors in long segments, %llu committed by the speculative block pass in %llu rounds; "
+                            "per-anchor path: %llu settled by the simple/shortcut step, %llu exact (%llu 64-lane window steps in all); "
+                            "shader cycles per per-anchor-path anchor: st %.0f simple %.0f exact %.0f tail %.0f\n",
+                    pass, g[16], g[24], g[25], g[17], g[19], g[18], g[20] / np_, g[21] / np_, g[22] / np_, g[23] / np_);
         }
         if (ca.lseg_prof) {   // the slowest long segments of this pass
             uint32_t nl = 0;

@@ -1921,6 +1921,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
 // the end of every block.  Keys are prefetched one block ahead.
 // ============================================================================
 constexpr int DP_NW = 4;          // waves per workgroup
+constexpr int SPEC_ROUNDS = 3;    // k_chain_long: speculative rounds per 64-anchor block before the per-anchor path
 constexpr int RING_WORDS = 256;   // 8192-bit mark ring (max_iter <= 8000)
 constexpr int RK = 256;           // anchor ring entries per wave (power of two, >= 256)
 static_assert((RK & (RK - 1)) == 0 && RK >= 256, "anchor ring size");
@@ -2527,10 +2528,11 @@ __global__ __launch_bounds__(1024) void k_lseg_order(ChainArgs a) {
 // ---- 5b. one long segment per wave, wave-cooperative (heaviest first)
 // PROF (MM2G_KNOB_LSEG_PROF): shader-clock cycles of each phase of the
 // per-anchor step, summed over the pass's long segments into a.gprof[16..31]:
-// [16] anchors, [17] settled by the simple / chain-shortcut step, [19] taken
-// through the exact loop, [18] 64-predecessor window steps of both paths;
-// cycles of [20] the st window, [21] the simple / shortcut attempt, [22] the
-// exact loop, [23] the register shift + ring store.
+// [16] anchors, [24] committed by the speculative block pass ([25] its
+// rounds); of the per-anchor path's: [17] settled by the simple / chain-shortcut
+// step, [19] taken through the exact loop; [18] 64-predecessor window steps;
+// cycles of the per-anchor path's [20] st window, [21] simple / shortcut
+// attempt, [22] exact loop, [23] register shift + ring store.
 template <bool PROF>
 __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
@@ -2582,7 +2584,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
         int32_t wp = 0, wq = 0, wf = 0, wpp = -1;
         bool try_simple = true;
         int32_t next_try = 0, backoff = 16;     // after a failed simple attempt: retry at next_try (backoff 16..128)
-        uint64_t pc_st = 0, pc_simple = 0, pc_exact = 0, pc_tail = 0, pn_done = 0, pn_exact = 0, tp = 0;
+        uint64_t pc_st = 0, pc_simple = 0, pc_exact = 0, pc_tail = 0, pn_done = 0, pn_exact = 0, tp = 0, pn_spec = 0, pn_rounds = 0;
 #define LP(acc) do { if (PROF) { const uint64_t t_ = clock64(); acc += t_ - tp; tp = t_; } } while (0)
         uint64_t nk = (s + lane < e) ? K[s + lane] : 0;
         for (int32_t i0 = s; i0 < e; i0 += 64) {
@@ -2602,7 +2604,129 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 wp = shr1_dpp(wp, (int32_t)((k0 >> qb) & rmask)); wq = shr1_dpp(wq, (int32_t)(k0 & qmask));
                 wf = shr1_dpp(wf, span); wpp = shr1_dpp(wpp, -1);
             }
-            for (int32_t i = ib; i < ie; ++i) {
+            // ---- speculative block pass (production): lane l runs the
+            // reference loop (lchain.rs:76-89) of anchor k = i0 + l over its 64
+            // nearest predecessors, all anchors of the block at once, on guessed
+            // f/pprev for the block's earlier anchors.  The first guess follows
+            // the chain (pprev[k] = k-1 when comput_sc accepts the pair: a
+            // composition scan from the block's final predecessor); each round
+            // replaces the guesses with what the lanes computed.  By induction
+            // in k, every anchor before the first lane whose result differs from
+            // its guess is exact, and so is that lane's result (all its inputs
+            // were exact): each round commits at least one anchor.  A lane whose
+            // loop would run past its 64 predecessors, and every anchor left after
+            // SPEC_ROUNDS rounds, takes the per-anchor path below.
+            int32_t i_seq = ib;
+            if (a.lazy) {
+                const int32_t k = i0 + lane;
+                const bool kv = k >= ib && k < ie;
+                const int32_t pk = (int32_t)((ak >> qb) & rmask), qk = (int32_t)(ak & qmask);
+                // candidates of k (lchain.rs:75-78): j in [max(st_k, k - max_iter), k-1];
+                // 65 = more than the 64 predecessors in reach
+                int32_t dlim;
+                {
+                    const int32_t base = max(s, k - 64);
+                    const int32_t pb = (int32_t)((rkey[base & (RK - 1)] >> qb) & rmask);
+                    int32_t stk = base;
+                    if (pk > (int32_t)((uint32_t)pb + (uint32_t)maxdx)) {    // st_k in (base, k]: branch-free search
+                        int32_t pos = base;                                 // invariant: pk > p(pos) + maxdx
+#pragma unroll
+                        for (int stp = 32; stp >= 1; stp >>= 1) {
+                            const int32_t m = pos + stp;
+                            const int32_t pm = (int32_t)((rkey[(m < k ? m : k) & (RK - 1)] >> qb) & rmask);
+                            if (m < k && pk > (int32_t)((uint32_t)pm + (uint32_t)maxdx)) pos = m;
+                        }
+                        stk = pos + 1;
+                    }
+                    int32_t nc = (stk == base && base > s) ? 65 : k - stk;
+                    nc = nc < P.max_iter ? nc : P.max_iter;
+                    dlim = kv ? nc : 0;
+                }
+                // first guess: the chain through k-1 (composition x -> max(x + a, b) of the lanes)
+                {
+                    const uint64_t kp = rkey[(k - 1) & (RK - 1)];
+                    const int32_t dq = qk - (int32_t)(kp & qmask), dr = pk - (int32_t)((kp >> qb) & rmask);
+                    const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                    const bool okp = kv && dlim >= 1 && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
+                    const int32_t dg = dr < dq ? dr : dq;
+                    const int32_t scp = (span < dg ? span : dg) - (int32_t)lut[okp ? dd : 0];
+                    constexpr int32_t NEG = -(1 << 29);
+                    int32_t ga = kv ? (okp ? scp : NEG) : 0, gb = kv ? (okp ? NEG : span) : NEG;
+                    scan_lb(ga, gb);
+                    const int32_t f_in = uni(rfp[(ib - 1) & (RK - 1)].x);
+                    const int32_t gf = max(f_in + ga, gb);
+                    if (kv) rfp[k & (RK - 1)] = make_int2(gf, okp ? k - 1 : -1);
+                }
+                wave_lds_sync();
+                int32_t committed = ib;
+                for (int rnd = 0; rnd < SPEC_ROUNDS && committed < ie; ++rnd) {
+                    const bool act0 = kv && k >= committed;
+                    int32_t mf = span, mj = -1, ns = 0, vis = 0;
+                    uint64_t mkm = 0;       // marks t[j] = k by offset d = k - j (bit d-1)
+                    bool brk = false;
+                    for (int d = 1; d <= 64; ++d) {
+                        const bool act = act0 && !brk && d <= dlim;
+                        if (!any(act)) break;
+                        const int32_t j = k - d;
+                        uint64_t kj = 0;
+                        int2 fpj = make_int2(0, -1);
+                        if (act) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
+                        const int32_t dq = qk - (int32_t)(kj & qmask), dr = pk - (int32_t)((kj >> qb) & rmask);
+                        const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                        const bool ok = act && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
+                        const int32_t dg = dr < dq ? dr : dq;
+                        const int32_t sv = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0] + fpj.x;
+                        vis += act ? 1 : 0;
+                        if (ok) {
+                            if (sv > mf) { mf = sv; mj = j; if (ns > 0) --ns; }
+                            else if ((mkm >> (d - 1)) & 1ULL) { ++ns; if (ns > P.max_skip) brk = true; }
+                            if (!brk && fpj.y >= 0) { const int32_t t = k - fpj.y; if (t <= 64) mkm |= 1ULL << ((t - 1) & 63); }
+                        }
+                    }
+                    const bool deep = act0 && !brk && dlim > 64;
+                    const int2 gv = act0 ? rfp[k & (RK - 1)] : make_int2(0, 0);
+                    const uint64_t badM = ballot(act0 && (deep || mf != gv.x || mj != gv.y));
+                    const int32_t fb = badM ? i0 + ctz64(badM) : ie;
+                    const bool fb_deep = badM && ((ballot(deep) >> ((fb - i0) & 63)) & 1ULL);
+                    const int32_t cend = fb_deep ? fb : (fb < ie ? fb + 1 : ie);     // committed after this round
+                    cpairs += (uint64_t)wave_sum((act0 && k < cend) ? (uint32_t)vis : 0u);
+                    ++n_steps;
+                    wave_lds_sync();
+                    if (act0 && k >= fb && !deep) rfp[k & (RK - 1)] = make_int2(mf, mj);   // lane fb exact, later lanes the next guess
+                    wave_lds_sync();
+                    if (PROF) { pn_spec += (uint64_t)(cend - committed); pn_rounds += 1; }
+                    committed = cend;
+                    if (fb_deep) break;
+                }
+                i_seq = committed;
+                if (i_seq < ie) {
+                    // the per-anchor path from i_seq: its register window (j = i_seq-1-l) from the ring,
+                    // and its st from a coarse seek (st only moves forward; the st loop finishes it)
+                    const int32_t jw = i_seq - 1 - lane;
+                    const uint64_t kw = rkey[jw & (RK - 1)];
+                    const int2 fw = rfp[jw & (RK - 1)];
+                    wp = (int32_t)((kw >> qb) & rmask); wq = (int32_t)(kw & qmask); wf = fw.x; wpp = fw.y;
+                    const int32_t pc = (int32_t)((rdl64(ak, i_seq - i0) >> qb) & rmask);
+                    int32_t slo = st, shi = i_seq;   // st_{i_seq} in [slo, shi]; st only ever lags it
+                    while (shi - slo > 64) {
+                        const int32_t stp = (shi - slo + 63) >> 6;
+                        const int32_t j = slo + lane * stp;
+                        const bool jin = j < shi;
+                        const uint64_t sr = rkey[j & (RK - 1)];
+                        const uint64_t sg = (jin && j < ring_lo) ? K[j] : 0;
+                        const uint64_t kj = j >= ring_lo ? sr : sg;
+                        // "i_seq's st lies beyond j": true on a prefix of the probes
+                        const bool past = jin && pc > (int32_t)((uint32_t)(int32_t)((kj >> qb) & rmask) + (uint32_t)maxdx);
+                        const int32_t npc = __popcll(ballot(past));
+                        if (npc == 0) break;
+                        const int32_t jl = slo + (npc - 1) * stp;
+                        slo = jl + 1;
+                        shi = min(shi, jl + stp);
+                    }
+                    st = slo > st ? slo : st;
+                }
+            }
+            for (int32_t i = i_seq; i < ie; ++i) {
                 if (PROF) tp = clock64();
                 const uint64_t ki = rdl64(ak, i - i0);
                 const int32_t pi = (int32_t)((ki >> qb) & rmask);
@@ -2840,6 +2964,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 atomicAdd(&a.gprof[18], (unsigned long long)n_steps); atomicAdd(&a.gprof[19], (unsigned long long)pn_exact);
                 atomicAdd(&a.gprof[20], (unsigned long long)pc_st); atomicAdd(&a.gprof[21], (unsigned long long)pc_simple);
                 atomicAdd(&a.gprof[22], (unsigned long long)pc_exact); atomicAdd(&a.gprof[23], (unsigned long long)pc_tail);
+                atomicAdd(&a.gprof[24], (unsigned long long)pn_spec); atomicAdd(&a.gprof[25], (unsigned long long)pn_rounds);
             }
         }
     }
