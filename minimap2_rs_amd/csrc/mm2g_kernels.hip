@@ -2664,23 +2664,38 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     int32_t mf = span, mj = -1, ns = 0, vis = 0;
                     uint64_t mkm = 0;       // marks t[j] = k by offset d = k - j (bit d-1)
                     bool brk = false;
-                    for (int d = 1; d <= 64; ++d) {
-                        const bool act = act0 && !brk && d <= dlim;
-                        if (!any(act)) break;
-                        const int32_t j = k - d;
-                        uint64_t kj = 0;
-                        int2 fpj = make_int2(0, -1);
-                        if (act) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
-                        const int32_t dq = qk - (int32_t)(kj & qmask), dr = pk - (int32_t)((kj >> qb) & rmask);
-                        const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-                        const bool ok = act && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
-                        const int32_t dg = dr < dq ? dr : dq;
-                        const int32_t sv = (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0] + fpj.x;
-                        vis += act ? 1 : 0;
-                        if (ok) {
-                            if (sv > mf) { mf = sv; mj = j; if (ns > 0) --ns; }
-                            else if ((mkm >> (d - 1)) & 1ULL) { ++ns; if (ns > P.max_skip) brk = true; }
-                            if (!brk && fpj.y >= 0) { const int32_t t = k - fpj.y; if (t <= 64) mkm |= 1ULL << ((t - 1) & 63); }
+                    // four predecessors per step: their loads and comput_sc are
+                    // independent (issued together), only the running maximum /
+                    // n_skip / marks update is sequential
+                    for (int d0 = 1; d0 <= 64; d0 += 4) {
+                        if (!any(act0 && !brk && d0 <= dlim)) break;
+                        int32_t sv4[4], pp4[4];
+                        bool ok4[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int d = d0 + u;
+                            const bool inr = act0 && d <= dlim;
+                            const int32_t j = k - d;
+                            uint64_t kj = 0;
+                            int2 fpj = make_int2(0, -1);
+                            if (inr) { kj = rkey[j & (RK - 1)]; fpj = rfp[j & (RK - 1)]; }
+                            const int32_t dq = qk - (int32_t)(kj & qmask), dr = pk - (int32_t)((kj >> qb) & rmask);
+                            const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                            ok4[u] = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
+                            const int32_t dg = dr < dq ? dr : dq;
+                            sv4[u] = (span < dg ? span : dg) - (int32_t)lut[ok4[u] ? dd : 0] + fpj.x;
+                            pp4[u] = fpj.y;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int d = d0 + u;
+                            const bool act = act0 && !brk && d <= dlim;
+                            vis += act ? 1 : 0;
+                            if (act && ok4[u]) {
+                                if (sv4[u] > mf) { mf = sv4[u]; mj = k - d; if (ns > 0) --ns; }
+                                else if ((mkm >> (d - 1)) & 1ULL) { ++ns; if (ns > P.max_skip) brk = true; }
+                                if (!brk && pp4[u] >= 0) { const int32_t t = k - pp4[u]; if (t <= 64) mkm |= 1ULL << ((t - 1) & 63); }
+                            }
                         }
                     }
                     const bool deep = act0 && !brk && dlim > 64;
@@ -3228,13 +3243,19 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                 // until the children lists).  An anchor none of whose predecessors
                 // moved keeps its argmax, and its own value already equals that
                 // maximum: the improvement skips it (after the first iteration).
+                // The moved anchors themselves are listed in gptr (free until the
+                // children lists) in index order.
                 for (int c0 = 0, carry = 0; c0 < len; c0 += 4096) {
                     uint32_t c4[4], sum = 0, tot;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; c4[k] = (t < len && vres[t] != fo[t]) ? 1u : 0u; sum += c4[k]; }
                     uint32_t ex = block_excl_sum(sum, tot, s_red) + (uint32_t)carry;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) { const int t = c0 + tid * 4 + k; if (t < len) { gch[t] = (int32_t)ex; fo[t] = vres[t]; } ex += c4[k]; }
+                    for (int k = 0; k < 4; ++k) {
+                        const int t = c0 + tid * 4 + k;
+                        if (t < len) { gch[t] = (int32_t)ex; if (c4[k]) gptr[ex] = t; fo[t] = vres[t]; }
+                        ex += c4[k];
+                    }
                     carry += (int)tot;
                 }
                 __syncthreads();
@@ -3245,12 +3266,32 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
                     if (lw & 0x8000u) continue;          // pinned: exact already
                     const uint64_t ki = gk[t];
                     const int32_t lo = t - (int32_t)lw;
-                    if (it > 0 && gch[t] == gch[lo]) continue;
                     int32_t mf = span, mj = -1;
-                    for (int32_t j = t - 1; j >= lo; --j) {
-                        bool ok;
-                        const int32_t sv = sc_of(ki, gk[j], ok) + fo[j];
-                        if (ok && sv > mf) { mf = sv; mj = j; }
+                    if (it == 0) {
+                        for (int32_t j = t - 1; j >= lo; --j) {
+                            bool ok;
+                            const int32_t sv = sc_of(ki, gk[j], ok) + fo[j];
+                            if (ok && sv > mf) { mf = sv; mj = j; }
+                        }
+                    } else {
+                        // Incremental: within a round values only rise (each policy is
+                        // greedy on its predecessor's values), so the previous argmax
+                        // J, now worth fo[t] = sc(t, J) + fo[J], still dominates every
+                        // window anchor whose value did not move; only the moved ones
+                        // can overtake it.  Same (value, visiting-order) maximum as the
+                        // full scan: strict > in decreasing j, the root (-1) first.
+                        const int32_t c1 = gch[t], cl = gch[lo];
+                        if (c1 == cl) continue;
+                        mf = fo[t]; mj = gp[t];
+                        for (int32_t c = c1 - 1; c >= cl; --c) {
+                            const int32_t j = gptr[c];
+                            bool ok;
+                            const int32_t sv = sc_of(ki, gk[j], ok) + fo[j];
+                            if (ok && (sv > mf || (sv == mf && mj >= 0 && j > mj))) { mf = sv; mj = j; }
+                        }
+                        ch |= mf != fo[t] ? 1u : 0u;
+                        gp[t] = mj;
+                        continue;
                     }
                     gp[t] = mj;
                     ch |= mf != fo[t] ? 1u : 0u;
