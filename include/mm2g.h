@@ -288,10 +288,11 @@ enum {
     MM2G_KNOB_HOST_THREADS = 18, /* host threads packing reads to nt4 [min(8, cores)]                         */
     MM2G_KNOB_WS_MIN = 19,       /* tests: a batch's first map starts with minimizer slots, filter-table and
                                     anchor workspaces of this many entries, forcing the re-map; 0 = off [0]   */
-    MM2G_KNOB_SORT_LDS_KB = 20,  /* dynamic LDS of the large-read sort in KiB (at most 157); 0 = 157 [0]     */
+    MM2G_KNOB_SORT_LDS_KB = 20,  /* dynamic LDS of the large-read sort in KiB (at most 157; up to 76: 512-thread workgroups, two per CU); 0 = 157 [0] */
     MM2G_KNOB_STOP_AT = 21,      /* measurement only (results invalid): 1 stop after the anchors, 2 after the
                                     sort, 3 no rescue pass, 4 no dv kernel; 0 = full path [0]                 */
-    MM2G_KNOB_COUNT = 22
+    MM2G_KNOB_SPEC_ROUNDS = 22,  /* speculative 64-anchor rounds of k_chain_long per block, 0..16 [3]            */
+    MM2G_KNOB_COUNT = 23
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

@@ -94,6 +94,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_GIANT_GBLOCKS: return 256;
     case MM2G_KNOB_FILTER: case MM2G_KNOB_LAZY: case MM2G_KNOB_PRUNE: case MM2G_KNOB_GIANT: return 1;
     case MM2G_KNOB_MIDHIST_BINS: return 4096;
+    case MM2G_KNOB_SPEC_ROUNDS: return 3;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -832,6 +833,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
     ca.seg_chunk = std::max<uint32_t>(64u, (uint32_t)K[MM2G_KNOB_SEG_CHUNK] & ~63u);
+    ca.spec_rounds = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(16, K[MM2G_KNOB_SPEC_ROUNDS]));
     // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
     // settle in a few no-break policy-iteration rounds.  Pass 0's long segments
     // are real chains whose windows carry many mark sources: k_chain_long is

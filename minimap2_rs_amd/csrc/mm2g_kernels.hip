@@ -928,6 +928,7 @@ constexpr uint32_t SEG_RANK = 2048;      // up to this: block-wide rank count; b
 constexpr int BIG_MAX = 128;             // larger segments listed per read (more: radix over the read)
 constexpr int GOFF_LDS = 256;            // group offsets staged in LDS when 2 * n_seq + 2 fits
 constexpr int SORT_LDS = 157 * 1024;     // dynamic LDS of k_sort_read (one workgroup per CU; 2.4 KB static)
+constexpr int SORT_LDS_HALF = 76 * 1024; // ... two 512-thread workgroups per CU (knob sort_lds_kb <= 76)
 #ifndef SORT_U
 #define SORT_U 8                          // keys per thread in flight in the block-wide passes over a read
 #endif
@@ -943,14 +944,14 @@ constexpr int SORT_LDS = 157 * 1024;     // dynamic LDS of k_sort_read (one work
 
 // 8 independent loads per thread, then fn(i, x) for each (i < n): hides HBM
 // latency in the block-wide passes of k_sort_read
-template <int U = 8, typename F>
+template <int U = 8, int NT = 1024, typename F>
 DEVI void block_pass8(const uint64_t* src, uint32_t n, F fn) {
-    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * U) {
+    for (uint32_t i0 = 0; i0 < n; i0 += NT * U) {
         uint64_t x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; x[u] = i < n ? src[i] : 0; }
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * NT + threadIdx.x; x[u] = i < n ? src[i] : 0; }
 #pragma unroll
-        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; if (i < n) fn(i, x[u]); }
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * NT + threadIdx.x; if (i < n) fn(i, x[u]); }
     }
 }
 
@@ -1011,37 +1012,37 @@ DEVI uint32_t count_below(const uint64_t* S, uint32_t lo, uint32_t hi, uint64_t 
 }
 
 // as block_pass8 over keys and their u16 tags (loaded together): fn(i, x, m)
-template <int U = 8, typename F>
+template <int U = 8, int NT = 1024, typename F>
 DEVI void block_pass_km(const uint64_t* src, const uint16_t* tag, uint32_t n, F fn) {
-    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * U) {
+    for (uint32_t i0 = 0; i0 < n; i0 += NT * U) {
         uint64_t x[U];
         uint16_t m[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x;
+            const uint32_t i = i0 + (uint32_t)u * NT + threadIdx.x;
             x[u] = i < n ? src[i] : 0;
             m[u] = i < n ? tag[i] : (uint16_t)0xffffu;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; if (i < n) fn(i, x[u], m[u]); }
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * NT + threadIdx.x; if (i < n) fn(i, x[u], m[u]); }
     }
 }
 
 // as block_pass_km, but fn(i, x, m, valid) runs on every lane (block-uniform
 // trip count) so that fn may ballot / shuffle
-template <int U = 8, typename F>
+template <int U = 8, int NT = 1024, typename F>
 DEVI void block_pass_kmu(const uint64_t* src, const uint16_t* tag, uint32_t n, F fn) {
-    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * U) {
+    for (uint32_t i0 = 0; i0 < n; i0 += NT * U) {
         uint64_t x[U];
         uint16_t m[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x;
+            const uint32_t i = i0 + (uint32_t)u * NT + threadIdx.x;
             x[u] = i < n ? src[i] : 0;
             m[u] = i < n ? tag[i] : (uint16_t)0xffffu;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + threadIdx.x; fn(i, x[u], m[u], i < n); }
+        for (int u = 0; u < U; ++u) { const uint32_t i = i0 + (uint32_t)u * NT + threadIdx.x; fn(i, x[u], m[u], i < n); }
     }
 }
 
@@ -1058,7 +1059,8 @@ DEVI void block_pass_u(const uint64_t* src, uint32_t n, F fn) {
     }
 }
 
-// exclusive scan over a 1024-thread block (all threads call it: it holds barriers)
+// exclusive scan over a block of NW waves (all threads call it: it holds barriers)
+template <int NW = 16>
 DEVI uint32_t block_excl_sum(uint32_t v, uint32_t& total, uint32_t* sc) {
     const int lane = lane_id(), wv = wave_id();
     uint32_t wt;
@@ -1068,11 +1070,12 @@ DEVI uint32_t block_excl_sum(uint32_t v, uint32_t& total, uint32_t* sc) {
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) { const uint32_t q = sc[t]; pre += t < wv ? q : 0u; tot += q; }
+    for (int t = 0; t < NW; ++t) { const uint32_t q = sc[t]; pre += t < wv ? q : 0u; tot += q; }
     total = tot;
     return pre + ex;
 }
 
+template <int NW = 16>
 DEVI uint64_t block_max64(uint64_t v, uint64_t* red) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(v, d, 64); v = o > v ? o : v; }
@@ -1081,7 +1084,7 @@ DEVI uint64_t block_max64(uint64_t v, uint64_t* red) {
     __syncthreads();
     v = 0;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) v = red[t] > v ? red[t] : v;
+    for (int t = 0; t < NW; ++t) v = red[t] > v ? red[t] : v;
     return v;
 }
 
@@ -1201,8 +1204,9 @@ DEVI void radix_range(uint64_t* src, uint64_t* dst, uint64_t* out, uint32_t A, u
 // parameter rather than a pointer chosen at run time: a pointer that may be
 // LDS or global compiles to flat loads, and every flat load waits for all
 // outstanding global loads and stores (vmcnt(0)), which serialised P1/P2 per key.
-template <bool GL>
-__global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
+template <bool GL, int NT>
+__global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
+    constexpr int NW = NT / 64;
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t red[32];
     __shared__ uint32_t s_sc[16], s_kept, s_nbig;
@@ -1232,7 +1236,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
     const bool filt = a.cells != 0;
     const uint32_t ng = 2u * a.n_seq + 2u;
     if (!GL && filt) {
-        for (uint32_t i = tid; i < ng && i < (uint32_t)GOFF_LDS; i += 1024) s_goff[i] = a.goff[i];
+        for (uint32_t i = tid; i < ng && i < (uint32_t)GOFF_LDS; i += NT) s_goff[i] = a.goff[i];
     }
     if (tid == 0) { s_nbig = 0; s_kept = 0; }
     __syncthreads();
@@ -1250,31 +1254,31 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
     if (!filt || A0 > 65535u) { defer(); return; }
     {
         // ---- P1: seen / seen-twice bitmaps
-        for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
+        for (uint32_t i = tid; i < 2 * nw; i += NT) dyn[i] = 0;
         __syncthreads();
         // staged per group of SORT_U1 keys: all cells, then all first atomics
         // (LDS round trips overlap instead of one chain per key)
-        for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U1) {
+        for (uint32_t i0 = 0; i0 < A0; i0 += NT * SORT_U1) {
             uint64_t x[SORT_U1];
             uint32_t c[SORT_U1], old[SORT_U1];
 #pragma unroll
-            for (int u = 0; u < SORT_U1; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
+            for (int u = 0; u < SORT_U1; ++u) { const uint32_t i = i0 + (uint32_t)u * NT + tid; x[u] = i < A0 ? K[i] : 0; }
 #pragma unroll
             for (int u = 0; u < SORT_U1; ++u) c[u] = cell_of(x[u]);
 #pragma unroll
             for (int u = 0; u < SORT_U1; ++u) {
-                const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
+                const uint32_t i = i0 + (uint32_t)u * NT + tid;
                 old[u] = i < A0 ? atomicOr(&B1[c[u] >> 5], 1u << (c[u] & 31)) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < SORT_U1; ++u) {
-                const uint32_t i = i0 + (uint32_t)u * 1024 + tid, bit = 1u << (c[u] & 31);
+                const uint32_t i = i0 + (uint32_t)u * NT + tid, bit = 1u << (c[u] & 31);
                 if (i < A0 && (old[u] & bit)) atomicOr(&B2[c[u] >> 5], bit);   // seen before: seen twice
             }
         }
         __syncthreads();
         // ---- KC (in place of B2) and the word prefix of its popcounts (in place of B1)
-        const uint32_t per = (nw + 1023) >> 10;
+        const uint32_t per = (nw + NT - 1) / NT;
         const uint32_t wa = min(nw, (uint32_t)tid * per), wb = min(nw, wa + per);
         uint32_t loc = 0;
         for (uint32_t w = wa; w < wb; ++w) {
@@ -1285,7 +1289,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
             loc += (uint32_t)__popc(kc);
         }
         uint32_t nkc;
-        uint32_t run = block_excl_sum(loc, nkc, s_sc);      // its barriers end the B1 reads
+        uint32_t run = block_excl_sum<NW>(loc, nkc, s_sc);      // its barriers end the B1 reads
         for (uint32_t w = wa; w < wb; ++w) { B1[w] = run; run += (uint32_t)__popc(B2[w]); }
         SORT_PH(0);
         if (pq && tid == 0) pq[13] = nkc;
@@ -1302,7 +1306,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
             constexpr uint64_t kmask = (1ULL << 48) - 1;
             uint32_t* C = dyn + cofs;
             uint64_t* S = dyn64;
-            for (uint32_t i = tid; i < cw; i += 1024) C[i] = 0;
+            for (uint32_t i = tid; i < cw; i += NT) C[i] = 0;
             __syncthreads();
             auto c16 = [&](uint32_t rk) -> uint32_t { return (C[rk >> 1] >> ((rk & 1) << 4)) & 0xffffu; };
             // ---- P2: counts per kept cell; the largest dropped key.  Each key's
@@ -1312,18 +1316,18 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
             uint64_t smx = 0;
             uint16_t* T16 = (uint16_t*)(a.meta + base);
             // staged like P1: all cells, all bitmap reads, then counts and tags
-            for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U2) {
+            for (uint32_t i0 = 0; i0 < A0; i0 += NT * SORT_U2) {
                 uint64_t x[SORT_U2];
                 uint32_t c[SORT_U2], kw[SORT_U2], pw[SORT_U2];
 #pragma unroll
-                for (int u = 0; u < SORT_U2; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
+                for (int u = 0; u < SORT_U2; ++u) { const uint32_t i = i0 + (uint32_t)u * NT + tid; x[u] = i < A0 ? K[i] : 0; }
 #pragma unroll
                 for (int u = 0; u < SORT_U2; ++u) c[u] = cell_of(x[u]);
 #pragma unroll
                 for (int u = 0; u < SORT_U2; ++u) { kw[u] = B2[c[u] >> 5]; pw[u] = B1[c[u] >> 5]; }
 #pragma unroll
                 for (int u = 0; u < SORT_U2; ++u) {
-                    const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
+                    const uint32_t i = i0 + (uint32_t)u * NT + tid;
                     if (i < A0) {
                         const uint32_t b = c[u] & 31;
                         const bool kept = (kw[u] >> b) & 1u;
@@ -1334,14 +1338,14 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                     }
                 }
             }
-            smx = block_max64(smx, red);               // (its barriers also end the count atomics)
+            smx = block_max64<NW>(smx, red);               // (its barriers also end the count atomics)
             // exclusive scan of the u16 counts, in place (offsets < A0 <= 65535)
-            const uint32_t per2 = (cw + 1023) >> 10;
+            const uint32_t per2 = (cw + NT - 1) / NT;
             const uint32_t ca = min(cw, (uint32_t)tid * per2), cb = min(cw, ca + per2);
             uint32_t l2 = 0;
             for (uint32_t i = ca; i < cb; ++i) { const uint32_t v = C[i]; l2 += (v & 0xffffu) + (v >> 16); }
             uint32_t A;
-            uint32_t o = block_excl_sum(l2, A, s_sc);
+            uint32_t o = block_excl_sum<NW>(l2, A, s_sc);
             for (uint32_t i = ca; i < cb; ++i) {
                 const uint32_t v = C[i], lo = v & 0xffffu;
                 C[i] = o | ((o + lo) << 16);
@@ -1366,7 +1370,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                     __syncthreads();
                     if (tid == 0) s_kept = 0;
                     __syncthreads();
-                    block_pass_kmu<8>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m, bool valid) {
+                    block_pass_kmu<8, NT>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m, bool valid) {
                         const bool mine = valid && (uint32_t)m == ra;
                         const uint64_t mb = ballot(mine);
                         uint32_t wb0 = 0;
@@ -1391,7 +1395,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                 // window keys carry their rank in the top 16 bits: the rank rises
                 // with the key, so the order is unchanged, and a key's segment is
                 // one shift away
-                block_pass_km<SORT_UG>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m) {
+                block_pass_km<SORT_UG, NT>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m) {
                     const uint32_t rk = m;
                     if (m != 0xffffu && rk >= ra && rk < rb) {
                         const uint32_t sh = (rk & 1) << 4;
@@ -1410,8 +1414,8 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                 };
                 // A: chunks holding a segment longer than SEG_TINY: one wave sorts 64 keys
                 const uint32_t nch = (nwin + 63) >> 6;
-                for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 32) {   // two chunks at a time (q, q + 16)
-                    const uint32_t ia = q * 64 + (uint32_t)lane, ib = ia + 16 * 64;
+                for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 2 * NW) {   // two chunks at a time (q, q + NW)
+                    const uint32_t ia = q * 64 + (uint32_t)lane, ib = ia + NW * 64;
                     const bool va = ia < nwin, vb = ib < nwin;
                     uint64_t xa = S[va ? ia : 0], xb = S[vb ? ib : 0];
                     uint32_t sa, ea, sb, eb;
@@ -1430,7 +1434,7 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                 // by their low dwords.
                 const uint32_t* S32 = (const uint32_t*)S;
                 uint32_t pc_tiny = 0, pc_long = 0, pc_srch = 0;     // MM2G_KNOB_SORT_PROF segment classes
-                for (uint32_t i = tid; i < nwin; i += 1024) {
+                for (uint32_t i = tid; i < nwin; i += NT) {
                     const uint64_t x = S[i];
                     uint32_t s, e;
                     seg_of(x, s, e);
@@ -1480,23 +1484,25 @@ __global__ __launch_bounds__(1024) void k_sort_read(SortArgs a) {
                     const uint32_t L = sg.y - sg.x;
                     if (L <= SEG_RANK) {
                         __syncthreads();
-                        block_pass8<4>(O + sg.x, L, [&](uint32_t i, uint64_t x) { dyn64[i] = x; });
+                        block_pass8<4, NT>(O + sg.x, L, [&](uint32_t i, uint64_t x) { dyn64[i] = x; });
                         __syncthreads();
-                        const uint32_t i0 = (uint32_t)tid, i1 = (uint32_t)tid + 1024;
-                        const uint64_t x0 = i0 < L ? dyn64[i0] : U64MAX, x1 = i1 < L ? dyn64[i1] : U64MAX;
-                        uint32_t r0 = 0, r1 = 0;
-                        if (L > 1024) {
-                            for (uint32_t j = 0; j < L; ++j) {
-                                const uint64_t y = dyn64[j];
-                                r0 += (y < x0 || (y == x0 && j < i0)) ? 1u : 0u;
-                                r1 += (y < x1 || (y == x1 && j < i1)) ? 1u : 0u;
+                        constexpr int KPT = (int)SEG_RANK / NT;   // keys per thread
+                        uint64_t xk[KPT];
+                        uint32_t rk[KPT];
+#pragma unroll
+                        for (int u = 0; u < KPT; ++u) { const uint32_t iu = (uint32_t)tid + (uint32_t)u * NT; xk[u] = iu < L ? dyn64[iu] : U64MAX; rk[u] = 0; }
+                        const int nu = (int)((L + NT - 1) / NT);
+                        for (uint32_t j = 0; j < L; ++j) {
+                            const uint64_t y = dyn64[j];
+#pragma unroll
+                            for (int u = 0; u < KPT; ++u) {
+                                const uint32_t iu = (uint32_t)tid + (uint32_t)u * NT;
+                                if (u < nu) rk[u] += (y < xk[u] || (y == xk[u] && j < iu)) ? 1u : 0u;
                             }
-                        } else {
-                            for (uint32_t j = 0; j < L; ++j) { const uint64_t y = dyn64[j]; r0 += (y < x0 || (y == x0 && j < i0)) ? 1u : 0u; }
                         }
                         __syncthreads();
-                        if (i0 < L) O[sg.x + r0] = x0;
-                        if (i1 < L) O[sg.x + r1] = x1;
+#pragma unroll
+                        for (int u = 0; u < KPT; ++u) { const uint32_t iu = (uint32_t)tid + (uint32_t)u * NT; if (iu < L) O[sg.x + rk[u]] = xk[u]; }
                     }
                 }
             }
@@ -1921,7 +1927,6 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
 // the end of every block.  Keys are prefetched one block ahead.
 // ============================================================================
 constexpr int DP_NW = 4;          // waves per workgroup
-constexpr int SPEC_ROUNDS = 3;    // k_chain_long: speculative rounds per 64-anchor block before the per-anchor path
 constexpr int RING_WORDS = 256;   // 8192-bit mark ring (max_iter <= 8000)
 constexpr int RK = 256;           // anchor ring entries per wave (power of two, >= 256)
 static_assert((RK & (RK - 1)) == 0 && RK >= 256, "anchor ring size");
@@ -2615,7 +2620,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
             // its guess is exact, and so is that lane's result (all its inputs
             // were exact): each round commits at least one anchor.  A lane whose
             // loop would run past its 64 predecessors, and every anchor left after
-            // SPEC_ROUNDS rounds, takes the per-anchor path below.
+            // a.spec_rounds rounds, takes the per-anchor path below.
             int32_t i_seq = ib;
             if (a.lazy) {
                 const int32_t k = i0 + lane;
@@ -2659,7 +2664,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 }
                 wave_lds_sync();
                 int32_t committed = ib;
-                for (int rnd = 0; rnd < SPEC_ROUNDS && committed < ie; ++rnd) {
+                for (int rnd = 0; rnd < (int)a.spec_rounds && committed < ie; ++rnd) {
                     const bool act0 = kv && k >= committed;
                     int32_t mf = span, mj = -1, ns = 0, vis = 0;
                     uint64_t mkm = 0;       // marks t[j] = k by offset d = k - j (bit d-1)
@@ -3120,14 +3125,18 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
             if constexpr (G) {
                 int32_t *v0 = val, *p0 = gptr, *v1 = val2, *p1 = gptr2;
                 for (int d = 0; d < dbl; ++d) {
+                    bool live = false;
                     for (int t = tid; t < len; t += 1024) {
                         const int32_t p = p0[t];
                         v1[t] = p >= 0 ? v0[t] + v0[p] : v0[t];
-                        p1[t] = p >= 0 ? p0[p] : -1;
+                        const int32_t np = p >= 0 ? p0[p] : -1;
+                        p1[t] = np;
+                        live = live || np >= 0;
                     }
-                    __syncthreads();
+                    const bool more = __syncthreads_or(live);   // every pointer at a root: the forest's depth is reached
                     int32_t* tv = v0; v0 = v1; v1 = tv;
                     int32_t* tp = p0; p0 = p1; p1 = tp;
+                    if (!more) break;
                 }
                 vres = v0;
             } else {
@@ -3762,12 +3771,21 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
         lds = std::min<size_t>(lds, (size_t)SORT_LDS);
         SortArgs b = a;
         b.lds_words = (uint32_t)(lds / 4);
-        if (2u * b.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_read<true>, dim3(a.n), dim3(1024), lds, st, b);
-        else hipLaunchKernelGGL(k_sort_read<false>, dim3(a.n), dim3(1024), lds, st, b);
+        // up to SORT_LDS_HALF: 512-thread workgroups, two per CU (one read's
+        // barrier and latency phases overlap the other's)
+        const bool gl = 2u * b.n_seq + 2u > (uint32_t)GOFF_LDS;
+        if (lds <= (size_t)SORT_LDS_HALF) {
+            if (gl) hipLaunchKernelGGL((k_sort_read<true, 512>), dim3(a.n), dim3(512), lds, st, b);
+            else hipLaunchKernelGGL((k_sort_read<false, 512>), dim3(a.n), dim3(512), lds, st, b);
+        } else if (gl) hipLaunchKernelGGL((k_sort_read<true, 1024>), dim3(a.n), dim3(1024), lds, st, b);
+        else hipLaunchKernelGGL((k_sort_read<false, 1024>), dim3(a.n), dim3(1024), lds, st, b);
     } else if (a.cells) {       // the singleton filter is on: every listed read takes the bucket path
         SortArgs b = a;
         b.lds_words = (uint32_t)(SORT_LDS / 4);
-        const unsigned grid = std::min<uint32_t>(a.n, 1024);
+        // persistent workgroups on a work counter: one per CU (the LDS allows no
+        // more); most batches list no read, and every extra workgroup would wait
+        // for a CU the other streams' kernels hold
+        const unsigned grid = std::min<uint32_t>(a.n, 256);
         if (2u * b.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_big<true>, dim3(grid), dim3(1024), (size_t)SORT_LDS, st, b);
         else hipLaunchKernelGGL(k_sort_big<false>, dim3(grid), dim3(1024), (size_t)SORT_LDS, st, b);
     } else {

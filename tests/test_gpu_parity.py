@@ -257,14 +257,15 @@ def test_cli_align_gpu(small_world, tmp_path):
     assert g == c and g.count("\n") > 50
 
 
-@pytest.mark.parametrize("seg_small", [1024, 64, 8, 1])
-def test_filtered_sort_parity(dev, small_world, dense_world, seg_small):
+@pytest.mark.parametrize("seg_small,lds_kb", [(1024, 0), (64, 0), (8, 0), (1, 0), (1024, 76), (8, 76)])
+def test_filtered_sort_parity(dev, small_world, dense_world, seg_small, lds_kb):
     """Production sort (cell buckets + per-segment ranking, singleton filter
     on): the anchors the DP runs on equal the oracle's sorted anchors minus
     the singletons, for every path -- thread-ranked small segments, block-
     ranked and radix-sorted big ones, the whole-read radix when too many big
-    segments (seg_small 1) or too many anchors (> 65535) appear."""
-    with knobs(dev, sort_small=1, seg_small=seg_small):
+    segments (seg_small 1) or too many anchors (> 65535) appear.  lds_kb 76:
+    the 512-thread, two-per-CU k_sort_read (smaller windows, more of them)."""
+    with knobs(dev, sort_small=1, seg_small=seg_small, sort_lds_kb=lds_kb):
         rng = random.Random(5)
         for world, mids in ((small_world, (None,)), (dense_world, (20, 5000, 100000))):
             ref, reads, rnames, rseqs = world
