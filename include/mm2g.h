@@ -292,7 +292,11 @@ enum {
     MM2G_KNOB_STOP_AT = 21,      /* measurement only (results invalid): 1 stop after the anchors, 2 after the
                                     sort, 3 no rescue pass, 4 no dv kernel; 0 = full path [0]                 */
     MM2G_KNOB_SPEC_ROUNDS = 22,  /* speculative 64-anchor rounds of k_chain_long per block, 0..16 [3]            */
-    MM2G_KNOB_COUNT = 23
+    MM2G_KNOB_MED_PAIRS = 23,    /* pass 0 (production): segments of up to this many estimated DP pairs take one
+                                    lane (k_chain_med), longer ones a wave (k_chain_long); 0 = every segment
+                                    over 8 anchors to a wave [0]                                                 */
+    MM2G_KNOB_MED_PAIRS_RESCUE = 24, /* the same for the rescue pass [0]                                          */
+    MM2G_KNOB_COUNT = 25
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

@@ -95,6 +95,8 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_FILTER: case MM2G_KNOB_LAZY: case MM2G_KNOB_PRUNE: case MM2G_KNOB_GIANT: return 1;
     case MM2G_KNOB_MIDHIST_BINS: return 4096;
     case MM2G_KNOB_SPEC_ROUNDS: return 3;
+    case MM2G_KNOB_MED_PAIRS: return 0;
+    case MM2G_KNOB_MED_PAIRS_RESCUE: return 0;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -798,7 +800,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
     build_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1);
     int16_t* lut; uint32_t* work;
-    ENSURE(c->lut, int16_t, c->h_lut.size(), lut);
+    ENSURE(c->lut, int16_t, (c->h_lut.size() + 7) & ~(size_t)7, lut);   // whole 16-B words (load_lut)
     ENSURE(c->work, uint32_t, 4, work);
     if (c->lut_dirty || c->lut_dev != c->lut.p) {   // the pen LUT stays resident; copied only when it changes
         HIPCHK(hipMemcpyAsync(lut, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice, c->stream));
@@ -879,6 +881,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         for (int stg = 0; stg < 5; ++stg) {
             ca.giant_min = giant_min[pass];
             ca.giant_exact = pass == 0 ? 1u : 0u;
+            ca.est_lane = (int32_t)std::max<int64_t>(0, std::min<int64_t>(1 << 20, K[pass ? MM2G_KNOB_MED_PAIRS_RESCUE : MM2G_KNOB_MED_PAIRS]));
             if (stg == 2) {   // longest-first order of the long segments (k_chain_giant and k_chain_long)
                 ProfScope ps(c, names[pass][stg]);
                 LCHK(launch_chain_stage(2, ca, 1, c->stream));

@@ -205,6 +205,7 @@ struct ChainArgs {
     uint32_t giant_gmax;     // global variant: anchors per workgroup scratch slice (0 = off)
     void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
     uint32_t spec_rounds = 3; // k_chain_long: speculative rounds per 64-anchor block (MM2G_KNOB_SPEC_ROUNDS)
+    int32_t est_lane = 0;    // k_chain_seg (production): estimated DP pairs up to which a segment takes one lane
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
     const uint32_t* abort = nullptr;
     unsigned long long* gprof = nullptr;   // MM2G_LSEG_PROF: k_chain_giant phase sums (16 counters)

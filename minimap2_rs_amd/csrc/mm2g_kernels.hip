@@ -1059,6 +1059,25 @@ DEVI void block_pass_u(const uint64_t* src, uint32_t n, F fn) {
     }
 }
 
+// the comput_sc pen LUT (n int16) into LDS in 16-B words, four in flight per
+// thread: the rescue pass's LUT (bw_long + 1 = 20,001 entries, 40 KB) was 80
+// dependent 2-byte load steps per thread at 256 threads (chain_seg rescue
+// 0.137 -> 0.115 ms per 10 k reads, 1 stream).  Both sides hold whole 16-B
+// words (LDS: lut_lds; HBM: the LUT buffer is allocated in 8-entry units).
+DEVI void load_lut(int16_t* lut, const int16_t* g, int n) {
+    const int nv = (n * 2 + 15) >> 4;
+    const uint4* src = (const uint4*)g;
+    uint4* dst = (uint4*)lut;
+    const int nt = (int)blockDim.x;
+    for (int i0 = (int)threadIdx.x; i0 < nv; i0 += 4 * nt) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { const int i = i0 + u * nt; if (i < nv) v[u] = src[i]; }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { const int i = i0 + u * nt; if (i < nv) dst[i] = v[u]; }
+    }
+}
+
 // exclusive scan over a block of NW waves (all threads call it: it holds barriers)
 template <int NW = 16>
 DEVI uint32_t block_excl_sum(uint32_t v, uint32_t& total, uint32_t* sc) {
@@ -1988,10 +2007,13 @@ DEVI void best_merge(int32_t& bf, int32_t& bi, int32_t f, int32_t i) {
 constexpr int KRING = 512;        // per-wave LDS ring of the newest anchor keys (k_chain_seg)
 constexpr int TQ = 128;           // per-wave LDS queue per tiny length class (2 | 3-4 | 5-8 anchors)
 constexpr int MEDB = 128;         // per-wave LDS buffer of medium segments before the global append
-constexpr int64_t EST_LANE = 2048;   // estimated DP pairs above which a segment goes to a whole wave
-// rescue pass (few reads, GPU otherwise idle) and pruned pass 0 (few segments
-// survive): latency matters, so only small segments stay on one lane
-constexpr int64_t EST_LANE_RESCUE = 96;
+constexpr int64_t EST_LANE = 2048;   // estimated DP pairs above which a segment goes to a whole wave (debug mode)
+// Production (a.est_lane, knobs med_pairs / med_pairs_rescue, both 0): every
+// segment over TINY anchors goes to a wave.  One lane walks its segment with a
+// dependent HBM round trip per step: k_chain_med took ~0.3 ms per 10 k reads
+// (1 stream) in each pass whatever its work (6.9 k rescued anchors as much as
+// 0.8 M pass-0 anchors), set by its slowest lane; k_chain_long absorbs the
+// same segments for +0.08 ms (pass 0) and +0.00 ms (rescue).
 
 // Scalar chain_dp_all (lchain.rs:73-90) of one segment of <= TINY anchors held
 // in registers (keys from the wave's LDS key ring); `act` lanes only.  Local indices; marks t[pprev[j]] = i are a
@@ -2112,7 +2134,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     uint8_t* tls = (uint8_t*)(tqs + DP_NW * 3 * TQ);            // their lengths
     int2* medbs = (int2*)(tls + DP_NW * 3 * TQ);
     if (blockIdx.x * DP_NW >= (uint32_t)a.item_off[a.n]) return;   // no work item for this workgroup: skip the LUT load
-    for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
+    load_lut(lut, a.lut, P.lut_n);
     __syncthreads();
     const int lane = lane_id(), wv = wave_id();
     uint64_t* kring = krings + wv * KRING;
@@ -2202,7 +2224,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
                 const int64_t bp = p1 - p0 > 0 ? (int64_t)(p1 - p0) : 1;
                 int64_t win = ((int64_t)len * maxdx + bp - 1) / bp;
                 win = win < len ? win : len;
-                med = (int64_t)len * win / 2 <= ((P.pass == 0 && !a.fmin) ? EST_LANE : EST_LANE_RESCUE);
+                med = (int64_t)len * win / 2 <= ((P.pass == 0 && !a.fmin) ? EST_LANE : (int64_t)a.est_lane);
             }
             const bool big = emit && len > TINY && !med;
             const uint64_t medM = ballot(med);
@@ -2314,7 +2336,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
     if (blockIdx.x * (blockDim.x >> 6) >= (uint32_t)a.item_off[a.n]) return;   // no work item: skip the LUT load
-    for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
+    load_lut(lut, a.lut, P.lut_n);
     __syncthreads();
     const int lane = lane_id();
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
@@ -2387,7 +2409,7 @@ __global__ __launch_bounds__(256) void k_chain_med(ChainArgs a) {
     const ChainKParams P = a.P;
     int16_t* lut = (int16_t*)smem;
     if (blockIdx.x * blockDim.x >= min(*a.mseg_n, a.mseg_cap)) return;   // no queue entry: skip the LUT load
-    for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
+    load_lut(lut, a.lut, P.lut_n);
     __syncthreads();
     const uint32_t qb = a.kl.qb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << a.kl.rb) - 1;
@@ -2549,7 +2571,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
     uint64_t* rkeys = (uint64_t*)(rings + DP_NW * RING_WORDS);
     int2* rfps = (int2*)(rkeys + DP_NW * RK);
     if (blockIdx.x * DP_NW >= min(*a.lseg_n, a.lseg_cap)) return;   // no long segment: skip the LUT load
-    for (int i = threadIdx.x; i < P.lut_n; i += blockDim.x) lut[i] = a.lut[i];
+    load_lut(lut, a.lut, P.lut_n);
     for (int i = threadIdx.x; i < DP_NW * RING_WORDS; i += blockDim.x) rings[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wv = wave_id();
@@ -3052,7 +3074,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
         }
         if (!mine) return;
     }
-    for (int i = tid; i < P.lut_n; i += 1024) lut[i] = a.lut[i];
+    load_lut(lut, a.lut, P.lut_n);
     __syncthreads();
     const uint32_t qb = a.kl.qb, rb = a.kl.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
