@@ -296,8 +296,7 @@ enum {
                                     lane (k_chain_med), longer ones a wave (k_chain_long); 0 = every segment
                                     over 8 anchors to a wave [0]                                                 */
     MM2G_KNOB_MED_PAIRS_RESCUE = 24, /* the same for the rescue pass [0]                                          */
-    MM2G_KNOB_RUN_PRUNE = 25,    /* the sort drops cell runs whose anchors x span < a lower bound of the read's best f [0] */
-    MM2G_KNOB_COUNT = 26
+    MM2G_KNOB_COUNT = 25
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

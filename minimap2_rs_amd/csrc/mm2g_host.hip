@@ -93,7 +93,6 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_GIANT_GMAX: return 65536;
     case MM2G_KNOB_GIANT_GBLOCKS: return 256;
     case MM2G_KNOB_FILTER: case MM2G_KNOB_LAZY: case MM2G_KNOB_PRUNE: case MM2G_KNOB_GIANT: return 1;
-    case MM2G_KNOB_RUN_PRUNE: return 0;   // measured slower on C3 so far (DESIGN.md "Run pruning")
     case MM2G_KNOB_MIDHIST_BINS: return 4096;
     case MM2G_KNOB_SPEC_ROUNDS: return 3;
     case MM2G_KNOB_MED_PAIRS: return 0;
@@ -227,7 +226,7 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
     fprintf(stderr, "[sort_prof] A0 q10/50/90/99/max=%u/%u/%u/%u/%u  A q10/50/90/99/max=%u/%u/%u/%u/%u  kept cells q10/50/90/99/max=%u/%u/%u/%u/%u\n",
             Q(q0, .1), Q(q0, .5), Q(q0, .9), Q(q0, .99), q0.back(), Q(q2, .1), Q(q2, .5), Q(q2, .9), Q(q2, .99), q2.back(),
             Q(q3, .1), Q(q3, .5), Q(q3, .9), Q(q3, .99), q3.back());
-    fprintf(stderr, "[sort_prof] reads=%u (whole-read radix %.0f, bucket path %.0f) A0=%.0f A=%.0f nbig=%.2f windows=%.2f us/read: p1+kc=%.1f p2=%.1f gather=%.1f prune=%.1f chunk=%.1f rank=%.1f p4b/radix=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
+    fprintf(stderr, "[sort_prof] reads=%u (whole-read radix %.0f, bucket path %.0f) A0=%.0f A=%.0f nbig=%.2f windows=%.2f us/read: p1+kc=%.1f p2=%.1f gather=%.1f segs=%.1f chunk=%.1f rank=%.1f p4b/radix=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
             m, nleg, nbigp, a0 / m, a2 / m, np / m, ph[7] / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
             ph[5] / m / 100, ph[6] / m / 100, tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
     fprintf(stderr, "[sort_prof] keys per read in segments <= %u: %.0f, 17..64: %.0f, > 64: %.0f (%.2f other-chunk searches each)\n",
@@ -776,20 +775,6 @@ static void build_lut(mm2g_ctx* c, float gap, int n) {
     c->lut_dirty = true;
 }
 
-// The pen LUT on the device (built for dd < n; kept while gap and n fit).
-static int upload_lut(mm2g_ctx* c, float gap, int n, int16_t** out) {
-    build_lut(c, gap, n);
-    int16_t* lut;
-    ENSURE(c->lut, int16_t, (c->h_lut.size() + 7) & ~(size_t)7, lut);   // whole 16-B words (load_lut)
-    if (c->lut_dirty || c->lut_dev != c->lut.p) {   // the pen LUT stays resident; copied only when it changes
-        HIPCHK(hipMemcpyAsync(lut, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        c->lut_dirty = false; c->lut_dev = c->lut.p;
-    }
-    *out = lut;
-    return 0;
-}
-
 // Argument checks of the Align flow (main.rs:189-230) shared by map and the stage entry points.
 static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_t& mdx1) {
     if (!(o->w > 0 && o->w < 256 && o->k > 0 && o->k <= 28)) return set_err(MM2G_E_ARG, "invalid w/k (0 < w < 256, 0 < k <= 28)");
@@ -813,9 +798,15 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                      unsigned long long* stat = nullptr) {
     int32_t *fb, *pb;
     ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
+    build_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1);
     int16_t* lut; uint32_t* work;
-    if (int e = upload_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1, &lut)) return e;
+    ENSURE(c->lut, int16_t, (c->h_lut.size() + 7) & ~(size_t)7, lut);   // whole 16-B words (load_lut)
     ENSURE(c->work, uint32_t, 4, work);
+    if (c->lut_dirty || c->lut_dev != c->lut.p) {   // the pen LUT stays resident; copied only when it changes
+        HIPCHK(hipMemcpyAsync(lut, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->lut_dirty = false; c->lut_dev = c->lut.p;
+    }
     HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));
     uint32_t* order;
     ENSURE(c->order, uint32_t, n, order);
@@ -1106,17 +1097,9 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.rlist = rlist; so.rcount = rlist + n; so.rwork = rlist + n + 1;
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
-    const int64_t stop_at = K[MM2G_KNOB_STOP_AT];   // measurement only: later stages skipped, results invalid
-    // run pruning: the sort drops cell runs that cannot hold the read's best f
-    // (pass 0's lower bound; valid for the rescue pass too: DESIGN.md "Run pruning")
-    if (filt && K[MM2G_KNOB_RUN_PRUNE]) {
-        int16_t* lut;
-        if (int e = upload_lut(c, 0.01f * 0.8f * (float)o->k, std::max(o->bw, o->bw_long) + 1, &lut)) return e;
-        so.lut = lut;
-        so.lb_maxdx = mdx0; so.lb_maxdy = std::max(o->max_gap, o->bw); so.lb_bw = o->bw; so.lb_span = o->k;
-    }
     uint64_t* sprof = nullptr;
     if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 128)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 128, c->stream)); so.prof = sprof; }
+    const int64_t stop_at = K[MM2G_KNOB_STOP_AT];   // measurement only: later stages skipped, results invalid
     if (stop_at != 1) {
     {
         ProfScope ps(c, "sort_small");

@@ -167,10 +167,6 @@ struct SortArgs {
     uint32_t* rcount = nullptr;
     const uint32_t* order = nullptr;   // k_sort_read: block b sorts read order[b] (heaviest first); null = b
     uint32_t* rwork = nullptr;         // k_sort_big: next list entry to take (zeroed by k_sort_small)
-    // run pruning (k_sort_read): the pass-0 comput_sc pen LUT and parameters of
-    // the best-f lower bound; lut == null = off (DESIGN.md "Run pruning")
-    const int16_t* lut = nullptr;
-    int32_t lb_maxdx = 0, lb_maxdy = 0, lb_bw = 0, lb_span = 0;
 };
 struct ChainArgs {
     uint32_t n;

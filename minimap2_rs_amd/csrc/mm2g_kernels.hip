@@ -942,52 +942,6 @@ constexpr int SORT_LDS_HALF = 76 * 1024; // ... two 512-thread workgroups per CU
 #define SORT_UG SORT_U                    // ... in the window gathers
 #endif
 
-// ---- wave scans (DPP), shared by the sort's run pruning and the chain kernels
-template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
-DEVI int32_t dpp(int32_t old, int32_t src) { return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, BANK_MASK, false); }
-// inclusive max-scan over the wave (row_shr 1/2/4/8, row_bcast 15/31)
-DEVI int32_t scan_max(int32_t v) {
-    v = max(v, dpp<0x111>(INT_MIN, v)); v = max(v, dpp<0x112>(INT_MIN, v));
-    v = max(v, dpp<0x114>(INT_MIN, v)); v = max(v, dpp<0x118>(INT_MIN, v));
-    v = max(v, dpp<0x142, 0xa>(INT_MIN, v)); v = max(v, dpp<0x143, 0xc>(INT_MIN, v));
-    return v;
-}
-// OR over the wave (row_shr 1/2/4/8 + row_bcast 15/31 leave the total in lane 63)
-DEVI uint32_t wave_or32(uint32_t v) {
-    int32_t x = (int32_t)v;
-    x |= dpp<0x111>(0, x); x |= dpp<0x112>(0, x); x |= dpp<0x114>(0, x); x |= dpp<0x118>(0, x);
-    x |= dpp<0x142, 0xa>(0, x); x |= dpp<0x143, 0xc>(0, x);
-    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
-}
-// lane l <- lane l-1, lane 0 <- old0 (wave_shr:1)
-DEVI int32_t shr1_dpp(int32_t v, int32_t old0) { return dpp<0x138>(old0, v); }
-// composition scan of x -> max(x + a, b) in lane order (earlier applied first)
-DEVI void scan_nskip(int32_t& a, int32_t& b) {
-    constexpr int32_t NEG = -(1 << 29);
-#define NS_STEP(CTRL, RM)                                                   \
-    {                                                                       \
-        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
-        b = max(ob + a, b); a = oa + a;                                     \
-    }
-    NS_STEP(0x111, 0xf) NS_STEP(0x112, 0xf) NS_STEP(0x114, 0xf) NS_STEP(0x118, 0xf)
-    NS_STEP(0x142, 0xa) NS_STEP(0x143, 0xc)
-#undef NS_STEP
-}
-
-// the same composition scan with the additive part clamped at NEG (a chain of
-// "no predecessor" steps must not overflow)
-DEVI void scan_lb(int32_t& a, int32_t& b) {
-    constexpr int32_t NEG = -(1 << 29);
-#define LB_STEP(CTRL, RM)                                                   \
-    {                                                                       \
-        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
-        b = max(ob + a, b); a = max(oa + a, NEG);                           \
-    }
-    LB_STEP(0x111, 0xf) LB_STEP(0x112, 0xf) LB_STEP(0x114, 0xf) LB_STEP(0x118, 0xf)
-    LB_STEP(0x142, 0xa) LB_STEP(0x143, 0xc)
-#undef LB_STEP
-}
-
 // 8 independent loads per thread, then fn(i, x) for each (i < n): hides HBM
 // latency in the block-wide passes of k_sort_read
 template <int U = 8, int NT = 1024, typename F>
@@ -1265,69 +1219,6 @@ DEVI void radix_range(uint64_t* src, uint64_t* dst, uint64_t* out, uint32_t A, u
     __syncthreads();
 }
 
-// Run pruning: a lower bound of the read's best f over n keys in sorted order
-// (one contiguous range of the read's sorted anchors, e.g. one cell run or its
-// prefix).  In chain_dp_all (lchain.rs:73-90) the first predecessor visited
-// for a non-isolated anchor i is i - 1, so f[i] >= LB[i] = max(span, LB[i-1] +
-// sc(i, i-1)) (k_chain_lb's recurrence, pass-0 parameters); the range's first
-// anchor restarts at span, which is still a lower bound.  LB is a composition
-// of x -> max(x + a, b) maps: every wave of the block scans one slice to its
-// composition (CA, CB) and to (alpha, beta) with max over the slice of LB =
-// max(c + alpha, beta) for an incoming c; thread 0 chains the slices.  All
-// threads call it (barriers); the result is returned to every thread.
-template <int NW>
-DEVI int32_t run_lb(const uint64_t* R, uint32_t n, const SortArgs& a, uint32_t qb, uint32_t gsh, uint64_t rmask, int32_t* sl) {
-    constexpr int32_t NEG = -(1 << 29);
-    const int lane = lane_id(), wv = wave_id();
-    const uint64_t qmask = (1ULL << qb) - 1;
-    const int32_t span = a.lb_span;
-    const uint32_t per = ((n + NW - 1) / NW + 63) & ~63u;
-    const uint32_t i0 = min(n, (uint32_t)wv * per), i1 = min(n, i0 + per);
-    int32_t CA = 0, CB = NEG, al = NEG, be = NEG;        // identity map; no position yet
-    uint64_t k0 = i0 > 0 && i0 < i1 ? R[i0 - 1] : 0;
-    uint32_t prev_lo = (uint32_t)k0, prev_hi = (uint32_t)(k0 >> 32);
-    for (uint32_t i00 = i0; i00 < i1; i00 += 64) {
-        const uint32_t il = i00 + (uint32_t)lane;
-        const bool valid = il < i1;
-        const uint64_t ak = valid ? R[il] : 0;
-        const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)prev_hi) << 32) |
-                            (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)prev_lo);
-        const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
-        const int32_t p = (int32_t)((ak >> qb) & rmask), pj = (int32_t)((pk >> qb) & rmask);
-        const int32_t q = (int32_t)(ak & qmask), qj = (int32_t)(pk & qmask);
-        const bool iso = il == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)a.lb_maxdx);
-        int32_t sa = valid ? NEG : 0, sb = valid ? span : NEG;   // invalid lanes: the identity map
-        if (valid && !iso) {
-            const int32_t dq = q - qj, dr = p - pj;
-            const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-            if (dq > 0 && dq <= a.lb_maxdx && dr != 0 && dq <= a.lb_maxdy && dd <= a.lb_bw) {
-                const int32_t dg = dr < dq ? dr : dq;
-                sa = (span < dg ? span : dg) - (int32_t)a.lut[dd];
-            }
-        }
-        scan_lb(sa, sb);
-        // prefix maps from the slice start: x -> max(x + CA + sa, max(CB + sa, sb))
-        const int32_t pa = max(CA + sa, NEG), pb = max(max(CB + sa, NEG), sb);
-        al = max(al, valid ? pa : NEG); be = max(be, valid ? pb : NEG);
-        CA = rdl(pa, 63); CB = rdl(pb, 63);
-        prev_lo = rdlu((uint32_t)ak, 63); prev_hi = rdlu((uint32_t)(ak >> 32), 63);
-    }
-    al = rdl(scan_max(al), 63); be = rdl(scan_max(be), 63);
-    __syncthreads();
-    if (lane == 0) { sl[4 * wv] = CA; sl[4 * wv + 1] = CB; sl[4 * wv + 2] = al; sl[4 * wv + 3] = be; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t c = NEG, best = span;
-        for (int w = 0; w < NW; ++w) {
-            best = max(best, max(c + sl[4 * w + 2], sl[4 * w + 3]));
-            c = max(max(c + sl[4 * w], NEG), sl[4 * w + 1]);
-        }
-        sl[4 * NW] = best;
-    }
-    __syncthreads();
-    return sl[4 * NW];
-}
-
 // GL: the group offsets stay in HBM (2 n_seq + 2 > GOFF_LDS).  A template
 // parameter rather than a pointer chosen at run time: a pointer that may be
 // LDS or global compiles to flat loads, and every flat load waits for all
@@ -1338,7 +1229,6 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t red[32];
     __shared__ uint32_t s_sc[16], s_kept, s_nbig;
-    __shared__ int32_t s_lbv, s_lbs[4 * 16 + 1];
     __shared__ uint2 s_big[BIG_MAX];
     __shared__ uint32_t s_goff[GOFF_LDS];
     extern __shared__ uint64_t dyn64[];
@@ -1429,14 +1319,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
         // top 16 bits, which the key layout must leave free.
         const uint32_t cofs = LW >= cw + 2 ? (LW - cw) & ~1u : 0u;
         const uint32_t kbits = gsh + (32u - (uint32_t)__builtin_clz(2u * a.n_seq | 1u));
-        // run pruning (a.lut set): below C the run-start bitmap RS (a bit per kept
-        // cell) and D (u16 per kept cell: its compacted output offset, 0xffff =
-        // pruned); both must stay clear of the bitmaps, which RS is built from
-        const uint32_t rsw = (nkc + 31) >> 5;
-        const uint32_t dofs0 = cofs >= rsw + cw + 2 ? (cofs - rsw - cw) & ~1u : 0u;
-        const bool prune = a.lut != nullptr && dofs0 >= 2 * nw && (dofs0 >> 1) >= SEG_RANK;
-        const uint32_t dofs = prune ? dofs0 : cofs;
-        const uint32_t W = dofs >> 1;                        // keys per window
+        const uint32_t W = cofs >> 1;                        // keys per window
         if (kbits > 48u || qb + CELL_SHIFT > 32u || cofs < 2 * nw || W < SEG_RANK) { defer(); return; }
         {
             constexpr uint64_t kmask = (1ULL << 48) - 1;
@@ -1487,62 +1370,14 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 C[i] = o | ((o + lo) << 16);
                 o += lo + (v >> 16);
             }
-            if (tid == 0) { a.smax[r] = smx; s_lbv = a.lb_span; }
-            // ---- run starts: kept cell c starts a run when cell c - 1 is not kept.
-            // A DP segment (consecutive anchors <= max_dist_x <= 2^CELL_SHIFT apart,
-            // one group) lies inside one run of consecutive kept cells.
-            uint32_t* RS = dyn + (cofs - rsw);
-            uint16_t* D16 = (uint16_t*)(dyn + dofs);
-            if (prune) {
-                for (uint32_t i = tid; i < rsw; i += NT) RS[i] = 0;
-                __syncthreads();
-                for (uint32_t w = wa; w < wb; ++w) {
-                    const uint32_t kc = B2[w];
-                    uint32_t m = kc & ~((kc << 1) | (w ? B2[w - 1] >> 31 : 0u));
-                    while (m) {
-                        const uint32_t b = (uint32_t)__builtin_ctz(m);
-                        m &= m - 1;
-                        const uint32_t rk = B1[w] + (uint32_t)__popc(kc & ((1u << b) - 1u));
-                        atomicOr(&RS[rk >> 5], 1u << (rk & 31));
-                    }
-                }
-            }
+            if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; }
             __syncthreads();
             SORT_PH(1);
             // ---- P3/P4: windows of whole kept cells (<= W keys), each gathered from K
             // into LDS by cell (C turns from start into end offsets as cells are
             // filled), chunk-sorted and ranked per cell segment into O.
             auto offx = [&](uint32_t rk) -> uint32_t { return rk < nkc ? c16(rk) : A; };   // start of an unfilled cell
-            // run pruning helpers (RS): the run start at or before x, the next one after x (or lim)
-            auto prev_start = [&](uint32_t x) -> uint32_t {
-                int32_t y = (int32_t)x;
-                for (;;) {       // rank 0 always starts a run
-                    const uint32_t v = RS[(uint32_t)y >> 5] & (0xffffffffu >> (31 - ((uint32_t)y & 31)));
-                    if (v) return ((uint32_t)y & ~31u) + 31u - (uint32_t)__builtin_clz(v);
-                    y = (int32_t)((uint32_t)y & ~31u) - 1;
-                }
-            };
-            auto next_start = [&](uint32_t x, uint32_t lim) -> uint32_t {
-                uint32_t y = x + 1;
-                while (y < lim) {
-                    const uint32_t v = RS[y >> 5] >> (y & 31);
-                    if (v) { y += (uint32_t)__builtin_ctz(v); break; }
-                    y = (y | 31u) + 1;
-                }
-                return min(y, lim);
-            };
-            // start offset (uncompacted) of rank x once ranks < rbw are gathered (C holds their end offsets)
-            auto st0 = [&](uint32_t x, uint32_t rbw) -> uint32_t {
-                if (x >= nkc) return A;
-                if (x == 0) return 0u;
-                return x < rbw ? c16(x - 1) : c16(x);
-            };
-            // a run survives when run anchors x span >= the lower bound of the read's best f
-            auto run_keep = [&](uint32_t x, uint32_t rbw, int32_t lbr) -> bool {
-                const uint32_t r0 = prev_start(x), r1 = next_start(x, nkc);
-                return (int32_t)(st0(r1, rbw) - st0(r0, rbw)) * a.lb_span >= lbr;
-            };
-            uint32_t ra = 0, oc = 0;      // oc: compacted output cursor (run pruning)
+            uint32_t ra = 0;
             while (ra < nkc) {
                 const uint32_t oa = c16(ra);
                 uint32_t lo = ra + 1, hi = nkc;                       // last rb with offx(rb) <= oa + W
@@ -1551,32 +1386,26 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 const uint32_t ob = offx(rb);
                 if (ob > oa + W) {
                     // cell ra alone exceeds the window: gather it into O unsorted (P4b sorts it)
-                    const bool keep = !prune || run_keep(ra, ra, s_lbv);
-                    const uint32_t dst = prune ? oc : oa;
                     __syncthreads();
                     if (tid == 0) s_kept = 0;
                     __syncthreads();
-                    if (keep) block_pass_kmu<8, NT>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m, bool valid) {
+                    block_pass_kmu<8, NT>(K, T16, A0, [&](uint32_t, uint64_t x, uint16_t m, bool valid) {
                         const bool mine = valid && (uint32_t)m == ra;
                         const uint64_t mb = ballot(mine);
                         uint32_t wb0 = 0;
                         if (lane == 0 && mb) wb0 = atomicAdd(&s_kept, (uint32_t)__popcll(mb));
                         wb0 = (uint32_t)__shfl((int)wb0, 0, 64);
-                        if (mine) O[CK(dst + wb0 + (uint32_t)__popcll(mb & lanemask_lt()), A0)] = x;
+                        if (mine) O[CK(oa + wb0 + (uint32_t)__popcll(mb & lanemask_lt()), A0)] = x;
                     });
                     __syncthreads();
                     if (tid == 0) {
                         const uint32_t sh = (ra & 1) << 4;
                         C[ra >> 1] = (C[ra >> 1] & ~(0xffffu << sh)) | (ob << sh);   // now its end offset
-                        if (prune) D16[ra] = keep ? (uint16_t)dst : (uint16_t)0xffffu;
-                        if (keep) {
-                            const uint32_t slot = s_nbig++;
-                            if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(dst, dst + (ob - oa));
-                        }
+                        const uint32_t slot = s_nbig++;
+                        if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa, ob);
                     }
                     __syncthreads();
                     SORT_PH(2);
-                    if (prune && keep) oc += ob - oa;
                     ra = ra + 1;
                     continue;
                 }
@@ -1602,98 +1431,6 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                     s = (rk ? c16(rk - 1) : 0u) - oa;
                     e = c16(rk) - oa;
                 };
-                const uint32_t* S32 = (const uint32_t*)S;
-                // rank of window key i inside its cell segment [s, e) (L <= seg_small;
-                // the chunks holding segments over SEG_TINY are sorted)
-                auto rank_in = [&](uint32_t i, uint32_t xl, uint32_t s, uint32_t e) -> uint32_t {
-                    uint32_t rank = 0;
-                    if (e - s <= SEG_TINY) {
-                        for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
-                    } else {
-                        const uint32_t co = i >> 6;
-                        rank = i - max(s, co << 6);
-                        for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
-                            if (c == co) continue;
-                            rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
-                        }
-                    }
-                    return rank;
-                };
-                // ---- run pruning (DESIGN.md "Run pruning"): sort the window's largest
-                // run into R (after the window's keys), take the lower bound of the
-                // read's best f over it (k_chain_lb's recurrence), keep the runs whose
-                // anchors x span reach it, and give the kept cells compacted offsets.
-                bool lbw = false;
-                uint32_t r0b = 0, r1b = 0, s0b = 0, e0b = 0;
-                uint64_t* R = S + nwin;
-                if (prune) {
-                    const uint32_t nrk = rb - ra, perr = (nrk + NT - 1) / NT;
-                    const uint32_t xa = ra + min(nrk, (uint32_t)tid * perr), xb = ra + min(nrk, (uint32_t)tid * perr + perr);
-                    uint64_t cand = 0;
-                    for (uint32_t x = xa; x < xb; ++x) {
-                        if (x != ra && !((RS[x >> 5] >> (x & 31)) & 1u)) continue;
-                        const uint32_t y = next_start(x, rb);
-                        const uint32_t cn = c16(y - 1) - (x == ra ? oa : c16(x - 1));
-                        const uint64_t v = ((uint64_t)cn << 32) | (0xffffu - x);
-                        cand = v > cand ? v : cand;
-                    }
-                    cand = block_max64<NW>(cand, red);
-                    const uint32_t nbst = (uint32_t)(cand >> 32);
-                    r0b = 0xffffu - (uint32_t)(cand & 0xffffu);
-                    r1b = next_start(r0b, rb);
-                    s0b = (r0b == ra ? oa : c16(r0b - 1)) - oa;
-                    e0b = c16(r1b - 1) - oa;
-                    lbw = nbst >= 2 && nwin + nbst <= W;
-                    if (lbw) {
-                        if (tid == 0) s_kept = 0;       // flags a cell over SEG_RANK (no bound from this window)
-                        for (uint32_t q = (s0b >> 6) + (uint32_t)wave_id(); q < (e0b + 63) >> 6; q += NW) {
-                            const uint32_t ia = q * 64 + (uint32_t)lane;
-                            const bool va = ia < nwin;
-                            uint64_t xk = S[va ? ia : 0];
-                            uint32_t sa, ea;
-                            seg_of(xk, sa, ea);
-                            xk = va ? xk : U64MAX;
-                            if (any(va && ea - sa > SEG_TINY)) { wave_bitonic64_np(xk); if (va) S[ia] = xk; }
-                        }
-                        __syncthreads();
-                        for (uint32_t i = s0b + tid; i < e0b; i += NT) {
-                            const uint64_t x = S[i];
-                            uint32_t s, e;
-                            seg_of(x, s, e);
-                            const uint32_t L = e - s, xl = (uint32_t)x;
-                            if (L > SEG_RANK) { s_kept = 1; continue; }
-                            R[s - s0b + rank_in(i, xl, s, e)] = x & kmask;
-                        }
-                        __syncthreads();
-                        lbw = s_kept == 0;
-                    }
-                    if (lbw) {
-                        const int32_t m = run_lb<NW>(R, e0b - s0b, a, qb, gsh, rmask, s_lbs);
-                        if (tid == 0 && m > s_lbv) s_lbv = m;
-                    }
-                    __syncthreads();
-                    // kept runs -> compacted offsets of the window's cells (D16)
-                    const int32_t lbr = s_lbv;
-                    uint32_t loc = 0, R1 = 0;
-                    bool kp = true;
-                    for (uint32_t x = xa; x < xb; ++x) {
-                        if (x == xa || x >= R1) { R1 = next_start(x, nkc); kp = run_keep(x, rb, lbr); }
-                        if (kp) loc += c16(x) - (x == ra ? oa : c16(x - 1));
-                    }
-                    uint32_t kept_w;
-                    uint32_t o2 = oc + block_excl_sum<NW>(loc, kept_w, s_sc);
-                    for (uint32_t x = xa; x < xb; ++x) {
-                        if (x == xa || x >= R1) { R1 = next_start(x, nkc); kp = run_keep(x, rb, lbr); }
-                        D16[x] = kp ? (uint16_t)o2 : (uint16_t)0xffffu;
-                        if (kp) o2 += c16(x) - (x == ra ? oa : c16(x - 1));
-                    }
-                    oc += kept_w;
-                    __syncthreads();
-                }
-                SORT_PH(3);
-                // a key is skipped by the chunk and rank phases when its run was pruned or is
-                // the bound's run (written from R)
-                auto skip_rk = [&](uint32_t rk) -> bool { return prune && (D16[rk] == 0xffffu || (lbw && rk >= r0b && rk < r1b)); };
                 // A: chunks holding a segment longer than SEG_TINY: one wave sorts 64 keys
                 const uint32_t nch = (nwin + 63) >> 6;
                 for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 2 * NW) {   // two chunks at a time (q, q + NW)
@@ -1703,10 +1440,9 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                     uint32_t sa, ea, sb, eb;
                     seg_of(xa, sa, ea);
                     seg_of(xb, sb, eb);
-                    const bool ka = va && !skip_rk((uint32_t)(xa >> 48)), kb = vb && !skip_rk((uint32_t)(xb >> 48));
                     xa = va ? xa : U64MAX; xb = vb ? xb : U64MAX;
-                    const bool na = any(ka && ea - sa > SEG_TINY && ea - sa <= a.seg_small);
-                    const bool nb = any(kb && eb - sb > SEG_TINY && eb - sb <= a.seg_small);
+                    const bool na = any(va && ea - sa > SEG_TINY && ea - sa <= a.seg_small);
+                    const bool nb = any(vb && eb - sb > SEG_TINY && eb - sb <= a.seg_small);
                     if (na) { wave_bitonic64_np(xa); if (va) S[ia] = xa; }
                     if (nb) { wave_bitonic64_np(xb); if (vb) S[ib] = xb; }
                 }
@@ -1714,34 +1450,39 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 SORT_PH(4);
                 // B: ranks inside the segments.  Keys of one segment share every bit
                 // above the cell-local lb <= 32 (rank, group, cell), so they compare
-                // by their low dwords.  Output offset of a segment: D16 (run pruning)
-                // or its uncompacted start.
+                // by their low dwords.
+                const uint32_t* S32 = (const uint32_t*)S;
                 uint32_t pc_tiny = 0, pc_long = 0, pc_srch = 0;     // MM2G_KNOB_SORT_PROF segment classes
                 for (uint32_t i = tid; i < nwin; i += NT) {
                     const uint64_t x = S[i];
-                    const uint32_t rk = (uint32_t)(x >> 48);
-                    if (skip_rk(rk)) continue;
                     uint32_t s, e;
                     seg_of(x, s, e);
                     const uint32_t L = e - s;
-                    const uint32_t os = prune ? (uint32_t)D16[rk] : oa + s;
                     if (L > a.seg_small) {             // P4b; copied unsorted
-                        O[os + (i - s)] = x & kmask;
+                        O[oa + i] = x & kmask;
                         if (i == s) {
                             const uint32_t slot = atomicAdd(&s_nbig, 1u);
-                            if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(os, os + L);
+                            if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s, oa + e);
                         }
                         continue;
                     }
+                    const uint32_t xl = (uint32_t)x;
+                    uint32_t rank = 0;
                     if (pq) {
                         if (L <= SEG_TINY) ++pc_tiny;
                         else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
                     }
-                    O[os + rank_in(i, (uint32_t)x, s, e)] = x & kmask;
-                }
-                if (lbw) {
-                    const uint32_t os = D16[r0b];
-                    for (uint32_t j = tid; j < e0b - s0b; j += NT) O[os + j] = R[j];
+                    if (L <= SEG_TINY) {
+                        for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
+                    } else {
+                        const uint32_t co = i >> 6;
+                        rank = i - max(s, co << 6);
+                        for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
+                            if (c == co) continue;
+                            rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
+                        }
+                    }
+                    O[oa + s + rank] = x & kmask;
                 }
                 if (pq) {
                     const uint64_t v14 = wave_sum64(((uint64_t)pc_long << 32) | pc_tiny), v15 = wave_sum64(pc_srch);
@@ -1751,7 +1492,6 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 SORT_PH(5);
                 ra = rb;
             }
-            if (tid == 0) a.cnt2[r] = prune ? oc : A;
             // ---- P4b: cells over seg_small, one at a time by the whole block (K is scratch now)
             const uint32_t nbig = s_nbig;
             bool big_radix = nbig > (uint32_t)BIG_MAX;
@@ -1925,8 +1665,7 @@ template <bool GL>
 __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;
     __shared__ uint64_t red[32];
-    __shared__ uint32_t s_sc[16], s_read, s_nbig, s_c0;
-    __shared__ int32_t s_lbs[4 * 16 + 1];
+    __shared__ uint32_t s_sc[16], s_read, s_nbig;
     __shared__ uint2 s_big[BIG_MAX];
     __shared__ uint32_t s_goff[GOFF_LDS];
     extern __shared__ uint64_t dyn64[];
@@ -2038,172 +1777,9 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
         uint32_t A;
         uint32_t o = block_excl_sum(l2, A, s_sc);
         for (uint32_t i = ca; i < cb; ++i) { const uint32_t v = CNT[i]; CNT[i] = o; o += v; }
-        if (tid == 0) { a.smax[r] = smx; s_nbig = 0; }
+        if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; s_nbig = 0; }
         __syncthreads();
         BIG_PH(1);
-        // ---- run pruning (DESIGN.md "Run pruning"; one bucket per kept cell
-        // only).  The largest cell run's prefix that fits the free LDS is
-        // gathered, sorted into its place in O and scanned for a lower bound of
-        // the read's best f; runs whose anchors x span stay below it are dropped,
-        // the kept cells get compacted offsets, and the sorted prefix moves to its
-        // own (P3 skips its keys and the dropped ones).
-        const uint32_t rsw = (nkc + 31) >> 5;
-        uint32_t* RSb = dyn + 2 * nw;
-        uint32_t* PRb = RSb + rsw;
-        const uint32_t xofs = (2 * nw + 2 * rsw + 1) & ~1u;
-        const uint32_t WX = cofs > xofs + 128 ? (cofs - xofs) >> 1 : 0u;
-        uint64_t* X = dyn64 + (xofs >> 1);
-        const bool prn = a.lut != nullptr && bsh == 0 && WX >= 64 && 2 * WX >= NB + 1;
-        bool lbok = false;
-        uint32_t r0 = 0, rp = 0, s0p = 0, np = 0, keptA = A;
-        auto rank_of = [&](uint64_t x) -> uint32_t {
-            const uint32_t c = cell_of(x), b = c & 31;
-            return B1[c >> 5] + (uint32_t)__popc(B2[c >> 5] & ((1u << b) - 1u));
-        };
-        auto next_start = [&](uint32_t x, uint32_t lim) -> uint32_t {
-            uint32_t y = x + 1;
-            while (y < lim) {
-                const uint32_t v = RSb[y >> 5] >> (y & 31);
-                if (v) { y += (uint32_t)__builtin_ctz(v); break; }
-                y = (y | 31u) + 1;
-            }
-            return min(y, lim);
-        };
-        auto prev_start = [&](uint32_t x) -> uint32_t {
-            int32_t y = (int32_t)x;
-            for (;;) {       // rank 0 always starts a run
-                const uint32_t v = RSb[(uint32_t)y >> 5] & (0xffffffffu >> (31 - ((uint32_t)y & 31)));
-                if (v) return ((uint32_t)y & ~31u) + 31u - (uint32_t)__builtin_clz(v);
-                y = (int32_t)((uint32_t)y & ~31u) - 1;
-            }
-        };
-        if (prn) {
-            for (uint32_t i = tid; i < 2 * rsw; i += 1024) RSb[i] = 0;
-            __syncthreads();
-            for (uint32_t w = wa; w < wb; ++w) {
-                const uint32_t kc = B2[w];
-                uint32_t m = kc & ~((kc << 1) | (w ? B2[w - 1] >> 31 : 0u));
-                while (m) {
-                    const uint32_t b = (uint32_t)__builtin_ctz(m);
-                    m &= m - 1;
-                    const uint32_t rk = B1[w] + (uint32_t)__popc(kc & ((1u << b) - 1u));
-                    atomicOr(&RSb[rk >> 5], 1u << (rk & 31));
-                }
-            }
-            __syncthreads();
-            auto st = [&](uint32_t x) -> uint32_t { return x < NB ? CNT[x] : A; };   // cell starts (NB == nkc)
-            const uint32_t perr = (nkc + 1023) >> 10;
-            const uint32_t xa = min(nkc, (uint32_t)tid * perr), xb = min(nkc, xa + perr);
-            uint64_t cand = 0;
-            for (uint32_t x = xa; x < xb; ++x) {
-                if (!((RSb[x >> 5] >> (x & 31)) & 1u)) continue;
-                const uint64_t v = ((uint64_t)(st(next_start(x, nkc)) - st(x)) << 32) | (0xffffu - x);
-                cand = v > cand ? v : cand;
-            }
-            cand = block_max64(cand, red);
-            r0 = 0xffffu - (uint32_t)(cand & 0xffffu);
-            const uint32_t r1 = next_start(r0, nkc);
-            s0p = st(r0);
-            uint32_t lo = r0, hi = r1;          // the most cells of the run whose keys fit X
-            while (lo < hi) { const uint32_t mid = (lo + hi + 1) >> 1; if (st(mid) - s0p <= WX) lo = mid; else hi = mid - 1; }
-            rp = lo;
-            np = st(rp) - s0p;
-            lbok = (cand >> 32) >= 2 && np >= 2;
-        }
-        if (lbok) {
-            // gather the prefix by cell (its cells' CNT turn into end offsets, as P3 leaves them)
-            for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U2) {
-                uint64_t x[SORT_U2];
-                uint32_t rk[SORT_U2];
-#pragma unroll
-                for (int u = 0; u < SORT_U2; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
-#pragma unroll
-                for (int u = 0; u < SORT_U2; ++u) {
-                    const uint32_t c = cell_of(x[u]), b = c & 31;
-                    const uint32_t kw = B2[c >> 5];
-                    rk[u] = ((kw >> b) & 1u) ? B1[c >> 5] + (uint32_t)__popc(kw & ((1u << b) - 1u)) : 0xffffffffu;
-                }
-#pragma unroll
-                for (int u = 0; u < SORT_U2; ++u) {
-                    const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
-                    if (i < A0 && rk[u] >= r0 && rk[u] < rp) X[atomicAdd(&CNT[rk[u]], 1u) - s0p] = x[u];
-                }
-            }
-            __syncthreads();
-            auto segx = [&](uint64_t x, uint32_t& s, uint32_t& e) {
-                const uint32_t rk = rank_of(x);
-                s = (rk == r0 ? s0p : CNT[rk - 1]) - s0p;
-                e = CNT[rk] - s0p;
-            };
-            for (uint32_t q = (uint32_t)wave_id(); q < (np + 63) >> 6; q += 16) {
-                const uint32_t i = q * 64 + (uint32_t)lane;
-                const bool v = i < np;
-                uint64_t xk = X[v ? i : 0];
-                uint32_t sq, eq;
-                segx(xk, sq, eq);
-                xk = v ? xk : U64MAX;
-                if (any(v && eq - sq > SEG_TINY)) { wave_bitonic64_np(xk); if (v) X[i] = xk; }
-            }
-            __syncthreads();
-            for (uint32_t i = tid; i < np; i += 1024) {
-                const uint64_t x = X[i];
-                uint32_t s0, e0;
-                segx(x, s0, e0);
-                uint32_t rank = 0;
-                if (e0 - s0 <= SEG_TINY) {
-                    for (uint32_t j = s0; j < e0; ++j) { const uint64_t y = X[j]; rank += (y < x || (y == x && j < i)) ? 1u : 0u; }
-                } else {
-                    const uint32_t co = i >> 6;
-                    rank = i - max(s0, co << 6);
-                    for (uint32_t c = s0 >> 6; c <= (e0 - 1) >> 6; ++c) {
-                        if (c == co) continue;
-                        rank += count_below(X, max(s0, c << 6), min(e0, (c << 6) + 64), x, c < co);
-                    }
-                }
-                O[s0p + s0 + rank] = x;
-            }
-            __syncthreads();
-            const int32_t lbr = run_lb<16>(O + s0p, np, a, qb, gsh, rmask, s_lbs);
-            // start of cell y (uncompacted): the prefix's cells hold end offsets now
-            auto st2 = [&](uint32_t y) -> uint32_t { return y == r0 ? s0p : (y > r0 && y <= rp) ? CNT[y - 1] : (y < NB ? CNT[y] : A); };
-            auto keep = [&](uint32_t x) -> bool { return (int32_t)(st2(next_start(x, nkc)) - st2(prev_start(x))) * a.lb_span >= lbr; };
-            const uint32_t perr = (nkc + 1023) >> 10;
-            const uint32_t xa = min(nkc, (uint32_t)tid * perr), xb = min(nkc, xa + perr);
-            uint32_t loc = 0, R1 = 0;
-            bool kp = true;
-            for (uint32_t x = xa; x < xb; ++x) {
-                if (x == xa || x >= R1) { R1 = next_start(x, nkc); kp = keep(x); }
-                if (kp) loc += st2(x + 1) - st2(x);
-            }
-            uint32_t tot;
-            uint32_t o2 = block_excl_sum(loc, tot, s_sc);
-            uint32_t* CN2 = (uint32_t*)X;      // compacted offsets (X is dead)
-            for (uint32_t x = xa; x < xb; ++x) {
-                if (x == xa || x >= R1) { R1 = next_start(x, nkc); kp = keep(x); }
-                const uint32_t c = st2(x + 1) - st2(x);
-                if (x == r0) s_c0 = o2;
-                CN2[x] = (x >= r0 && x < rp) ? o2 + c : o2;     // the prefix's cells: their end (placed below)
-                if (!kp) atomicOr(&PRb[x >> 5], 1u << (x & 31));
-                if (kp) o2 += c;
-            }
-            __syncthreads();
-            for (uint32_t x = tid; x < NB; x += 1024) CNT[x] = CN2[x];
-            keptA = tot;
-            const uint32_t c0 = s_c0;
-            __syncthreads();
-            if (c0 != s0p) {      // move the sorted prefix down (chunks in increasing order: no unread source is overwritten)
-                for (uint32_t j0 = 0; j0 < np; j0 += 1024) {
-                    const uint32_t j = j0 + tid;
-                    const uint64_t v = j < np ? O[s0p + j] : 0;
-                    __syncthreads();
-                    if (j < np) O[c0 + j] = v;
-                    __syncthreads();
-                }
-            }
-            s0p = c0;       // from here: the prefix's compacted range [s0p, s0p + np)
-        }
-        if (tid == 0) a.cnt2[r] = keptA;
-        auto in_prefix = [&](uint32_t s0, uint32_t e0) -> bool { return lbok && s0 >= s0p && e0 <= s0p + np; };
         // ---- P3: scatter of the kept keys by bucket; CNT[b] turns into bucket b's end
         for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U2) {
             uint64_t x[SORT_U2];
@@ -2220,9 +1796,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                 const uint32_t b = c[u] & 31;
                 if (i < A0 && ((kw[u] >> b) & 1u)) {
                     const uint32_t bk = (pw[u] + (uint32_t)__popc(kw[u] & ((1u << b) - 1u))) >> bsh;
-                    // run pruning: the prefix is in place, dropped runs are not copied
-                    if (!lbok || (!(bk >= r0 && bk < rp) && !((PRb[bk >> 5] >> (bk & 31)) & 1u)))
-                        O[CK(atomicAdd(&CNT[bk], 1u), A0)] = x[u];
+                    O[CK(atomicAdd(&CNT[bk], 1u), A0)] = x[u];
                 }
             }
         }
@@ -2244,7 +1818,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
         while (ba < NB) {
             const uint32_t oa = bstart(ba);
             if (CNT[ba] - oa > W) {                 // one bucket beyond a window: radix in HBM
-                if (!in_prefix(oa, CNT[ba])) radix_big(oa, CNT[ba]);
+                radix_big(oa, CNT[ba]);
                 if (pq && tid == 0) pq[7] += 1;
                 ba = ba + 1;
                 continue;
@@ -2314,7 +1888,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                 const uint32_t L = e0 - s0;
                 if (L > SEG_RANK) {
                     O[oa + i] = x;
-                    if (i == s0 && !in_prefix(oa + s0, oa + e0)) { const uint32_t slot = atomicAdd(&s_nbig, 1u); if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s0, oa + e0); }
+                    if (i == s0) { const uint32_t slot = atomicAdd(&s_nbig, 1u); if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s0, oa + e0); }
                     continue;
                 }
                 uint32_t rank = 0;
@@ -2341,7 +1915,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
             BIG_PH(6);
             ba = bb;
         }
-        if (pq && tid == 0) { pq[8] = A0; pq[9] = (0xfffeULL << 32) | keptA; pq[11] = wall_clock64(); }
+        if (pq && tid == 0) { pq[8] = A0; pq[9] = (0xfffeULL << 32) | A; pq[11] = wall_clock64(); }
 #undef BIG_PH
     }
 }
@@ -2375,6 +1949,51 @@ constexpr int DP_NW = 4;          // waves per workgroup
 constexpr int RING_WORDS = 256;   // 8192-bit mark ring (max_iter <= 8000)
 constexpr int RK = 256;           // anchor ring entries per wave (power of two, >= 256)
 static_assert((RK & (RK - 1)) == 0 && RK >= 256, "anchor ring size");
+
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+DEVI int32_t dpp(int32_t old, int32_t src) { return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, BANK_MASK, false); }
+// inclusive max-scan over the wave (row_shr 1/2/4/8, row_bcast 15/31)
+DEVI int32_t scan_max(int32_t v) {
+    v = max(v, dpp<0x111>(INT_MIN, v)); v = max(v, dpp<0x112>(INT_MIN, v));
+    v = max(v, dpp<0x114>(INT_MIN, v)); v = max(v, dpp<0x118>(INT_MIN, v));
+    v = max(v, dpp<0x142, 0xa>(INT_MIN, v)); v = max(v, dpp<0x143, 0xc>(INT_MIN, v));
+    return v;
+}
+// OR over the wave (row_shr 1/2/4/8 + row_bcast 15/31 leave the total in lane 63)
+DEVI uint32_t wave_or32(uint32_t v) {
+    int32_t x = (int32_t)v;
+    x |= dpp<0x111>(0, x); x |= dpp<0x112>(0, x); x |= dpp<0x114>(0, x); x |= dpp<0x118>(0, x);
+    x |= dpp<0x142, 0xa>(0, x); x |= dpp<0x143, 0xc>(0, x);
+    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
+// lane l <- lane l-1, lane 0 <- old0 (wave_shr:1)
+DEVI int32_t shr1_dpp(int32_t v, int32_t old0) { return dpp<0x138>(old0, v); }
+// composition scan of x -> max(x + a, b) in lane order (earlier applied first)
+DEVI void scan_nskip(int32_t& a, int32_t& b) {
+    constexpr int32_t NEG = -(1 << 29);
+#define NS_STEP(CTRL, RM)                                                   \
+    {                                                                       \
+        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
+        b = max(ob + a, b); a = oa + a;                                     \
+    }
+    NS_STEP(0x111, 0xf) NS_STEP(0x112, 0xf) NS_STEP(0x114, 0xf) NS_STEP(0x118, 0xf)
+    NS_STEP(0x142, 0xa) NS_STEP(0x143, 0xc)
+#undef NS_STEP
+}
+
+// the same composition scan with the additive part clamped at NEG (a chain of
+// "no predecessor" steps must not overflow)
+DEVI void scan_lb(int32_t& a, int32_t& b) {
+    constexpr int32_t NEG = -(1 << 29);
+#define LB_STEP(CTRL, RM)                                                   \
+    {                                                                       \
+        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
+        b = max(ob + a, b); a = max(oa + a, NEG);                           \
+    }
+    LB_STEP(0x111, 0xf) LB_STEP(0x112, 0xf) LB_STEP(0x114, 0xf) LB_STEP(0x118, 0xf)
+    LB_STEP(0x142, 0xa) LB_STEP(0x143, 0xc)
+#undef LB_STEP
+}
 
 constexpr uint32_t LSEG_DONE = 0xffffffffu;   // lseg[].w: handled by k_chain_giant
 constexpr int TINY = CHAIN_TINY;  // segments up to this many anchors: one lane, registers

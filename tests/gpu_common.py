@@ -159,38 +159,3 @@ def _singleton_keep(a: np.ndarray) -> np.ndarray:
     left = np.array([(c - 1) in occ for c in cell.tolist()], dtype=bool)
     right = np.array([(c + 1) in occ for c in cell.tolist()], dtype=bool)
     return (cnt[inv] >= 2) | left | right
-
-
-def _cell_ids(a: np.ndarray) -> np.ndarray:
-    """32 kb cell of each (x, y) anchor in its (rid, strand) group or the Q19
-    pseudo-group (as _singleton_keep); non-decreasing on sorted anchors."""
-    x = a[:, 0]
-    hi = x >> np.uint64(32)
-    gid = np.where(hi == np.uint64(0xffffffff), np.uint64(1 << 33), hi)
-    return (gid << np.uint64(20)) | ((x & np.uint64(0x7fffffff)) >> np.uint64(15))
-
-
-def assert_run_pruning(got: np.ndarray, want: np.ndarray, what=""):
-    """Run pruning (DESIGN.md "Run pruning"): the device's sorted anchors `got`
-    are the singleton-filtered oracle anchors `want` with some cell runs
-    (maximal runs of consecutive kept cells) cut to a prefix or dropped, and
-    every cut run is one that cannot reach the read's best pass-0 f: its
-    anchors x span (15) stay below max f of chain_dp_all over `want`."""
-    if len(got) == len(want):
-        assert np.array_equal(got, want), what
-        return
-    assert len(got) < len(want), what
-    cell = _cell_ids(want).astype(np.int64)
-    run = np.concatenate([[0], np.cumsum(np.diff(cell) > 1)])
-    pos = {(int(a), int(b)): i for i, (a, b) in enumerate(want.tolist())}
-    idx = np.array([pos[(int(a), int(b))] for a, b in got.tolist()], dtype=np.int64)
-    assert (np.diff(idx) > 0).all(), what + ": not an ordered subsequence"
-    f = O.chain_dp(want, 15, bw=500)[0]
-    maxf = int(np.max(f))
-    tot = np.bincount(run)
-    kept = np.bincount(run[idx], minlength=len(tot))
-    for k in np.nonzero(kept < tot)[0]:
-        first = int(np.searchsorted(run, k))
-        sel = idx[run[idx] == k]
-        assert np.array_equal(sel, np.arange(first, first + len(sel))), what + f": run {k} is not cut to a prefix"
-        assert int(tot[k]) * 15 < maxf, what + f": run {k} of {tot[k]} anchors dropped, best f {maxf}"

@@ -20,7 +20,7 @@ import pytest
 import minimap2_rs_amd as M
 from oracle import oracle as O
 from tools import simdata
-from tests.gpu_common import _singleton_keep, assert_records, assert_run_pruning, knobs
+from tests.gpu_common import _singleton_keep, assert_records, knobs
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -118,10 +118,6 @@ def test_c3_hg38_300_x_10kb(hg38, tmp_path):
     seqs, rn = _reads(gbuf, lens, 300, 10000, 3)
     res, rec = _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c3")
     assert (rec[:, 0] & 8).sum() > 20 and (rec[:, 0] & 2).sum() >= 1     # panics and rescues are covered
-    for r in range(20):       # run pruning in k_sort_read
-        want, _ = oi.anchors(seqs[r], 10, 15, mid)
-        if len(want) > 1:
-            assert_run_pruning(dev.debug_anchors(r), want[_singleton_keep(want)], f"c3 read {r}")
     dev.set_reads(seqs[:60])
     got = dev.seed_batch(M.map_opts())
     for r in range(60):
@@ -148,23 +144,16 @@ def test_c5_hg38_100kb(hg38, tmp_path):
     assert rec[:, 1].max() > 65535
     rescued = [r for r in range(len(seqs)) if res[r].flags & 2]
     assert len(rescued) >= 4
-    for r in list(range(4)) + rescued[:2]:       # run pruning in the bucket sort (k_sort_big)
+    for r in rescued:
         want, _ = oi.anchors(seqs[r], 10, 15, mid)
-        assert_run_pruning(dev.debug_anchors(r), want[_singleton_keep(want)], f"c5 read {r}")
-    # the rescue pass's DP arrays, on every kept anchor (run pruning off)
-    with knobs(dev, run_prune=0):
-        dev.set_reads(seqs)
-        assert_records(dev.map(M.map_opts()), seqs, rec, "c5 no run pruning")
-        for r in rescued:
-            want, _ = oi.anchors(seqs[r], 10, 15, mid)
-            want = want[_singleton_keep(want)]
-            got = dev.debug_anchors(r)
-            assert np.array_equal(got, want), r
-            f, pp, _, _, _ = O.chain_dp(want, 15, bw=20000)
-            gf, gpp = dev.debug_dp(r)
-            n = len(want)
-            assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
-    with knobs(dev, giant_lcap=64, run_prune=0):
+        want = want[_singleton_keep(want)]
+        got = dev.debug_anchors(r)
+        assert np.array_equal(got, want), r
+        f, pp, _, _, _ = O.chain_dp(want, 15, bw=20000)
+        gf, gpp = dev.debug_dp(r)
+        n = len(want)
+        assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
+    with knobs(dev, giant_lcap=64):
         res2, _ = _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5hbm")
         for r in rescued:
             want, _ = oi.anchors(seqs[r], 10, 15, mid)

@@ -12,7 +12,7 @@ import pytest
 import minimap2_rs_amd as M
 from oracle import oracle as O
 from tools import simdata
-from tests.gpu_common import (_mutate, _production_vs_oracle, _rand_seq, _singleton_keep, assert_records, assert_run_pruning, dense_world, knobs,  # noqa: F401
+from tests.gpu_common import (_mutate, _production_vs_oracle, _rand_seq, _singleton_keep, assert_records, dense_world, knobs,  # noqa: F401
                               small_world)
 
 pytestmark = pytest.mark.gpu
@@ -265,7 +265,7 @@ def test_filtered_sort_parity(dev, small_world, dense_world, seg_small, lds_kb):
     ranked and radix-sorted big ones, the whole-read radix when too many big
     segments (seg_small 1) or too many anchors (> 65535) appear.  lds_kb 76:
     the 512-thread, two-per-CU k_sort_read (smaller windows, more of them)."""
-    with knobs(dev, sort_small=1, seg_small=seg_small, sort_lds_kb=lds_kb, run_prune=0):
+    with knobs(dev, sort_small=1, seg_small=seg_small, sort_lds_kb=lds_kb):
         rng = random.Random(5)
         for world, mids in ((small_world, (None,)), (dense_world, (20, 5000, 100000))):
             ref, reads, rnames, rseqs = world
@@ -286,39 +286,6 @@ def test_filtered_sort_parity(dev, small_world, dense_world, seg_small, lds_kb):
                         want = want[_singleton_keep(want)]
                     got = dev.debug_anchors(r)
                     assert np.array_equal(got, want), (seg_small, mid, r, len(got), len(want))
-    dev.set_debug(True)
-
-
-@pytest.mark.parametrize("seg_small,lds_kb", [(1024, 0), (64, 76)])
-def test_run_pruning(dev, small_world, dense_world, seg_small, lds_kb):
-    """Run pruning on (the default): the anchors the DP runs on are the
-    singleton-filtered oracle anchors minus whole cell runs (or run suffixes)
-    whose anchors x span stay below the read's best f, and the PAF of every
-    read equals the oracle's (assert_run_pruning; _production_vs_oracle)."""
-    with knobs(dev, sort_small=1, seg_small=seg_small, sort_lds_kb=lds_kb, run_prune=1):
-        pruned = 0
-        for world, mids in ((small_world, (None,)), (dense_world, (20, 5000))):
-            ref, reads, rnames, rseqs = world
-            qs = list(rseqs)
-            if world is dense_world:
-                qs += [rseqs[0] * 3, rseqs[8] + rseqs[16]]
-            oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
-            idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
-            for mid in mids:
-                mid = mid if mid is not None else max(idx.calc_mid_occ(2e-4), 10)
-                dev.upload_index(idx, mid)
-                dev.set_debug(False)
-                dev.set_reads(qs)
-                dev.map(M.map_opts())
-                for r, q in enumerate(qs):
-                    want, _ = oi.anchors(q, 10, 15, mid)
-                    if len(want) > 1:
-                        want = want[_singleton_keep(want)]
-                    got = dev.debug_anchors(r)
-                    pruned += len(want) - len(got)
-                    assert_run_pruning(got, want, f"{seg_small} mid {mid} read {r}")
-        assert pruned > 0
-        _production_vs_oracle(dev, small_world, dense_world, tag="run pruning")
     dev.set_debug(True)
 
 
