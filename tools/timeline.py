@@ -63,6 +63,24 @@ def main():
     print(f"{'kernel':32s} {'attrib_ms':>10s} {'frac':>6s} {'sum_dur_ms':>10s} {'calls':>6s}")
     for n, a in sorted(att.items(), key=lambda x: -x[1]):
         print(f"{n:32s} {a / 1e6:10.2f} {a / win:6.3f} {dur[n] / 1e6:10.2f} {cnt[n]:6d}")
+    # busy fraction per tenth of the window: the warm-up, the ramp at the start of
+    # the timed region and the isolated runs after it show as dips; the steady
+    # state of the timed region is the plateau
+    marks = sorted([(s, 1) for s, e, n in rows] + [(e, -1) for s, e, n in rows])
+    edges = [t0 + (win * k) // 10 for k in range(11)]
+    sl = [0] * 10
+    live, prev = 0, t0
+    for t, d in marks + [(t1, 0)]:
+        if live > 0:
+            a = prev
+            while a < t:
+                k = min(9, (a - t0) * 10 // win)
+                b = min(t, edges[k + 1])
+                sl[k] += b - a
+                a = b if b > a else t
+        prev = t
+        live += d
+    print("busy per tenth of the window: " + " ".join(f"{x / (win / 10):.2f}" for x in sl))
 
 
 if __name__ == "__main__":
