@@ -121,16 +121,40 @@ def rank_read_seed(read_seed: int, rank: int) -> int:
 
 
 def reduce_step_time(dist, elapsed: float, n_bases: int, world: int, device):
-    """Max-over-ranks wall time and all ranks' bases (one all-reduce each,
-    outside the timed region)."""
+    """Max-over-ranks wall time, all ranks' bases and every rank's own time (an
+    all-reduce each and one all-gather, outside the timed region): the per-rank
+    times make a short multi-GPU line diagnosable (which rank, how uneven)."""
     if world <= 1:
-        return elapsed, float(n_bases)
+        return elapsed, float(n_bases), [elapsed]
     import torch
     tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     bt = torch.tensor([float(n_bases)], dtype=torch.float64, device=device)
     dist.all_reduce(bt, op=dist.ReduceOp.SUM)
-    return float(tt.item()), float(bt.item())
+    every = [None] * world
+    dist.all_gather_object(every, float(elapsed))
+    return float(tt.item()), float(bt.item()), [float(x) for x in every]
+
+
+def rank_times(every, steps: int) -> dict:
+    """Per-rank ms/step and the straggler ratio max/mean over ranks."""
+    ms = [x / max(steps, 1) * 1e3 for x in every]
+    mean = sum(ms) / max(len(ms), 1)
+    return {"per_rank_ms_per_step": [round(x, 3) for x in ms],
+            "rank_time_max_over_mean": round(max(ms) / mean, 4) if mean > 0 else None}
+
+
+def ref_size(nb: int) -> str:
+    """Reference size for config.workload: Gb above 0.1 Gb, else Mb (E. coli is 4.64 Mb, not 0.00 Gb)."""
+    return f"{nb / 1e9:.2f} Gb" if nb >= 1e8 else f"{nb / 1e6:.2f} Mb"
+
+
+def affinity_cpus() -> int:
+    """CPUs in this process's affinity set (the CPU baseline's all-cores leg uses every one)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def device_identity(gpu: int) -> str:
@@ -622,7 +646,7 @@ def main():
                     "ms_per_step": round(trs / args.resident_steps * 1e3, 3),
                     "note": "the same batch re-mapped from HBM: no host packing, no H2D (not the metric)"}
 
-    elapsed, all_bases = reduce_step_time(dist, elapsed, my_bases, world, red_dev)
+    elapsed, all_bases, every_rank = reduce_step_time(dist, elapsed, my_bases, world, red_dev)
     value = all_bases / elapsed / 1e9
     ms_per_step = elapsed / max(args.steps, 1) * 1e3
 
@@ -705,8 +729,8 @@ def main():
     dp_pairs_s = cnt["dp_pairs"] / elapsed if world == 1 else None
 
     # ---- oracle parity on a sample of every rank's timed batches; CPU baseline
-    # N=1: ~3,000 reads (the CPU baseline's ~8 s runs come out of it); N>1: 100 per rank
-    n_sample = 0 if args.no_parity else min(args.reads * args.steps, 3000 if world == 1 else 100)
+    # N=1: ~3,000 reads (the CPU baseline's ~8 s runs come out of it); N>1: 500 per rank
+    n_sample = 0 if args.no_parity else min(args.reads * args.steps, 3000 if world == 1 else 500)
     samp = sample_reads(args, batches, timed, n_sample, S)
     gathered = [samp] if world == 1 else [None] * world
     if world > 1:
@@ -730,7 +754,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic (hg38-shaped reference, seeded ONT-shaped reads, a distinct batch every step; SURVEY.md §8d)",
             "config": {
-                "workload": f"{args.preset}-shaped {lens.sum() / 1e9:.2f} Gb reference index in HBM + "
+                "workload": f"{args.preset}-shaped {ref_size(int(lens.sum()))} reference index in HBM + "
                             f"{args.reads}x{args.read_len // 1000} kb ONT reads per GPU per step, from host RAM "
                             f"(nt4 pack + H2D + map + PAF in the timed region)",
                 "reads_per_gpu_step": args.reads, "read_len": args.read_len, "ref_bases": int(lens.sum()),
@@ -741,6 +765,7 @@ def main():
                 "launch": ("self-spawned ranks" if os.environ.get("MM2G_BENCH_SPAWNED") else
                            ("torch.distributed.run" if world > 1 else "single process")),
                 "parallelism": f"reads sharded x{world} (index replicated), {S} streams per GPU, {P} units per batch",
+                **rank_times(every_rank, args.steps),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -862,11 +887,12 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
         n_s = int(min(len(seqs), max(n_cal, args.cpu_seconds / per_read)))
         bases = int(offs[n_s])
         t1 = [oi.align_buffer(rnames[:n_s], cat, offs[:n_s + 1], None, mid_occ=mid, threads=1)[2] for _ in range(3)]
-        tN = [oi.align_buffer(rnames[:n_s], cat, offs[:n_s + 1], None, mid_occ=mid, threads=thr)[2] for _ in range(3)]
+        ncpu = affinity_cpus()   # every CPU in the affinity set, not the OMP_NUM_THREADS share
+        tN = [oi.align_buffer(rnames[:n_s], cat, offs[:n_s + 1], None, mid_occ=mid, threads=ncpu)[2] for _ in range(3)]
         v1 = bases / statistics.median(t1) / 1e9
         vN = bases / statistics.median(tN) / 1e9
         pf = float(((rec[:n_s, 0] & 8) != 0).sum()) / max(n_s, 1)
-        log(f"cpu baseline: {n_s} reads, 1 thread {t1} s, {thr} threads {tN} s")
+        log(f"cpu baseline: {n_s} reads, 1 thread {t1} s, {ncpu} threads {tN} s")
         cpu = {"value": round(v1, 9), "unit": "Gbases/s", "cores": 1, "kind": "port",
                "sample": f"{n_s} reads ({bases / 1e6:.1f} Mb) spread over the timed steps' batches; oracle/ C++ restatement "
                          f"of mm2rs align (1 thread, as the reference), index build excluded, median of 3 runs; "
@@ -874,10 +900,10 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
                          f"(their chaining cost is paid, only the PAF line is missing)",
                "runs_s": [round(x, 3) for x in t1],
                "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-               "all_cores": {"value": round(vN, 9), "cores": thr, "runs_s": [round(x, 3) for x in tN],
-                             "note": f"{thr} threads: the process's CPU affinity / OMP_NUM_THREADS share "
-                                     f"({len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else '?'} "
-                                     f"CPUs in the affinity set of {os.cpu_count()} on the host)"}}
+               "all_cores": {"value": round(vN, 9), "cores": ncpu, "runs_s": [round(x, 3) for x in tN],
+                             "note": f"{ncpu} threads, one per CPU in the process's affinity set ({os.cpu_count()} CPUs "
+                                     f"on the host; OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')} is not "
+                                     f"used for this leg); the same sample as the 1-thread leg"}}
     oi.close()
     return cpu, parity
 

@@ -296,7 +296,11 @@ enum {
                                     lane (k_chain_med), longer ones a wave (k_chain_long); 0 = every segment
                                     over 8 anchors to a wave [0]                                                 */
     MM2G_KNOB_MED_PAIRS_RESCUE = 24, /* the same for the rescue pass [0]                                          */
-    MM2G_KNOB_COUNT = 25
+    MM2G_KNOB_WS_FAIL = 25,      /* tests: the next this-many up-front anchor-workspace reservations fail as if
+                                    HBM were full, forcing the exact-size fallback; 0 = off [0]              */
+    MM2G_KNOB_SORT_LB = 26,      /* the sort computes the pass-0 DP lower bound and candidate segments (k_chain_lb
+                                    skips those reads, k_chain_seg runs only the candidates) [1]             */
+    MM2G_KNOB_COUNT = 27
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

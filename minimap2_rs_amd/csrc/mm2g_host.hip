@@ -97,6 +97,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SPEC_ROUNDS: return 3;
     case MM2G_KNOB_MED_PAIRS: return 0;
     case MM2G_KNOB_MED_PAIRS_RESCUE: return 0;
+    case MM2G_KNOB_SORT_LB: return 1;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -126,7 +127,7 @@ struct mm2g_ctx {
     DevBuf tab_off, tab_key, tab_cnt;
     DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
     DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist, ncand;
     DevBuf dstat;                          // batch status block (BS_* word, workspace needs, counters)
     DevBuf chain_rdoff;                    // mm2g_chain_batch: prefix sums of the caller's qlen
     uint64_t cap_tab = 0, cap_A = 0;       // filter-table entries / anchors the workspaces hold
@@ -135,6 +136,7 @@ struct mm2g_ctx {
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
     bool mapped = false, collected = false, stop_after_sort = false, dv_separate = false;
     bool redo = false;                     // inside wait_batch's re-map (MM2G_KNOB_WS_MIN applies to first maps only)
+    bool ws_exact = false;                 // anchor workspace sized to the batches' exact counts (HBM was short)
     uint64_t n_anchors = 0;
     KeyLayout kl{};
     mm2g_map_opts last_opts{};
@@ -495,7 +497,7 @@ static int upload_flat(mm2g_ctx* c, const HostIndex& H, const FlatIndex& F, int3
         run += ((uint64_t)H.max_len >> CELL_SHIFT) + 3;
         goff[2 * H.n_seq + 1] = (uint32_t)std::min<uint64_t>(run, 0xffffffffu);
         // two bitmaps must fit the LDS budget of k_sort_read next to its static arrays
-        c->dix->cells = (run <= (uint64_t)320 * 1024) ? (uint32_t)run : 0u;
+        c->dix->cells = (run <= (uint64_t)MAX_CELLS) ? (uint32_t)run : 0u;
         uint32_t* dg;
         ENSURE(c->dix->goff, uint32_t, goff.size(), dg);
         HIPCHK(hipMemcpyAsync(dg, goff.data(), goff.size() * 4, hipMemcpyHostToDevice, c->stream));
@@ -775,10 +777,31 @@ static void build_lut(mm2g_ctx* c, float gap, int n) {
     c->lut_dirty = true;
 }
 
+// The pen LUT on the device (n entries, whole 16-B words for load_lut): it
+// stays resident and is copied only when it changes.
+static int upload_lut(mm2g_ctx* c, float gap, int n, int16_t** out) {
+    build_lut(c, gap, n);
+    int16_t* lut;
+    ENSURE(c->lut, int16_t, (c->h_lut.size() + 7) & ~(size_t)7, lut);
+    if (c->lut_dirty || c->lut_dev != c->lut.p) {
+        HIPCHK(hipMemcpyAsync(lut, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->lut_dirty = false; c->lut_dev = c->lut.p;
+    }
+    *out = lut;
+    return 0;
+}
+
 // Argument checks of the Align flow (main.rs:189-230) shared by map and the stage entry points.
 static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_t& mdx1) {
     if (!(o->w > 0 && o->w < 256 && o->k > 0 && o->k <= 28)) return set_err(MM2G_E_ARG, "invalid w/k (0 < w < 256, 0 < k <= 28)");
-    if (o->min_cnt < 2) return set_err(MM2G_E_UNSUP, "-n < 2 is outside the supported parity envelope (DESIGN.md Q4)");
+    // -n <= 1: the backtrack (lchain.rs:92-160) breaks out of mg_chain_bk_end after one step (it has just set
+    // t[i] = 2), so every chain it yields is one anchor with score f[i] - f[pprev[i]] <= span (or f[i] = span);
+    // with -m above the span none passes and the fallback path is exactly -n >= 2's (DESIGN.md "-n <= 1").
+    // Otherwise the output hangs on Rust's sort_unstable tie order (z by f, merge by qs).
+    if (o->min_cnt < 2 && o->min_chain_score <= o->k)
+        return set_err(MM2G_E_UNSUP, "-n %d with -m %d <= k %d: the output depends on Rust's sort_unstable tie order (DESIGN.md \"-n <= 1\")",
+                       o->min_cnt, o->min_chain_score, o->k);
     if (o->bw < 0 || o->bw_long < 0) return set_err(MM2G_E_ARG, "negative bandwidth");
     mdx0 = std::max(o->max_gap, o->bw); mdx1 = std::max(o->max_gap, o->bw_long);
     if (std::max(o->bw, o->bw_long) + 1 > 60000) return set_err(MM2G_E_UNSUP, "bandwidth > 59999 not supported");
@@ -795,18 +818,12 @@ static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_
 static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const ChainKParams& P0, float gap, int npass, int32_t mdx1,
                      int32_t mdy1, int32_t bw_long, uint64_t A_cap, const uint64_t* a_off, const uint32_t* a_cnt, uint64_t* keys,
                      uint64_t* ktmp, const uint32_t* cnt2, const uint64_t* smax, ReadOut* out, const uint32_t* abort, bool full,
-                     unsigned long long* stat = nullptr) {
+                     unsigned long long* stat = nullptr, const uint32_t* ncand = nullptr, int32_t* sort_fmin = nullptr) {
     int32_t *fb, *pb;
     ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
-    build_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1);
     int16_t* lut; uint32_t* work;
-    ENSURE(c->lut, int16_t, (c->h_lut.size() + 7) & ~(size_t)7, lut);   // whole 16-B words (load_lut)
+    if (int e = upload_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1, &lut)) return e;
     ENSURE(c->work, uint32_t, 4, work);
-    if (c->lut_dirty || c->lut_dev != c->lut.p) {   // the pen LUT stays resident; copied only when it changes
-        HIPCHK(hipMemcpyAsync(lut, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        c->lut_dirty = false; c->lut_dev = c->lut.p;
-    }
     HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));
     uint32_t* order;
     ENSURE(c->order, uint32_t, n, order);
@@ -829,8 +846,13 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                  lseg, lseg_n, lcap, lseg_order, rbest, cnt2, smax, mseg, lseg_n + 2, lseg_n + 3, mcap2, nullptr, 0u,
                  lazy ? 1u : 0u, nullptr, 0u};
     ca.abort = abort;
+    ca.full_dp = full ? 1u : 0u;   // not "no fmin": with pruning off, production still follows the med_pairs knobs
+    ca.ncand = ncand;              // pass 0: the sort's candidate segments / LB (null: every read streams)
     int32_t* fmin_buf = nullptr;
-    if (!full && K[MM2G_KNOB_PRUNE]) ENSURE(c->fmin, int32_t, n, fmin_buf);
+    if (!full && K[MM2G_KNOB_PRUNE]) {
+        if (sort_fmin) fmin_buf = sort_fmin;   // initialised (and set for its LB reads) by the sort
+        else ENSURE(c->fmin, int32_t, n, fmin_buf);
+    }
     uint32_t* item_off;
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
@@ -866,7 +888,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         // mode; the rescue pass runs on few reads, where it costs more than it saves)
         ca.fmin = pass == 0 ? fmin_buf : nullptr;
         if (ca.fmin) {
-            HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
+            if (!sort_fmin) HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
             ProfScope ps(c, "chain_lb");
             LCHK(launch_chain_stage(5, ca, 2048, c->stream));
         }
@@ -949,8 +971,15 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
 // batches.  The first estimate is 3 anchors per base (C3 has 2): about 10 GB
 // per context for a 100 Mb batch.  When HBM cannot hold that, the batch's exact
 // anchor count (the scan's total; one synchronisation) is used instead, so a
-// batch whose anchors fit is never refused for the estimate.
+// batch whose anchors fit is never refused for the estimate.  The
+// fallback first frees all five buffers (a partial grab of the estimate must
+// not keep HBM from the exact one), clears the failed hipMalloc's error, and
+// leaves the context in exact-size mode: later batches keep the exact
+// capacity (grown by wait_batch's re-map when a batch needs more) instead of
+// re-inflating to the estimate and paying hipFree + a failed hipMalloc + a
+// stream synchronisation every batch.
 static int reserve_anchor_ws(mm2g_ctx* c, const unsigned long long* st, uint64_t& A_cap) {
+    DevBuf* bufs[5] = {&c->keys, &c->keys_tmp, &c->fbuf, &c->ppbuf, &c->tmark};
     auto grab = [&](uint64_t n) -> int {
         uint64_t* p64; int32_t* p32;
         if (int e = ensure<uint64_t>(c->keys, n, &p64)) return e;
@@ -960,12 +989,27 @@ static int reserve_anchor_ws(mm2g_ctx* c, const unsigned long long* st, uint64_t
         if (int e = ensure<int32_t>(c->tmark, n, &p32)) return e;
         return 0;
     };
-    if (grab(A_cap) == 0) return 0;
+    if (c->knob[MM2G_KNOB_WS_FAIL] > 0) {   // tests: a partial grab (keys at the estimate), then HBM "full"
+        --c->knob[MM2G_KNOB_WS_FAIL];
+        uint64_t* p64;
+        if (int e = ensure<uint64_t>(c->keys, A_cap, &p64)) return e;
+    } else if (grab(A_cap) == 0) {
+        return 0;
+    }
+    (void)hipGetLastError();                  // the failed hipMalloc must not surface as a launch error
     unsigned long long tot = 0;
     HIPCHK(hipMemcpyAsync(&tot, st + 2, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    c->cap_A = A_cap = std::max<uint64_t>((uint64_t)tot, 1);
-    return grab(A_cap);
+    HIPCHK(hipStreamSynchronize(c->stream));  // also: nothing queued still uses the buffers freed below
+    const uint64_t need = std::max<uint64_t>((uint64_t)tot, 1);
+    for (DevBuf* b : bufs) if (b->cap < need * (b == &c->keys || b == &c->keys_tmp ? 8 : 4)) {
+        for (DevBuf* d : bufs) { if (d->p) (void)hipFree(d->p); d->p = nullptr; d->cap = 0; }
+        break;
+    }
+    c->ws_exact = true;
+    c->cap_A = A_cap = need;
+    const int e = grab(A_cap);
+    if (e) (void)hipGetLastError();
+    return e;
 }
 
 // Queue the whole path for the resident batch on the context stream (no host
@@ -1059,7 +1103,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         ProfScope ps(c, "seed_count");
         LCHK(launch_seed_count(sa, grid_for(n), c->stream));
     }
-    c->cap_A = std::max<uint64_t>(c->cap_A, 3 * c->total_bases + 65536);
+    if (!c->ws_exact) c->cap_A = std::max<uint64_t>(c->cap_A, 3 * c->total_bases + 65536);   // exact-size mode: see reserve_anchor_ws
     if (c->knob[MM2G_KNOB_WS_MIN] > 0 && !c->redo) c->cap_A = (uint64_t)c->knob[MM2G_KNOB_WS_MIN];   // tests: force the re-map
     uint64_t A_cap = c->cap_A;
     {
@@ -1089,6 +1133,26 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     ENSURE(c->rlist, uint32_t, n + 2, rlist);
     ENSURE(c->smax, uint64_t, n, smax);
     const bool filt = !c->debug && !stop_after_sort && K[MM2G_KNOB_FILTER] && std::max(mdx0, mdx1) <= (1 << CELL_SHIFT);
+    const int64_t stop_at = K[MM2G_KNOB_STOP_AT];   // measurement only: later stages skipped, results invalid
+    // pass-0 chain parameters (main.rs:201-214): the sort's LB pass uses them too
+    ChainKParams P{};
+    P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
+    P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
+    const float gap = 0.01f * 0.8f * (float)o->k;
+    const int npass = stop_at == 3 ? 1 : 2;
+    const bool chain = !stop_after_sort && stop_at != 1 && stop_at != 2;
+    uint32_t* ncand;
+    ENSURE(c->ncand, uint32_t, n, ncand);
+    int32_t* fmin_buf = nullptr;
+    const int16_t* lut_sort = nullptr;
+    if (chain && !c->debug && K[MM2G_KNOB_PRUNE]) {
+        ENSURE(c->fmin, int32_t, n, fmin_buf);
+        if (filt && K[MM2G_KNOB_SORT_LB] && P.lut_n <= SORT_LB_LUT) {
+            int16_t* l;
+            if (int e = upload_lut(c, gap, std::max(o->bw, npass > 1 ? o->bw_long : 0) + 1, &l)) return e;
+            lut_sort = l;
+        }
+    }
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
                 filt ? c->dix->cells : 0u, cnt2, smax, (uint32_t)std::min<int64_t>(K[MM2G_KNOB_SORT_SMALL], 4096), nullptr, 0u,
                 (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_SEG_SMALL], SEG_THREAD)), nullptr};
@@ -1097,9 +1161,9 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.rlist = rlist; so.rcount = rlist + n; so.rwork = rlist + n + 1;
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
+    so.ncand = ncand; so.fmin = fmin_buf; so.lut = lut_sort; so.P = P; so.lb_mode = (uint32_t)K[MM2G_KNOB_SORT_LB];
     uint64_t* sprof = nullptr;
     if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 128)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 128, c->stream)); so.prof = sprof; }
-    const int64_t stop_at = K[MM2G_KNOB_STOP_AT];   // measurement only: later stages skipped, results invalid
     if (stop_at != 1) {
     {
         ProfScope ps(c, "sort_small");
@@ -1118,13 +1182,10 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     std::swap(c->keys.p, c->keys_tmp.p); std::swap(c->keys.cap, c->keys_tmp.cap);
     std::swap(keys, ktmp);
     }
-    if (!stop_after_sort && stop_at != 1 && stop_at != 2) {
+    if (chain) {
         // 5. chain DP + fallback + rescue
-        ChainKParams P{};
-        P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
-        P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
-        if (int e = run_chain(c, n, c->d_rd_off, P, 0.01f * 0.8f * (float)o->k, stop_at == 3 ? 1 : 2, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
-                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug, st))
+        if (int e = run_chain(c, n, c->d_rd_off, P, gap, npass, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
+                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug, st, ncand, fmin_buf))
             return e;
         // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
         const bool sep = (H.w != o->w || H.k != o->k);
@@ -1378,7 +1439,6 @@ int mm2g_chain_batch(mm2g_ctx* c, const mm2g_chain_params* p, uint32_t n, const 
     const uint64_t A = a_off[n] - a_off[0];
     if (A && !xy) return set_err(MM2G_E_ARG, "null anchors");
     if (p->chn_pen_skip != 0.0f) return set_err(MM2G_E_UNSUP, "chn_pen_skip != 0 (the reference fixes it at 0, main.rs:116)");
-    if (p->min_cnt < 2) return set_err(MM2G_E_UNSUP, "min_cnt < 2 is outside the supported parity envelope (DESIGN.md Q4)");
     if (p->bw < 0 || p->bw_long < 0 || p->max_chain_iter < 1 || p->max_chain_skip < 0) return set_err(MM2G_E_ARG, "invalid chain parameters");
     if (std::max(p->bw, p->bw_long) + 1 > 60000) return set_err(MM2G_E_UNSUP, "bandwidth > 59999 not supported");
     HIPCHK(hipSetDevice(c->device));
@@ -1402,6 +1462,9 @@ int mm2g_chain_batch(mm2g_ctx* c, const mm2g_chain_params* p, uint32_t n, const 
         else if (sp != span) return set_err(MM2G_E_UNSUP, "anchors of different spans (the device DP keeps one span)");
     }
     if (span < 0) span = 15;
+    if (p->min_cnt < 2 && A && p->min_chain_score <= span)   // see check_opts: one-anchor backtrack chains can pass
+        return set_err(MM2G_E_UNSUP, "min_cnt %d with min_chain_score %d <= span %lld: Rust sort_unstable tie order (DESIGN.md \"-n <= 1\")",
+                       p->min_cnt, p->min_chain_score, (long long)span);
     KeyLayout kl;
     kl.n_seq = (uint32_t)max_rid + 1;
     kl.qb = std::max<uint32_t>(1, bit_width(max_q));

@@ -147,6 +147,7 @@ constexpr int SEED_PARTS = 4;
 constexpr int32_t SEG_CHUNK = 4096;     // anchors per work item of the streaming chain kernels
 constexpr uint32_t SEG_THREAD = 1024;   // cell segments up to this length: one thread per anchor (default seg_small)
 constexpr int CELL_SHIFT = 15;   // 32 kb reference cells (>= every max_dist_x the filter is used with)
+constexpr uint32_t MAX_CELLS = 320 * 1024;   // more cells: singleton filter off (the sorts' two LDS bitmaps must fit)
 struct SortArgs {
     uint32_t n;
     const uint64_t* a_off;
@@ -167,7 +168,20 @@ struct SortArgs {
     uint32_t* rcount = nullptr;
     const uint32_t* order = nullptr;   // k_sort_read: block b sorts read order[b] (heaviest first); null = b
     uint32_t* rwork = nullptr;         // k_sort_big: next list entry to take (zeroed by k_sort_small)
+    // Pass-0 DP lower bound and candidate segments (k_sort_read, DESIGN.md
+    // "Chain DP from the sort"): per read the LB of k_chain_lb over the whole
+    // sorted read (fmin) and the segments that can hold the best f (len * span
+    // >= fmin), written as u16 start | u16 length << 16 over the read's own
+    // (dead) unsorted-key region; ncand: their count, or NC_STREAM / NC_STREAM_LB
+    uint32_t* ncand = nullptr;         // per read (k_sort_small initialises every read to NC_STREAM)
+    int32_t* fmin = nullptr;           // null: no LB / candidates (debug mode, pruning off)
+    uint32_t lb_mode = 1;              // EXPERIMENT: 2 = only drain stores + barrier, 3 = LB without candidates
+    const int16_t* lut = nullptr;      // comput_sc pen LUT of pass 0 (lut_n entries)
+    ChainKParams P{};                  // pass-0 chain parameters (max_dist_x/y, bw, span, lut_n)
 };
+constexpr uint32_t NC_STREAM = 0xffffffffu;      // no LB from the sort: k_chain_lb + streaming k_chain_seg
+constexpr uint32_t NC_STREAM_LB = 0xfffffffeu;   // fmin from the sort (k_chain_lb skips the read), streaming k_chain_seg
+constexpr int SORT_LB_LUT = 8192;                // the sort's LB pass keeps the pen LUT in LDS up to this many entries
 struct ChainArgs {
     uint32_t n;
     const uint64_t* rd_off;
@@ -206,6 +220,8 @@ struct ChainArgs {
     void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
     uint32_t spec_rounds = 3; // k_chain_long: speculative rounds per 64-anchor block (MM2G_KNOB_SPEC_ROUNDS)
     int32_t est_lane = 0;    // k_chain_seg (production): estimated DP pairs up to which a segment takes one lane
+    uint32_t full_dp = 0;    // debug mode (exact f/pprev everywhere): pass 0 uses EST_LANE instead of est_lane
+    const uint32_t* ncand = nullptr;   // pass 0: per read NC_STREAM, NC_STREAM_LB or the sort's candidate count (SortArgs)
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
     const uint32_t* abort = nullptr;
     unsigned long long* gprof = nullptr;   // MM2G_LSEG_PROF: k_chain_giant phase sums (16 counters)

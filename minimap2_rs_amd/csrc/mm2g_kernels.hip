@@ -865,6 +865,10 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     __shared__ uint64_t s[SORT_SMALL];
     const uint32_t r = blockIdx.x;
     if (r >= a.n) return;
+    if (threadIdx.x == 0) {   // k_sort_read overwrites both for the reads whose LB pass it runs
+        if (a.ncand) a.ncand[r] = NC_STREAM;
+        if (a.fmin) a.fmin[r] = 0;
+    }
     const uint64_t base = a.a_off[r];
     const uint32_t A = (uint32_t)(a.a_off[r + 1] - base);
     if (A > a.small_max) return;
@@ -1064,17 +1068,18 @@ DEVI void block_pass_u(const uint64_t* src, uint32_t n, F fn) {
 // dependent 2-byte load steps per thread at 256 threads (chain_seg rescue
 // 0.137 -> 0.115 ms per 10 k reads, 1 stream).  Both sides hold whole 16-B
 // words (LDS: lut_lds; HBM: the LUT buffer is allocated in 8-entry units).
+// (No array and no conditional assignment: a conditionally assigned uint4[4]
+// was put in scratch memory, and every load then made a serial HBM round trip
+// through it, ~10 us at each block start of every chain kernel.)
 DEVI void load_lut(int16_t* lut, const int16_t* g, int n) {
     const int nv = (n * 2 + 15) >> 4;
     const uint4* src = (const uint4*)g;
     uint4* dst = (uint4*)lut;
     const int nt = (int)blockDim.x;
     for (int i0 = (int)threadIdx.x; i0 < nv; i0 += 4 * nt) {
-        uint4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { const int i = i0 + u * nt; if (i < nv) v[u] = src[i]; }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { const int i = i0 + u * nt; if (i < nv) dst[i] = v[u]; }
+        const int i1 = i0 + nt < nv ? i0 + nt : i0, i2 = i0 + 2 * nt < nv ? i0 + 2 * nt : i0, i3 = i0 + 3 * nt < nv ? i0 + 3 * nt : i0;
+        const uint4 v0 = src[i0], v1 = src[i1], v2 = src[i2], v3 = src[i3];
+        dst[i3] = v3; dst[i2] = v2; dst[i1] = v1; dst[i0] = v0;   // clamped slots rewrite v0's word last with v0
     }
 }
 
@@ -1217,6 +1222,191 @@ DEVI void radix_range(uint64_t* src, uint64_t* dst, uint64_t* out, uint32_t A, u
     __syncthreads();
     if (src != out) block_pass8(src, A, [&](uint32_t i, uint64_t x) { out[i] = x; });
     __syncthreads();
+}
+
+// ---- DPP helpers (wave scans) of the sort's LB pass and the chain kernels
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+DEVI int32_t dpp(int32_t old, int32_t src) { return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, BANK_MASK, false); }
+// inclusive max-scan over the wave (row_shr 1/2/4/8, row_bcast 15/31)
+DEVI int32_t scan_max(int32_t v) {
+    v = max(v, dpp<0x111>(INT_MIN, v)); v = max(v, dpp<0x112>(INT_MIN, v));
+    v = max(v, dpp<0x114>(INT_MIN, v)); v = max(v, dpp<0x118>(INT_MIN, v));
+    v = max(v, dpp<0x142, 0xa>(INT_MIN, v)); v = max(v, dpp<0x143, 0xc>(INT_MIN, v));
+    return v;
+}
+// OR over the wave (row_shr 1/2/4/8 + row_bcast 15/31 leave the total in lane 63)
+DEVI uint32_t wave_or32(uint32_t v) {
+    int32_t x = (int32_t)v;
+    x |= dpp<0x111>(0, x); x |= dpp<0x112>(0, x); x |= dpp<0x114>(0, x); x |= dpp<0x118>(0, x);
+    x |= dpp<0x142, 0xa>(0, x); x |= dpp<0x143, 0xc>(0, x);
+    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
+// lane l <- lane l-1, lane 0 <- old0 (wave_shr:1)
+DEVI int32_t shr1_dpp(int32_t v, int32_t old0) { return dpp<0x138>(old0, v); }
+// composition scan of x -> max(x + a, b) in lane order (earlier applied first)
+DEVI void scan_nskip(int32_t& a, int32_t& b) {
+    constexpr int32_t NEG = -(1 << 29);
+#define NS_STEP(CTRL, RM)                                                   \
+    {                                                                       \
+        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
+        b = max(ob + a, b); a = oa + a;                                     \
+    }
+    NS_STEP(0x111, 0xf) NS_STEP(0x112, 0xf) NS_STEP(0x114, 0xf) NS_STEP(0x118, 0xf)
+    NS_STEP(0x142, 0xa) NS_STEP(0x143, 0xc)
+#undef NS_STEP
+}
+
+// the same composition scan with the additive part clamped at NEG (a chain of
+// "no predecessor" steps must not overflow)
+DEVI void scan_lb(int32_t& a, int32_t& b) {
+    constexpr int32_t NEG = -(1 << 29);
+#define LB_STEP(CTRL, RM)                                                   \
+    {                                                                       \
+        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
+        b = max(ob + a, b); a = max(oa + a, NEG);                           \
+    }
+    LB_STEP(0x111, 0xf) LB_STEP(0x112, 0xf) LB_STEP(0x114, 0xf) LB_STEP(0x118, 0xf)
+    LB_STEP(0x142, 0xa) LB_STEP(0x143, 0xc)
+#undef LB_STEP
+}
+
+// ---- Chain DP from the sort: the pass-0 lower bound of the read's best f and
+// the segments that can hold it, from the read's sorted keys O[0, A) (complete).
+//   LB[i] = max(span, LB[i-1] + sc(i, i-1)) (k_chain_lb, lchain.rs:73-90: the
+//   first predecessor visited is i-1 and n_skip needs > max_skip visits), a
+//   composition of x -> max(x + a, b).  Each wave walks a contiguous range of
+//   64-key chunks (DPP scan per chunk, the range's composition carried in
+//   registers, U chunks' loads in flight) and keeps max_i A_i and max_i B_i of
+//   its prefix compositions (A_i, B_i); one exchange of the waves' (A, B, maxA,
+//   maxB) then gives max LB over the whole read = max_w max(x_w + maxA_w, maxB_w)
+//   with x_w the LB entering wave w.  k_chain_lb restarts at every 4096-anchor
+//   work item, so this bound is at least as large.
+//   Segments run from an isolated anchor (lchain.rs:75: i == 0, another group,
+//   or rpos_i > rpos_{i-1} + max_dist_x) to the next; one of len anchors has f
+//   <= len * span, so only those with len * span >= max LB can hold the read's
+//   best f or a tie of it (k_chain_seg's pruning rule, with the same bound).
+// The isolated anchors form a bitmap in LDS; each thread takes a run of its
+// words, finds the next start after its last one by a block suffix-min, and
+// the candidates go out as u16 start | u16 len << 16 to Kc (the read's own
+// unsorted-key region, dead now) in position order, with their count in
+// ncand[r] -- or NC_STREAM_LB when there are more than `budget` (k_chain_seg
+// then streams the read: many one-segment items would cost more).  fmin[r] =
+// max LB either way.  LDS: the pen LUT, then ceil(A / 64) u64 bitmap words;
+// w4: 5 NW words of static LDS.
+template <int NT>
+DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, const uint64_t* O, uint32_t* Kc, uint32_t A, unsigned char* lds,
+                        uint32_t* w4, uint32_t* s_sc) {
+    constexpr int NW = NT / 64;
+    constexpr int32_t NEG = -(1 << 29);
+    constexpr int U = 8;                           // chunks whose loads are in flight together
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const ChainKParams P = a.P;                   // a copy: a reference into the kernel argument forces it to scratch
+    int16_t* lut = (int16_t*)lds;
+    uint64_t* isob = (uint64_t*)(lds + (((P.lut_n * 2) + 15) & ~15));
+    load_lut(lut, a.lut, P.lut_n);
+    __syncthreads();
+    const uint32_t qb = a.qb, gsh = a.qb + a.rb;
+    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << a.rb) - 1;
+    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    const uint32_t nwd = (A + 63) >> 6;
+    const uint32_t wper = (nwd + NW - 1) / NW;
+    const uint32_t c_lo = min(nwd, (uint32_t)wv * wper), c_hi = min(nwd, c_lo + wper);
+    int32_t CA = 0, CB = NEG, MA = NEG, MB = NEG;   // the range's composition so far (identity), max prefix A / B
+    uint64_t prevk = 0;
+    if (c_lo < c_hi && c_lo > 0) prevk = uni64(O[c_lo * 64 - 1]);
+    for (uint32_t c0 = c_lo; c0 < c_hi; c0 += U) {
+        uint64_t kk[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = (c0 + (uint32_t)u) * 64 + (uint32_t)lane;
+            kk[u] = (c0 + (uint32_t)u < c_hi && i < A) ? O[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (c0 + (uint32_t)u < c_hi) {         // wave-uniform; no break: kk[] stays in registers
+            const uint32_t i = (c0 + (uint32_t)u) * 64 + (uint32_t)lane;
+            const bool valid = i < A;
+            const uint64_t ak = kk[u];
+            const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)(uint32_t)(prevk >> 32)) << 32) |
+                                (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)(uint32_t)prevk);
+            const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
+            const int32_t p = (int32_t)((ak >> qb) & rmask), pj = (int32_t)((pk >> qb) & rmask);
+            const int32_t q = (int32_t)(ak & qmask), qj = (int32_t)(pk & qmask);
+            const bool iso = valid && (i == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx));
+            int32_t sa = NEG;
+            if (valid && !iso) {   // comput_sc (lchain.rs:17-34) of (i, i-1); the LUT is (gap*dd + 0.5*log2(dd+1)) as i32
+                const int32_t dq = q - qj, dr = p - pj;
+                const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+                if (dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw) {
+                    const int32_t dg = dr < dq ? dr : dq;
+                    sa = (span < dg ? span : dg) - (int32_t)lut[dd];
+                }
+            }
+            int32_t sb = valid ? span : NEG;
+            scan_lb(sa, sb);
+            const int32_t Ai = max(CA + sa, NEG), Bi = max(CB + sa, sb);
+            if (valid) { MA = max(MA, Ai); MB = max(MB, Bi); }
+            const uint64_t im = ballot(iso);
+            if (lane == 0) isob[c0 + (uint32_t)u] = im;
+            CA = rdl(Ai, 63); CB = rdl(Bi, 63);
+            prevk = ((uint64_t)rdlu((uint32_t)(ak >> 32), 63) << 32) | rdlu((uint32_t)ak, 63);
+          }
+        }
+    }
+    MA = rdl(scan_max(MA), 63); MB = rdl(scan_max(MB), 63);
+    int32_t* wca = (int32_t*)w4;
+    if (lane == 0) { wca[wv] = CA; wca[NW + wv] = CB; wca[2 * NW + wv] = MA; wca[3 * NW + wv] = MB; }
+    __syncthreads();
+    int32_t x = NEG, best = span;
+#pragma unroll
+    for (int t = 0; t < NW; ++t) {
+        best = max(best, max(x + wca[2 * NW + t], wca[3 * NW + t]));
+        x = max(max(x + wca[t], NEG), wca[NW + t]);
+    }
+    // segment starts: thread t takes bitmap words [t * wpt, t * wpt + wpt)
+    const uint32_t wpt = (nwd + NT - 1) / NT;
+    const uint32_t wa0 = min(nwd, (uint32_t)tid * wpt), wb0 = min(nwd, wa0 + wpt);
+    uint32_t fpos = A;                             // my first start
+    for (uint32_t w = wa0; w < wb0 && fpos == A; ++w) { const uint64_t m = isob[w]; if (m) fpos = w * 64 + (uint32_t)__builtin_ctzll(m); }
+    // next start after my words: exclusive suffix min over the threads
+    uint32_t v = fpos;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { const uint32_t o = (uint32_t)__shfl_down((int)v, d, 64); if (lane + d < 64) v = min(v, o); }
+    uint32_t* wmin = w4 + 4 * NW;
+    if (lane == 0) wmin[wv] = v;
+    uint32_t after = (uint32_t)__shfl_down((int)v, 1, 64);
+    __syncthreads();
+    if (lane == 63) after = A;
+    for (int t = wv + 1; t < NW; ++t) after = min(after, wmin[t]);
+    const int64_t need = best;
+    // a candidate has >= Lmin anchors; from Lmin >= 64 on only the last start of
+    // a word can begin one (any other start's segment ends inside the word)
+    const bool top_only = (int64_t)63 * span < need;
+    auto visit = [&](auto&& fn) {
+        for (uint32_t w = wa0; w < wb0; ++w) {
+            const uint64_t m0 = isob[w];
+            if (!m0) continue;
+            uint64_t m = top_only ? (1ULL << (63 - __builtin_clzll(m0))) : m0;
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                const uint64_t rest = b == 63 ? 0ULL : (m0 >> (b + 1)) << (b + 1);
+                uint32_t e = after;
+                if (rest) e = w * 64 + (uint32_t)__builtin_ctzll(rest);
+                else for (uint32_t w2 = w + 1; w2 < wb0; ++w2) { const uint64_t m2 = isob[w2]; if (m2) { e = w2 * 64 + (uint32_t)__builtin_ctzll(m2); break; } }
+                const uint32_t sk = w * 64 + b;
+                if ((int64_t)(e - sk) * span >= need) fn(sk, e);
+            }
+        }
+    };
+    uint32_t mine = 0;
+    if (a.lb_mode != 3) visit([&](uint32_t, uint32_t) { ++mine; });
+    if (a.lb_mode == 3) mine = 0xffff;   // EXPERIMENT
+    uint32_t tot;
+    uint32_t o = block_excl_sum<NW>(mine, tot, s_sc);
+    const uint32_t budget = A / 32u + 8u;
+    if (tot <= budget && mine) visit([&](uint32_t sk, uint32_t e) { Kc[o++] = sk | ((e - sk) << 16); });
+    if (tid == 0) { a.fmin[r] = best; a.ncand[r] = tot <= budget ? tot : NC_STREAM_LB; }
 }
 
 // GL: the group offsets stay in HBM (2 n_seq + 2 > GOFF_LDS).  A template
@@ -1526,6 +1716,13 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 }
             }
             SORT_PH(6);
+            // pass-0 LB and candidate segments (k_chain_lb / k_chain_seg's scan, fused)
+            if (a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
+                __syncthreads();                   // O complete (rank phase, P4b) and visible to the block
+                if (a.lb_mode == 2) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); __syncthreads(); }
+                else sort_lb_cands<NT>(a, r, O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc);
+                SORT_PH(3);
+            }
             SORT_END(nbig, A);
             return;
         }
@@ -1661,6 +1858,9 @@ DEVI uint32_t block_incl_min(uint32_t v, uint32_t* sc) {
 // work counter (the list is roughly heaviest first: k_sort_read defers in its
 // heaviest-first order).
 constexpr uint32_t BIG_NB_MAX = 16384;
+// k_sort_big / k_sort_read keep both cell bitmaps (2 x MAX_CELLS bits) plus the
+// bucket counts in SORT_LDS; `LW - 2 * nw - 64` below is unsigned
+static_assert(SORT_LDS / 4 > 2 * (MAX_CELLS / 32) + 64 + 4096, "MAX_CELLS bitmaps must leave LDS for the bucket counts");
 template <bool GL>
 __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;
@@ -1950,51 +2150,6 @@ constexpr int RING_WORDS = 256;   // 8192-bit mark ring (max_iter <= 8000)
 constexpr int RK = 256;           // anchor ring entries per wave (power of two, >= 256)
 static_assert((RK & (RK - 1)) == 0 && RK >= 256, "anchor ring size");
 
-template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
-DEVI int32_t dpp(int32_t old, int32_t src) { return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, BANK_MASK, false); }
-// inclusive max-scan over the wave (row_shr 1/2/4/8, row_bcast 15/31)
-DEVI int32_t scan_max(int32_t v) {
-    v = max(v, dpp<0x111>(INT_MIN, v)); v = max(v, dpp<0x112>(INT_MIN, v));
-    v = max(v, dpp<0x114>(INT_MIN, v)); v = max(v, dpp<0x118>(INT_MIN, v));
-    v = max(v, dpp<0x142, 0xa>(INT_MIN, v)); v = max(v, dpp<0x143, 0xc>(INT_MIN, v));
-    return v;
-}
-// OR over the wave (row_shr 1/2/4/8 + row_bcast 15/31 leave the total in lane 63)
-DEVI uint32_t wave_or32(uint32_t v) {
-    int32_t x = (int32_t)v;
-    x |= dpp<0x111>(0, x); x |= dpp<0x112>(0, x); x |= dpp<0x114>(0, x); x |= dpp<0x118>(0, x);
-    x |= dpp<0x142, 0xa>(0, x); x |= dpp<0x143, 0xc>(0, x);
-    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
-}
-// lane l <- lane l-1, lane 0 <- old0 (wave_shr:1)
-DEVI int32_t shr1_dpp(int32_t v, int32_t old0) { return dpp<0x138>(old0, v); }
-// composition scan of x -> max(x + a, b) in lane order (earlier applied first)
-DEVI void scan_nskip(int32_t& a, int32_t& b) {
-    constexpr int32_t NEG = -(1 << 29);
-#define NS_STEP(CTRL, RM)                                                   \
-    {                                                                       \
-        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
-        b = max(ob + a, b); a = oa + a;                                     \
-    }
-    NS_STEP(0x111, 0xf) NS_STEP(0x112, 0xf) NS_STEP(0x114, 0xf) NS_STEP(0x118, 0xf)
-    NS_STEP(0x142, 0xa) NS_STEP(0x143, 0xc)
-#undef NS_STEP
-}
-
-// the same composition scan with the additive part clamped at NEG (a chain of
-// "no predecessor" steps must not overflow)
-DEVI void scan_lb(int32_t& a, int32_t& b) {
-    constexpr int32_t NEG = -(1 << 29);
-#define LB_STEP(CTRL, RM)                                                   \
-    {                                                                       \
-        const int32_t oa = dpp<CTRL, RM>(0, a), ob = dpp<CTRL, RM>(NEG, b); \
-        b = max(ob + a, b); a = max(oa + a, NEG);                           \
-    }
-    LB_STEP(0x111, 0xf) LB_STEP(0x112, 0xf) LB_STEP(0x114, 0xf) LB_STEP(0x118, 0xf)
-    LB_STEP(0x142, 0xa) LB_STEP(0x143, 0xc)
-#undef LB_STEP
-}
-
 constexpr uint32_t LSEG_DONE = 0xffffffffu;   // lseg[].w: handled by k_chain_giant
 constexpr int TINY = CHAIN_TINY;  // segments up to this many anchors: one lane, registers
 constexpr int MED = CHAIN_MED;    // up to this many: one lane, state machine over HBM; longer: whole wave
@@ -2092,7 +2247,9 @@ __global__ __launch_bounds__(1024) void k_seg_items(ChainArgs a) {
         if (t < a.n) {
             const uint32_t r = a.order[t];
             const bool on = a.P.pass == 0 || (a.out[r].flags & RF_RESCUED);
-            c = on ? (a.cnt2[r] + a.seg_chunk - 1) / a.seg_chunk : 0u;
+            const uint32_t nc = (a.P.pass == 0 && a.ncand) ? a.ncand[r] : NC_STREAM;
+            // the sort's candidate segments (one item each), else 4096-anchor chunks
+            c = !on ? 0u : nc < NC_STREAM_LB ? nc : (a.cnt2[r] + a.seg_chunk - 1) / a.seg_chunk;
         }
         uint32_t wt;
         const uint32_t ex = wave_excl_sum(c, wt);
@@ -2153,13 +2310,24 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     for (uint32_t it = blockIdx.x * DP_NW + wv; it < n_items; it += nwaves) {
         const uint32_t t = (uint32_t)uni((int32_t)item_owner(a.item_off, a.n, it));
         const uint32_t r = (uint32_t)uni((int32_t)a.order[t]);
-        const int32_t c0 = (int32_t)(it - (uint32_t)uni((int32_t)a.item_off[t])) * (int32_t)a.seg_chunk;
+        const uint32_t j = it - (uint32_t)uni((int32_t)a.item_off[t]);
         const uint64_t t_start = wall_clock64();
         if (t < (uint32_t)a.n_prio) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
         const uint64_t base = uni64(a.a_off[r]);
-        const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);      // anchors kept by the singleton filter
-        const int32_t c1 = min(A, c0 + (int32_t)a.seg_chunk);
+        const uint32_t nc = (a.ncand && P.pass == 0) ? (uint32_t)uni((int32_t)a.ncand[r]) : NC_STREAM;
+        int32_t c0, c1, A;
+        if (nc < NC_STREAM_LB) {
+            // one candidate segment [s, s + len) of the sort (sort_lb_cands), in the
+            // read's dead unsorted-key region (now a.chain's): streamed as if it
+            // were the whole read, so exactly it is routed
+            const uint32_t cv = (uint32_t)uni((int32_t)a.chain[2 * base + j]);
+            c0 = (int32_t)(cv & 0xffffu); A = c0 + (int32_t)(cv >> 16); c1 = A;
+        } else {
+            c0 = (int32_t)j * (int32_t)a.seg_chunk;
+            A = (int32_t)uni((int32_t)a.cnt2[r]);      // anchors kept by the singleton filter
+            c1 = min(A, c0 + (int32_t)a.seg_chunk);
+        }
         if (c0 >= A) continue;
 #ifdef MM2G_CHECKED
         if (base + (uint64_t)A > a.cap_keys) { if (lane == 0) CK(base + A, a.cap_keys); continue; }
@@ -2224,7 +2392,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
                 const int64_t bp = p1 - p0 > 0 ? (int64_t)(p1 - p0) : 1;
                 int64_t win = ((int64_t)len * maxdx + bp - 1) / bp;
                 win = win < len ? win : len;
-                med = (int64_t)len * win / 2 <= ((P.pass == 0 && !a.fmin) ? EST_LANE : (int64_t)a.est_lane);
+                med = (int64_t)len * win / 2 <= ((P.pass == 0 && a.full_dp) ? EST_LANE : (int64_t)a.est_lane);
             }
             const bool big = emit && len > TINY && !med;
             const uint64_t medM = ballot(med);
@@ -2350,6 +2518,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + wave_id(); it < n_items; it += nwaves) {
         const uint32_t t = (uint32_t)uni((int32_t)item_owner(a.item_off, a.n, it));
         const uint32_t r = (uint32_t)uni((int32_t)a.order[t]);
+        if (a.ncand && (uint32_t)uni((int32_t)a.ncand[r]) != NC_STREAM) continue;   // the sort set fmin[r] (a larger bound)
         const int32_t c0 = (int32_t)(it - (uint32_t)uni((int32_t)a.item_off[t])) * (int32_t)a.seg_chunk;
         const uint64_t base = uni64(a.a_off[r]);
         const int32_t A = min((int32_t)uni((int32_t)a.cnt2[r]), c0 + (int32_t)a.seg_chunk);
@@ -3807,7 +3976,9 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
         // persistent workgroups on a work counter: one per CU (the LDS allows no
         // more); most batches list no read, and every extra workgroup would wait
         // for a CU the other streams' kernels hold
-        const unsigned grid = std::min<uint32_t>(a.n, 256);
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const unsigned grid = std::min<uint32_t>(a.n, (uint32_t)std::max(ncu, 1));
         if (2u * b.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_big<true>, dim3(grid), dim3(1024), (size_t)SORT_LDS, st, b);
         else hipLaunchKernelGGL(k_sort_big<false>, dim3(grid), dim3(1024), (size_t)SORT_LDS, st, b);
     } else {

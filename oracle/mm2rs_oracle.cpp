@@ -514,6 +514,19 @@ struct DpResult { std::vector<std::vector<size_t>> chains; std::vector<int32_t> 
 
 static void sort_chains_stable(const std::vector<Anchor>& anchors, std::vector<std::vector<size_t>>& chains, std::vector<int32_t>& scores);
 
+// Tie order of Rust's sort_unstable_by_key (lchain.rs:97 z by f, :267 / :292
+// merge items by qs): unspecified by Rust and not restated here.  0: std::sort;
+// 1 / 2: stable, equal keys in ascending / descending input order -- the two
+// extremes, for measuring which outputs depend on it (orc_set_tie_order).
+static int g_tie_order = 0;
+template <typename T>
+static void sort_unstable_by_first(std::vector<std::pair<int32_t, T>>& v) {
+    auto lt = [](const std::pair<int32_t, T>& a, const std::pair<int32_t, T>& b) { return a.first < b.first; };
+    if (g_tie_order == 0) { std::sort(v.begin(), v.end(), lt); return; }
+    if (g_tie_order == 2) std::reverse(v.begin(), v.end());
+    std::stable_sort(v.begin(), v.end(), lt);
+}
+
 // lchain.rs:59-176
 static DpResult chain_dp_all(const std::vector<Anchor>& anchors, const ChainParams& p, ChainStats* stats) {
     DpResult R;
@@ -551,8 +564,9 @@ static DpResult chain_dp_all(const std::vector<Anchor>& anchors, const ChainPara
     std::vector<std::pair<int32_t, size_t>> z;
     for (size_t i = 0; i < n; ++i) if (f[i] > 0) z.push_back({f[i], i});
     if (z.empty()) return R;
-    // sort_unstable_by_key: tie order differs from Rust's ipnsort (only observable when min_cnt <= 1)
-    std::sort(z.begin(), z.end(), [](const std::pair<int32_t, size_t>& a, const std::pair<int32_t, size_t>& b) { return a.first < b.first; });
+    // sort_unstable_by_key: tie order unspecified (g_tie_order); observable only when a backtrack chain passes
+    // min_chain_score, i.e. min_cnt <= 1 and min_chain_score <= span (DESIGN.md "-n <= 1")
+    sort_unstable_by_first(z);
     std::fill(t.begin(), t.end(), 0);
     size_t n_v = 0, n_u = 0;
     for (size_t kk = z.size(); kk-- > 0;) {   // first pass
@@ -699,7 +713,7 @@ static void select_and_filter_chains(const std::vector<Anchor>& anchors, const s
 static std::vector<std::vector<size_t>> merge_adjacent_chains_with_gap(const std::vector<Anchor>& anchors, const std::vector<std::vector<size_t>>& chains, int32_t max_gap_q, int32_t max_gap_t) {   // lchain.rs:288-314
     std::vector<std::pair<int32_t, size_t>> items;
     for (size_t i = 0; i < chains.size(); ++i) { int32_t qs, qe; chain_qrange(anchors, chains[i], qs, qe); items.push_back({qs, i}); }
-    std::sort(items.begin(), items.end(), [](const std::pair<int32_t, size_t>& a, const std::pair<int32_t, size_t>& b) { return a.first < b.first; });
+    sort_unstable_by_first(items);   // ties: see g_tie_order
     std::vector<std::vector<size_t>> merged;
     for (auto& it : items) {
         const auto& ch = chains[it.second];
@@ -1104,6 +1118,7 @@ long long orc_align_fasta(void* idx, const char* reads_fa, const char* out_path,
 void orc_set_quiet(int q) { g_quiet = q != 0; }
 // paf.rs:178's binary_search as rustc 1.52-1.81 (1) or >= 1.82 (0, default) compiles it
 void orc_set_binary_search(int pre182) { g_binsearch_pre182 = pre182 != 0; }
+void orc_set_tie_order(int mode) { g_tie_order = mode; }
 // the two algorithms on a caller array (tests): returns found, *idx = Ok / Err index
 int orc_binary_search(const int32_t* v, uint64_t n, int32_t target, int pre182, uint64_t* idx) {
     std::vector<int32_t> a(v, v + n);

@@ -65,6 +65,7 @@ def lib() -> C.CDLL:
                                      C.POINTER(C.c_float), C.c_int, C.c_int, _P64, C.POINTER(C.c_double)]
         L.orc_set_quiet.argtypes = [C.c_int]
         L.orc_set_binary_search.argtypes = [C.c_int]
+        L.orc_set_tie_order.argtypes = [C.c_int]
         L.orc_binary_search.restype = C.c_int
         L.orc_binary_search.argtypes = [C.POINTER(C.c_int32), C.c_uint64, C.c_int32, C.c_int, _P64]
         L.orc_align_records.restype = C.c_longlong
@@ -240,6 +241,12 @@ def set_quiet(q: bool = True) -> None:
 def set_binary_search(pre182: bool) -> None:
     """paf.rs:178's `binary_search` as rustc 1.52-1.81 (True) or >= 1.82 (False, the default) compiles it."""
     lib().orc_set_binary_search(1 if pre182 else 0)
+
+
+def set_tie_order(mode: int) -> None:
+    """Tie order of the reference's two sort_unstable_by_key calls (lchain.rs:97, :292): 0 std::sort, 1 / 2
+    stable with equal keys in ascending / descending input order (the extremes, for exposure counts)."""
+    lib().orc_set_tie_order(int(mode))
 
 
 def binary_search(v, target: int, pre182: bool = False):

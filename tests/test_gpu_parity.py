@@ -257,6 +257,28 @@ def test_cli_align_gpu(small_world, tmp_path):
     assert g == c and g.count("\n") > 50
 
 
+def test_cli_align_min_cnt(small_world, dense_world, tmp_path):
+    """`mm2rs align -n 1` / `-n 0` / `-n -1` with -m above k (the default 40,
+    and 16): byte-identical to the oracle CLI with the same flags -- the
+    backtrack yields one-anchor chains scored <= k, so none passes and the
+    fallback path runs (DESIGN.md "-n <= 1").  `-n 1 -m 15` is refused."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mm2rs = os.path.join(root, "minimap2_rs_amd", "build", "mm2rs")
+    cpu = os.path.join(root, "oracle", "build", "mm2rs-cpu")
+    for wi, world in enumerate((small_world, dense_world)):
+        ref, reads, rnames, rseqs = world
+        mmi = str(tmp_path / f"ref{wi}.mmi")
+        subprocess.run([mm2rs, "index", ref, "-d", mmi], check=True, capture_output=True)
+        for flags in (["-n", "1"], ["-n", "0"], ["-n", "-1", "-m", "16"]):
+            g = subprocess.run([mm2rs, "align", mmi, reads] + flags, check=True, capture_output=True, text=True).stdout
+            c = subprocess.run([cpu, "align", ref, reads] + flags, check=True, capture_output=True, text=True).stdout
+            c3 = subprocess.run([cpu, "align", ref, reads], check=True, capture_output=True, text=True).stdout
+            assert g == c == c3 and g.count("\n") > 10, flags
+        bad = subprocess.run([mm2rs, "align", mmi, reads, "-n", "1", "-m", "15"], capture_output=True, text=True)
+        assert bad.returncode != 0 and "tie order" in bad.stderr
+
+
 @pytest.mark.parametrize("seg_small,lds_kb", [(1024, 0), (64, 0), (8, 0), (1, 0), (1024, 76), (8, 76)])
 def test_filtered_sort_parity(dev, small_world, dense_world, seg_small, lds_kb):
     """Production sort (cell buckets + per-segment ranking, singleton filter

@@ -71,6 +71,21 @@ def test_workspace_remap(dev, small_world, dense_world):
             _production_vs_oracle(dev, small_world, dense_world, tag=f"ws_min {ws}")
 
 
+def test_workspace_exact_fallback(small_world, dense_world):
+    """The up-front anchor reservation fails as if HBM were full
+    (MM2G_KNOB_WS_FAIL: keys grabbed at the estimate, then the failure): the
+    context frees all five anchor buffers, clears the hipMalloc error, takes
+    the batch's exact anchor count and stays in exact-size mode; later batches
+    (larger ones grow by the re-map) still equal the oracle."""
+    d = M.Device(0)
+    try:
+        with knobs(d, ws_fail=2):
+            _production_vs_oracle(d, small_world, dense_world, tag="ws_fail")
+        _production_vs_oracle(d, small_world, dense_world, tag="exact-size mode")
+    finally:
+        d.close()
+
+
 @pytest.mark.parametrize("max_gap,bw_long", [(5000, 40000), (40000, 20000)])
 def test_wide_gaps_vs_oracle(dev, small_world, dense_world, max_gap, bw_long):
     """max_dist_x beyond the sort's 32 kb cells (-g 40000, -r 500,40000): the
@@ -150,8 +165,13 @@ def test_chain_batch_rejects(dev):
         dev.chain_batch([b], [1000])
     with pytest.raises(Mm2gError):
         dev.chain_batch([a[::-1].copy()], [1000], M.chain_params(15, chn_pen_skip=0.5))
-    with pytest.raises(Mm2gError):
-        dev.chain_batch([a[::-1].copy()], [1000], M.chain_params(15, min_cnt=1))
+    with pytest.raises(Mm2gError):   # -n <= 1 with -m <= span: Rust sort_unstable tie order (DESIGN.md "-n <= 1")
+        dev.chain_batch([a[::-1].copy()], [1000], M.chain_params(15, min_cnt=1, min_chain_score=15))
+    # -n <= 1 with -m above the span: no backtrack chain can pass, the result is -n 3's
+    for mc in (1, 0):
+        r1 = dev.chain_batch([a[::-1].copy()], [1000], M.chain_params(15, min_cnt=mc))
+        r3 = dev.chain_batch([a[::-1].copy()], [1000], M.chain_params(15))
+        assert np.array_equal(r1[1][0], r3[1][0]) and bytes(r1[0][0]) == bytes(r3[0][0])
 
 
 def test_dv_binary_search_even_k(dev):

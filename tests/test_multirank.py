@@ -26,8 +26,8 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dist.barrier()
-        t, b = bench.reduce_step_time(dist, elapsed=1.0 + rank, n_bases=1000 * (rank + 1), world=world, device="cpu")
-        q.put((rank, t, b, bench.rank_read_seed(3, rank)))
+        t, b, every = bench.reduce_step_time(dist, elapsed=1.0 + rank, n_bases=1000 * (rank + 1), world=world, device="cpu")
+        q.put((rank, t, b, bench.rank_read_seed(3, rank), every, bench.rank_times(every, 10)))
     finally:
         dist.destroy_process_group()
 
@@ -46,10 +46,18 @@ def test_reduce_over_two_ranks():
     assert [g[1] for g in got] == [2.0, 2.0]              # max over ranks
     assert [g[2] for g in got] == [3000.0, 3000.0]        # whole-job bases
     assert got[0][3] != got[1][3]                         # each rank maps its own reads
+    assert [g[4] for g in got] == [[1.0, 2.0], [1.0, 2.0]]   # every rank's own time, in rank order
+    rt = got[0][5]                                        # config fields of the bench line
+    assert rt["per_rank_ms_per_step"] == [100.0, 200.0] and rt["rank_time_max_over_mean"] == round(200 / 150, 4)
 
 
 def test_single_rank_no_collective():
-    assert bench.reduce_step_time(None, 1.5, 42, 1, "cpu") == (1.5, 42.0)
+    assert bench.reduce_step_time(None, 1.5, 42, 1, "cpu") == (1.5, 42.0, [1.5])
+    assert bench.rank_times([1.5], 3) == {"per_rank_ms_per_step": [500.0], "rank_time_max_over_mean": 1.0}
+
+
+def test_workload_reference_size_units():
+    assert bench.ref_size(4_641_652) == "4.64 Mb" and bench.ref_size(3_088_269_832) == "3.09 Gb"
 
 
 @pytest.mark.parametrize("n,s", [(10000, 1), (10000, 3), (7, 3), (0, 2), (5, 8)])
