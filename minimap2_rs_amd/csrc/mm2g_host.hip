@@ -83,6 +83,8 @@ struct SketchBufs {
     bool exact = false;    // slots sized by the true counts (after an overflow)
     uint64_t cap = 0;      // minimizer slots allocated
 };
+// query sketch views (run_sketch): the view table, per-view slots, per-read view offsets
+struct ViewBufs { DevBuf read, len, pre, from, cnt, need, off, base, end, last, nvr, vo, x, y; };
 
 static int64_t knob_default(int k) {
     switch (k) {
@@ -98,6 +100,8 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_MED_PAIRS: return 0;
     case MM2G_KNOB_MED_PAIRS_RESCUE: return 0;
     case MM2G_KNOB_SORT_LB: return 1;
+    case MM2G_KNOB_SKETCH_VIEW: return 2560;
+    case MM2G_KNOB_MW_MIN: return 0;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -123,6 +127,8 @@ struct mm2g_ctx {
     DevBuf rd_dev;
     const uint64_t *d_rd_off = nullptr, *d_pk_off = nullptr, *d_amb_off = nullptr, *d_words = nullptr;
     SketchBufs sk1, sk2;                   // CLI (w, k) sketch; index (w, k) sketch for dv when they differ
+    ViewBufs vw;                           // query views of both sketches (one at a time on the stream)
+    bool views_off = false;                // a re-map after a minimizer-slot overflow: whole-read sketch
     DevBuf keep, mz_n, mz_poff;
     DevBuf tab_off, tab_key, tab_cnt;
     DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
@@ -731,6 +737,38 @@ static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf) {
     }
     SketchArgs a{nullptr, c->d_rd_off, n, w, k, base, end, x, y, cnt, ovf};
     a.pk_words = c->d_words; a.pk_off = c->d_pk_off; a.amb_off = c->d_amb_off; a.mz_need = need;
+    // query views (odd k only: the fixed warm-up is exact there; a re-run
+    // after a slot overflow has them off, so the exact per-read layout needs one pass)
+    const uint32_t V = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(c->knob[MM2G_KNOB_SKETCH_VIEW], 1 << 30));
+    if (V >= 64 && (k & 1) && !c->views_off && c->max_read_len > V && !c->knob[MM2G_KNOB_SKETCH_PROF] && !slot) {
+        const uint32_t W0 = (uint32_t)((2 * (w + k) + 64 + 7) & ~7);
+        const uint64_t nvmax = (uint64_t)n + c->total_bases / V + 1;
+        uint32_t *v_read, *v_len, *v_pre, *v_from, *v_cnt, *v_need, *nvr; uint64_t *v_off, *v_base, *v_end, *vo, *vx; uint8_t* v_last; uint32_t* vy;
+        ViewBufs& Vb = c->vw;
+        ENSURE(Vb.read, uint32_t, nvmax, v_read); ENSURE(Vb.len, uint32_t, nvmax, v_len); ENSURE(Vb.pre, uint32_t, nvmax, v_pre);
+        ENSURE(Vb.from, uint32_t, nvmax, v_from); ENSURE(Vb.cnt, uint32_t, nvmax, v_cnt); ENSURE(Vb.need, uint32_t, nvmax, v_need);
+        ENSURE(Vb.off, uint64_t, nvmax, v_off); ENSURE(Vb.base, uint64_t, nvmax, v_base); ENSURE(Vb.end, uint64_t, nvmax, v_end);
+        ENSURE(Vb.last, uint8_t, nvmax, v_last); ENSURE(Vb.nvr, uint32_t, n + 1, nvr); ENSURE(Vb.vo, uint64_t, n + 1, vo);
+        const uint64_t vcap = c->total_bases + 16 * nvmax + 16;
+        ENSURE(Vb.x, uint64_t, vcap, vx); ENSURE(Vb.y, uint32_t, vcap, vy);
+        {
+            ProfScope ps(c, "sketch_views");
+            HIPCHK(hipMemsetAsync(v_len, 0, nvmax * 4, c->stream));     // views past the real count: empty
+            LCHK(launch_view_count(n, c->d_rd_off, V, nvr, c->stream));
+            LCHK(launch_excl_scan(nvr, n, vo, 0, 0, k, 0, nullptr, 0, 0, c->stream));
+            LCHK(launch_view_fill(n, c->d_rd_off, V, W0, vo, v_read, v_off, v_len, v_pre, v_from, v_last, v_base, v_end, c->stream));
+        }
+        SketchArgs va = a;
+        va.n = (uint32_t)nvmax; va.out_base = v_base; va.out_end = v_end; va.mz_x = vx; va.mz_y = vy; va.mz_cnt = v_cnt; va.mz_need = v_need;
+        va.view_off = v_off; va.view_len = v_len; va.view_pre = v_pre; va.emit_from = v_from; va.view_last = v_last; va.view_read = v_read;
+        {
+            ProfScope ps(c, "sketch");
+            LCHK(launch_sketch(va, grid_for((uint32_t)nvmax), c->stream));
+        }
+        ProfScope ps(c, "sketch_views");
+        LCHK(launch_view_compact(n, vo, v_off, v_base, v_cnt, v_need, vx, vy, base, end, x, y, cnt, need, ovf, c->stream));
+        return 0;
+    }
     ProfScope ps(c, "sketch");
     uint64_t* skp = nullptr;
     if (c->knob[MM2G_KNOB_SKETCH_PROF]) { HIPCHK(hipMalloc(&skp, (size_t)n * 64)); HIPCHK(hipMemsetAsync(skp, 0, (size_t)n * 64, c->stream)); a.prof = skp; }
@@ -795,7 +833,7 @@ static int upload_lut(mm2g_ctx* c, float gap, int n, int16_t** out) {
 // Argument checks of the Align flow (main.rs:189-230) shared by map and the stage entry points.
 static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_t& mdx1) {
     if (!(o->w > 0 && o->w < 256 && o->k > 0 && o->k <= 28)) return set_err(MM2G_E_ARG, "invalid w/k (0 < w < 256, 0 < k <= 28)");
-    // -n <= 1: the backtrack (lchain.rs:92-160) breaks out of mg_chain_bk_end after one step (it has just set
+    // -n <= 1: the backtrack (lchain.rs:92-160) leaves mg_chain_bk_end after one step (:110,114: it has just set
     // t[i] = 2), so every chain it yields is one anchor with score f[i] - f[pprev[i]] <= span (or f[i] = span);
     // with -m above the span none passes and the fallback path is exactly -n >= 2's (DESIGN.md "-n <= 1").
     // Otherwise the output hangs on Rust's sort_unstable tie order (z by f, merge by qs).
@@ -824,7 +862,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     int16_t* lut; uint32_t* work;
     if (int e = upload_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1, &lut)) return e;
     ENSURE(c->work, uint32_t, 4, work);
-    HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));
+    HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));   // [0..1] k_chain_giant hand-out per pass, [2..3] k_chain_long_mw
     uint32_t* order;
     ENSURE(c->order, uint32_t, n, order);
     int32_t* tmark;
@@ -923,6 +961,17 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                     ca.giant_gmax = gmax;
                     LCHK(launch_chain_stage(8, ca, gblocks, c->stream));
                 }
+            }
+            // pass 0's longest segments (C5's 100 kb chains): one 8-wave workgroup each
+            if (stg == 2 && pass == 0 && ca.lazy && K[MM2G_KNOB_MW_MIN] > 0) {
+                uint32_t mw = 1;
+                while ((int64_t)mw < K[MM2G_KNOB_MW_MIN] && mw < (1u << 30)) mw <<= 1;   // a power of two (k_chain_long_mw)
+                ca.mw_min = mw;
+                int dev = 0, ncu = 256;
+                if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+                ProfScope ps(c, "chain_long_mw");
+                LCHK(launch_chain_stage(9, ca, std::max(1, ncu) * 4, c->stream));
+                ca.mw_min = 0;
             }
             if (stg == 2) continue;   // launched above
             ProfScope ps(c, names[pass][stg]);
@@ -1222,6 +1271,7 @@ static int wait_batch(mm2g_ctx* c) {
         if (it >= 4) return set_err(MM2G_E_STATE, "batch workspaces did not converge (status %u)", bits);
         if (bits & BS_SKETCH) { if (int e = sketch_exact_layout(c, c->sk1)) return e; }
         if (dv_ovf) { if (int e = sketch_exact_layout(c, c->sk2)) return e; }
+        if ((bits & BS_SKETCH) || dv_ovf) c->views_off = true;   // a view may have overflowed its own slot
         if (bits & BS_TAB) c->cap_tab = std::max(c->cap_tab, c->h_stat[1] + c->h_stat[1] / 4 + 1024);
         if (bits & BS_ANCHORS) c->cap_A = std::max(c->cap_A, c->h_stat[2] + c->h_stat[2] / 4 + 65536);
         const mm2g_map_opts o = c->last_opts;
@@ -1233,6 +1283,7 @@ static int wait_batch(mm2g_ctx* c) {
     c->n_anchors = c->h_stat[2];
     c->prof_collect();
     c->collected = true;
+    c->views_off = false;
     return 0;
 }
 
@@ -1359,9 +1410,11 @@ int mm2g_batch_sketch(mm2g_ctx* c, int w, int k, uint32_t rid, uint64_t* out_off
         HIPCHK(hipMemcpyAsync(&o, ovf, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (!o) break;
-        if (it) return set_err(MM2G_E_STATE, "sketch slots did not converge");
+        if (it) { c->views_off = false; return set_err(MM2G_E_STATE, "sketch slots did not converge"); }
         if (int e = sketch_exact_layout(c, B)) return e;
+        c->views_off = true;   // a view may have overflowed its own slot: whole-read sketch for the re-run
     }
+    c->views_off = false;
     std::vector<uint32_t> hc(n); std::vector<uint64_t> hb(n);
     if (n) {
         HIPCHK(hipMemcpyAsync(hc.data(), B.cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));

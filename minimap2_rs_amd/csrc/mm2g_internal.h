@@ -113,6 +113,10 @@ struct SketchArgs {
     const uint64_t* pk_off = nullptr;
     const uint64_t* amb_off = nullptr;
     uint32_t* mz_need = nullptr;   // per sequence: the unclamped minimizer count (mz_cnt is clamped to the slot)
+    // Query views (views of nt4 reads, odd k; DESIGN.md "Query sketch views"):
+    // view r is [view_off[r], + view_len[r]) of read view_read[r] (view_off a
+    // multiple of 8), with the same view_pre / emit_from / view_last meaning.
+    const uint32_t* view_read = nullptr;
 };
 struct FilterArgs {
     uint32_t n;
@@ -221,6 +225,7 @@ struct ChainArgs {
     uint32_t spec_rounds = 3; // k_chain_long: speculative rounds per 64-anchor block (MM2G_KNOB_SPEC_ROUNDS)
     int32_t est_lane = 0;    // k_chain_seg (production): estimated DP pairs up to which a segment takes one lane
     uint32_t full_dp = 0;    // debug mode (exact f/pprev everywhere): pass 0 uses EST_LANE instead of est_lane
+    uint32_t mw_min = 0;     // k_chain_long_mw: segments of >= this many anchors (a power of two; 0 = off)
     const uint32_t* ncand = nullptr;   // pass 0: per read NC_STREAM, NC_STREAM_LB or the sort's candidate count (SortArgs)
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
     const uint32_t* abort = nullptr;
@@ -264,6 +269,13 @@ int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, in
 int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st);
 // minimizer slots: read r gets [rd_off[r] + 16r, rd_off[r+1] + 16(r+1)), or `slot` entries each when non-zero (tests)
 int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st);
+// query sketch views: per-read view counts; view table from their exclusive scan vo; per-read concatenation
+int launch_view_count(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t* nv, hipStream_t st);
+int launch_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, const uint64_t* vo, uint32_t* v_read, uint64_t* v_off,
+                     uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end, hipStream_t st);
+int launch_view_compact(uint32_t n, const uint64_t* vo, const uint64_t* v_off, const uint64_t* v_base, const uint32_t* v_cnt,
+                        const uint32_t* v_need, const uint64_t* vx, const uint32_t* vy, const uint64_t* base, const uint64_t* end, uint64_t* x,
+                        uint32_t* y, uint32_t* cnt, uint32_t* need, int32_t* overflow, hipStream_t st);
 int launch_mid_hist(const mm2g::IxEntry* tab, uint64_t cap, uint32_t nbins, unsigned long long* hist, uint32_t* ovf, uint32_t ovf_cap,
                     uint32_t* ovf_n, hipStream_t st);
 int launch_ix_build(const uint64_t* keys, const uint32_t* offs, const uint32_t* ns, uint64_t nk, mm2g::IxEntry* tab, uint32_t log2cap, hipStream_t st);

@@ -250,8 +250,10 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
         uint64_t roff;
         int64_t L, pre = 0, efrom = 0;
         bool flush = true;
-        if (a.view_off) {   // index chunk: a view into a contig (see SketchArgs)
-            roff = uni64(a.view_off[r]); L = (int64_t)(uint32_t)uni((int32_t)a.view_len[r]);
+        if (a.view_off) {   // index chunk / query view: a view into a contig or read (see SketchArgs)
+            L = (int64_t)(uint32_t)uni((int32_t)a.view_len[r]);
+            if (L == 0) { if (lane == 0) { a.mz_cnt[r] = 0; if (a.mz_need) a.mz_need[r] = 0; } continue; }   // also unused query views
+            roff = uni64(a.view_off[r]);
             pre = (int64_t)(uint32_t)uni((int32_t)a.view_pre[r]); efrom = (int64_t)(uint32_t)uni((int32_t)a.emit_from[r]);
             flush = uni((int32_t)a.view_last[r]) != 0;
         } else {
@@ -260,13 +262,17 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
         }
         Src src;
         if constexpr (std::is_same<Src, SeqNt4>::value) {
-            const uint64_t ao = uni64(a.amb_off[r]);
-            src = Src{(const uint16_t*)(a.pk_words + uni64(a.pk_off[r])), ao == U64MAX ? nullptr : (const uint8_t*)(a.pk_words + ao), L};
+            // query view: the read's words from the view start (a multiple of 8 bases); the
+            // k-mer walk-back reads the read's earlier words (negative positions, >= -pre)
+            const uint32_t rr = a.view_read ? (uint32_t)uni((int32_t)a.view_read[r]) : r;
+            const uint64_t v8 = a.view_read ? roff >> 3 : 0;
+            const uint64_t ao = uni64(a.amb_off[rr]);
+            src = Src{(const uint16_t*)(a.pk_words + uni64(a.pk_off[rr])) + v8, ao == U64MAX ? nullptr : (const uint8_t*)(a.pk_words + ao) + v8, L};
         } else {
             src = Src{a.seq + roff, L};
         }
         const uint64_t obase = uni64(a.out_base[r]), oend = uni64(a.out_end[r]);
-        if (L == 0) { if (lane == 0) a.mz_cnt[r] = 0; continue; }
+        if (L == 0) { if (lane == 0) { a.mz_cnt[r] = 0; if (a.mz_need) a.mz_need[r] = 0; } continue; }
         uint64_t pt[6] = {0, 0, 0, 0, 0, 0}, tz = a.prof ? wall_clock64() : 0;
 #define SK_PT(ph) do { if (a.prof) { const uint64_t t_ = wall_clock64(); pt[ph] += t_ - tz; tz = t_; } } while (0)
         // history slots = positions [-w, -1]: MAX
@@ -2721,6 +2727,239 @@ __global__ __launch_bounds__(1024) void k_lseg_order(ChainArgs a) {
     }
 }
 
+// ---- 5b'. the longest pass-0 segments, one 8-wave workgroup each (C5's
+// ~28 k-anchor chains): k_chain_long's speculative 64-anchor block pass spread
+// over a window of MW_NW blocks.  Per window [W0, W0 + 512): every anchor gets
+// the k_chain_lb guess (a composition scan across the window, seeded with the
+// exact f of W0 - 1); then in each round every lane runs the reference loop
+// (lchain.rs:76-89) of its anchor over its 64 nearest predecessors on the
+// current guesses (Jacobi), and everything before the window's first anchor
+// whose result differs from its guess -- and that anchor, unless its loop
+// reaches past 64 predecessors ("deep") -- is exact and committed (the same
+// induction as k_chain_long's, over the whole window).  A deep anchor at the
+// front of the window gets the reference loop from one thread (marks in an LDS
+// bitmap, predecessors exact).  Segments handled here are marked LSEG_DONE for
+// k_chain_long.  Segments are taken longest first; the list's log2-length
+// buckets make "shorter than mw_min (a power of two)" the end of the work.
+constexpr int MW_NW = 8;                  // waves per workgroup: blocks per window
+constexpr int MW_WIN = MW_NW * 64;
+constexpr int MW_RK = 1024;               // anchor ring (keys, f/pprev): >= window + 64 predecessors + the previous window
+constexpr int MW_MKW = 160;               // mark bitmap words of the one-thread path (max_iter <= 5120)
+static_assert(MW_RK >= 2 * MW_WIN, "ring holds the window and the window before it");
+__global__ __launch_bounds__(MW_NW * 64) void k_chain_long_mw(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int32_t s_ca[MW_NW], s_cb[MW_NW];
+    __shared__ uint32_t s_bad[MW_NW], s_q;
+    __shared__ uint32_t s_mk[MW_MKW];
+    __shared__ unsigned long long s_best;
+    const ChainKParams P = a.P;
+    int16_t* lut = (int16_t*)smem;
+    const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
+    uint64_t* rkey = (uint64_t*)(smem + lut_bytes);
+    int2* rfp = (int2*)(rkey + MW_RK);
+    const uint32_t nl = min(*a.lseg_n, a.lseg_cap);
+    if (nl == 0 || a.mw_min == 0) return;
+    {   // the longest segment is first: nothing to do below mw_min
+        const uint4 L0 = a.lseg[a.lseg_order[0]];
+        if (L0.z - L0.y < a.mw_min) return;
+    }
+    load_lut(lut, a.lut, P.lut_n);
+    __syncthreads();
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const uint32_t qb = a.kl.qb, rb = a.kl.rb;
+    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
+    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
+    constexpr int32_t NEG = -(1 << 29);
+    constexpr uint32_t RM = MW_RK - 1;
+    auto sc_of = [&](uint64_t ki, uint64_t kj, bool& ok) -> int32_t {   // comput_sc (lchain.rs:17-34), LUT penalty
+        const int32_t dq = (int32_t)(ki & qmask) - (int32_t)(kj & qmask), dr = (int32_t)((ki >> qb) & rmask) - (int32_t)((kj >> qb) & rmask);
+        const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
+        ok = dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
+        const int32_t dg = dr < dq ? dr : dq;
+        return (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
+    };
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) s_q = atomicAdd(&a.work[2 + (P.pass & 1)], 1u);
+        __syncthreads();
+        const uint32_t t = s_q;
+        if (t >= nl) break;
+        const uint32_t q = a.lseg_order[t];
+        const uint4 L = a.lseg[q];
+        if (L.z - L.y < a.mw_min) break;            // every later one is shorter
+        if (L.w == LSEG_DONE) continue;
+        const uint32_t r = L.x;
+        const int32_t s = (int32_t)L.y, e = (int32_t)L.z;
+        const uint64_t base = a.a_off[r];
+        const uint64_t* K = a.keys + base;
+        int32_t* F = a.f + base; int32_t* PP = a.pp + base;
+        int32_t bf = INT_MIN, bi = -1;
+        uint64_t pairs = 0;
+        if (tid == 0) {                             // anchor s: isolated
+            rkey[s & RM] = K[s]; rfp[s & RM] = make_int2(span, -1);
+            F[s] = span; PP[s] = -1;
+            best_merge(bf, bi, span, s);
+            s_best = 0;
+        }
+        int32_t committed = s + 1;
+        while (committed < e) {
+            const int32_t W0 = committed, W1 = min(e, W0 + MW_WIN);
+            const int32_t k = W0 + tid;
+            const bool kv = k < W1;
+            const uint64_t ak = kv ? K[k] : 0;
+            if (kv) rkey[k & RM] = ak;
+            __syncthreads();
+            // predecessors within reach: j in [max(st_k, k - max_iter), k-1]; 65 = more than 64
+            int32_t dlim = 0;
+            const int32_t pk = (int32_t)((ak >> qb) & rmask);
+            if (kv) {
+                const int32_t b0 = max(s, k - 64);
+                const int32_t pb = (int32_t)((rkey[b0 & RM] >> qb) & rmask);
+                int32_t stk = b0;
+                if (pk > (int32_t)((uint32_t)pb + (uint32_t)maxdx)) {
+                    int32_t pos = b0;
+#pragma unroll
+                    for (int stp = 32; stp >= 1; stp >>= 1) {
+                        const int32_t m = pos + stp;
+                        const int32_t pm = (int32_t)((rkey[(m < k ? m : k) & RM] >> qb) & rmask);
+                        if (m < k && pk > (int32_t)((uint32_t)pm + (uint32_t)maxdx)) pos = m;
+                    }
+                    stk = pos + 1;
+                }
+                int32_t nc = (stk == b0 && b0 > s) ? 65 : k - stk;
+                dlim = nc < P.max_iter ? nc : P.max_iter;
+            }
+            // first guess: the chain through k-1, a composition scan over the window
+            {
+                bool okp = false;
+                int32_t scp = 0;
+                if (kv && dlim >= 1) scp = sc_of(ak, rkey[(k - 1) & RM], okp);
+                int32_t ga = kv ? (okp ? scp : NEG) : 0, gb = kv ? (okp ? NEG : span) : NEG;
+                scan_lb(ga, gb);
+                if (lane == 63) { s_ca[wv] = ga; s_cb[wv] = gb; }
+                __syncthreads();
+                int32_t x = rfp[(W0 - 1) & RM].x;
+                for (int w2 = 0; w2 < wv; ++w2) x = max(max(x + s_ca[w2], NEG), s_cb[w2]);
+                if (kv) rfp[k & RM] = make_int2(max(x + ga, gb), okp ? k - 1 : -1);
+            }
+            __syncthreads();
+            int32_t comm = W0;
+            bool stuck = false;                     // the window's first unsettled anchor is deep
+            for (int rnd = 0; rnd < 8; ++rnd) {
+                const bool act0 = kv && k >= comm;
+                int32_t mf = span, mj = -1, ns = 0, vis = 0;
+                uint64_t mkm = 0;
+                bool brk = false;
+                for (int d0 = 1; d0 <= 64; d0 += 4) {
+                    if (!any(act0 && !brk && d0 <= dlim)) break;
+                    int32_t sv4[4], pp4[4];
+                    bool ok4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int d = d0 + u;
+                        const bool inr = act0 && d <= dlim;
+                        const int32_t j = k - d;
+                        uint64_t kj = 0;
+                        int2 fpj = make_int2(0, -1);
+                        if (inr) { kj = rkey[j & RM]; fpj = rfp[j & RM]; }
+                        bool ok;
+                        const int32_t sc = sc_of(ak, kj, ok);
+                        ok4[u] = inr && ok;
+                        sv4[u] = sc + fpj.x;
+                        pp4[u] = fpj.y;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int d = d0 + u;
+                        const bool act = act0 && !brk && d <= dlim;
+                        vis += act ? 1 : 0;
+                        if (act && ok4[u]) {
+                            if (sv4[u] > mf) { mf = sv4[u]; mj = k - d; if (ns > 0) --ns; }
+                            else if ((mkm >> (d - 1)) & 1ULL) { ++ns; if (ns > P.max_skip) brk = true; }
+                            if (!brk && pp4[u] >= 0) { const int32_t tt = k - pp4[u]; if (tt <= 64) mkm |= 1ULL << ((tt - 1) & 63); }
+                        }
+                    }
+                }
+                const bool deep = act0 && !brk && dlim > 64;
+                const int2 gv = act0 ? rfp[k & RM] : make_int2(0, 0);
+                const bool bad = act0 && (deep || mf != gv.x || mj != gv.y);
+                const uint64_t badM = ballot(bad), deepM = ballot(deep);
+                if (lane == 0) s_bad[wv] = badM ? ((uint32_t)(wv * 64 + ctz64(badM)) | (((deepM >> ctz64(badM)) & 1ULL) ? 0x80000000u : 0u)) : 0x7fffffffu;
+                __syncthreads();                    // every lane has read rfp; the first bad anchors are known
+                uint32_t fbw = 0x7fffffffu;
+                for (int w2 = 0; w2 < MW_NW; ++w2) { const uint32_t v = s_bad[w2]; if ((v & 0x7fffffffu) < (fbw & 0x7fffffffu)) fbw = v; }
+                const bool fb_deep = fbw != 0x7fffffffu && (fbw & 0x80000000u);
+                const int32_t fb = fbw == 0x7fffffffu ? W1 : W0 + (int32_t)(fbw & 0x7fffffffu);
+                const int32_t cend = fb_deep ? fb : (fb < W1 ? fb + 1 : W1);
+                pairs += (act0 && k < cend) ? (uint64_t)vis : 0ull;
+                if (act0 && k >= fb && !deep) rfp[k & RM] = make_int2(mf, mj);   // fb exact, later lanes the next guess
+                __syncthreads();
+                comm = cend;
+                if (comm >= W1) break;
+                if (fb_deep) { stuck = true; break; }
+            }
+            // commit [W0, comm)
+            if (kv && k < comm) {
+                const int2 v = rfp[k & RM];
+                F[k] = v.x; PP[k] = v.y;
+                best_merge(bf, bi, v.x, k);
+            }
+            if (stuck) {
+                // the reference loop for anchor c = comm, one thread; every predecessor is exact
+                __syncthreads();                    // F/PP of this window's committed anchors written
+                if (tid == 0) {
+                    const int32_t c = comm;
+                    const uint64_t kc = rkey[c & RM];
+                    const int32_t pc = (int32_t)((kc >> qb) & rmask);
+                    int32_t lo = s, hi = c;         // st_c: the first j >= s with pc <= p_j + maxdx (keys sorted by p)
+                    while (lo < hi) {
+                        const int32_t m = (lo + hi) >> 1;
+                        const uint64_t km = m >= W0 - MW_WIN ? rkey[m & RM] : K[m];
+                        if (pc > (int32_t)((uint32_t)(int32_t)((km >> qb) & rmask) + (uint32_t)maxdx)) lo = m + 1; else hi = m;
+                    }
+                    const int32_t jlo = max(lo, c - P.max_iter);
+                    const int32_t nwd = (c - jlo + 31) >> 5;
+                    for (int32_t w2 = 0; w2 < nwd && w2 < MW_MKW; ++w2) s_mk[w2] = 0;
+                    int32_t mf = span, mj = -1, ns = 0;
+                    for (int32_t j = c - 1; j >= jlo; --j) {
+                        const bool in_ring = j >= W0 - MW_WIN;
+                        const uint64_t kj = in_ring ? rkey[j & RM] : K[j];
+                        const int2 fpj = in_ring ? rfp[j & RM] : make_int2(F[j], PP[j]);
+                        bool ok;
+                        const int32_t sv = sc_of(kc, kj, ok) + fpj.x;
+                        ++pairs;
+                        if (!ok) continue;
+                        if (sv > mf) { mf = sv; mj = j; if (ns > 0) --ns; }
+                        else if ((s_mk[(j - jlo) >> 5] >> ((j - jlo) & 31)) & 1u) { if (++ns > P.max_skip) break; }
+                        if (fpj.y >= jlo) s_mk[(fpj.y - jlo) >> 5] |= 1u << ((fpj.y - jlo) & 31);
+                    }
+                    rfp[c & RM] = make_int2(mf, mj);
+                    F[c] = mf; PP[c] = mj;
+                    best_merge(bf, bi, mf, c);
+                }
+                comm += 1;
+            }
+            __syncthreads();
+            committed = comm;
+        }
+        // the segment's last argmax f (packed key) and DP pair count
+        uint64_t bk = bi >= 0 ? best_key(bf, bi) : 0ull;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(bk, d, 64); bk = o > bk ? o : bk; }
+        pairs = wave_sum64(pairs);
+        if (lane == 0) {
+            if (bk) atomicMax(&s_best, bk);
+            if (pairs) atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)pairs);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            atomicMax(a.rbest + r, s_best);
+            a.lseg[q].w = LSEG_DONE;
+        }
+    }
+}
+
 // ---- 5b. one long segment per wave, wave-cooperative (heaviest first)
 // PROF (MM2G_KNOB_LSEG_PROF): shader-clock cycles of each phase of the
 // per-anchor step, summed over the pass's long segments into a.gprof[16..31]:
@@ -3868,6 +4107,64 @@ __global__ void k_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, ui
     end[r] = rd_off[r + 1] + 16ull * (r + 1);
 }
 
+// ---- Query sketch views (DESIGN.md "Query sketch views"): a read longer than
+// V bases is sketched as views of V emitting bases, each after a warm-up of
+// >= W0 bases (W0 = 2(w+k)+64 rounded up to 8: enough for odd k, DESIGN.md
+// §10), one wave per view, so a 10 kb read is not 20 sequential tiles of one
+// wave.  View outputs go to their own slots and are concatenated per read.
+__global__ void k_view_count(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t* nv) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t L = rd_off[r + 1] - rd_off[r];
+    nv[r] = L <= V ? 1u : (uint32_t)((L + V - 1) / V);
+}
+// view v = vo[r] + j of read r: emitting [jV, min(L, (j+1)V)), starting W0 (or
+// more, to a multiple of 8) bases earlier; its output slot is [rd_off[r] + jV +
+// 16 v, + emitting bases + 16), disjoint across all views
+__global__ void k_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, const uint64_t* vo, uint32_t* v_read,
+                            uint64_t* v_off, uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base,
+                            uint64_t* v_end) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t L = rd_off[r + 1] - rd_off[r];
+    const uint32_t nv = L <= V ? 1u : (uint32_t)((L + V - 1) / V);
+    for (uint32_t j = 0; j < nv; ++j) {
+        const uint64_t v = vo[r] + j;
+        const uint64_t c0 = (uint64_t)j * V, ve = c0 + V < L ? c0 + V : L;
+        const uint64_t vs = j ? (c0 > W0 ? (c0 - W0) & ~7ULL : 0) : 0;
+        v_read[v] = r; v_off[v] = vs; v_len[v] = (uint32_t)(ve - vs); v_pre[v] = (uint32_t)vs;
+        v_from[v] = (uint32_t)(c0 - vs); v_last[v] = ve == L ? 1 : 0;
+        v_base[v] = rd_off[r] + c0 + 16 * v; v_end[v] = v_base[v] + (ve - c0) + 16;
+    }
+}
+// one wave per read: its views' minimizers, in view order, into the read's slot
+// (y + view start << 1: positions are view-relative), clamped and flagged like k_sketch
+__global__ __launch_bounds__(256) void k_view_compact(uint32_t n, const uint64_t* vo, const uint64_t* v_off, const uint64_t* v_base,
+                                                      const uint32_t* v_cnt, const uint32_t* v_need, const uint64_t* vx, const uint32_t* vy,
+                                                      const uint64_t* base, const uint64_t* end, uint64_t* x, uint32_t* y,
+                                                      uint32_t* cnt, uint32_t* need, int32_t* overflow) {
+    const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const int lane = lane_id();
+    const uint64_t b = base[r], capn = end[r] - b;
+    uint64_t o = 0, tn = 0;   // copied so far; the views' true (unclamped) counts
+    for (uint64_t v = vo[r]; v < vo[r + 1]; ++v) {
+        const uint64_t vb = v_base[v];
+        const uint32_t c = v_cnt[v];
+        const uint32_t add = (uint32_t)(v_off[v] << 1);
+        for (uint32_t i = lane; i < c; i += 64) {
+            if (o + i < capn) { x[b + o + i] = vx[vb + i]; y[b + o + i] = vy[vb + i] + add; }
+        }
+        o += c;
+        tn += v_need[v];
+    }
+    if (lane == 0) {   // a view that overflowed its own slot flagged it already; the re-run has views off
+        cnt[r] = (uint32_t)(o > capn ? capn : o);
+        need[r] = (uint32_t)(tn > 0xffffffffULL ? 0xffffffffULL : tn);
+        if (o > capn) atomicOr(overflow, 1);
+    }
+}
+
 // Build the device index table from (key, off, n) triples (insert with CAS).
 __global__ void k_ix_build(const uint64_t* keys, const uint32_t* offs, const uint32_t* ns, uint64_t nk, IxEntry* tab, uint32_t log2cap) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4026,6 +4323,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
     case 7: hipLaunchKernelGGL(k_chain_giant<false>, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
     case 8: hipLaunchKernelGGL(k_chain_giant<true>, dim3(blocks), dim3(1024), lut_lds(a.P.lut_n), st, a); break;
+    case 9: hipLaunchKernelGGL(k_chain_long_mw, dim3(blocks), dim3(MW_NW * 64), lut_lds(a.P.lut_n) + (size_t)MW_RK * 16, st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 3) / 4), dim3(256), 0, st, a); break;
     }
     LAUNCH_CHECK();
@@ -4045,6 +4343,29 @@ int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, in
 }
 int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st) {
     hipLaunchKernelGGL(k_batch_sums, dim3(1), dim3(1024), 0, st, n, mz_cnt, cnt2, status64);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_view_count(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t* nv, hipStream_t st) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_view_count, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, V, nv);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, const uint64_t* vo, uint32_t* v_read, uint64_t* v_off,
+                     uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end, hipStream_t st) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_view_fill, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, V, W0, vo, v_read, v_off, v_len, v_pre, v_from,
+                       v_last, v_base, v_end);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_view_compact(uint32_t n, const uint64_t* vo, const uint64_t* v_off, const uint64_t* v_base, const uint32_t* v_cnt,
+                        const uint32_t* v_need, const uint64_t* vx, const uint32_t* vy, const uint64_t* base, const uint64_t* end, uint64_t* x,
+                        uint32_t* y, uint32_t* cnt, uint32_t* need, int32_t* overflow, hipStream_t st) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_view_compact, dim3((n + 3) / 4), dim3(256), 0, st, n, vo, v_off, v_base, v_cnt, v_need, vx, vy, base, end, x, y,
+                       cnt, need, overflow);
     LAUNCH_CHECK();
     return 0;
 }

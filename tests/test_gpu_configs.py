@@ -153,6 +153,9 @@ def test_c5_hg38_100kb(hg38, tmp_path):
         gf, gpp = dev.debug_dp(r)
         n = len(want)
         assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
+    # pass 0's 100 kb chains through k_chain_long_mw (one 8-wave workgroup per segment of >= 4096 anchors)
+    with knobs(dev, mw_min=4096):
+        _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5mw")
     with knobs(dev, giant_lcap=64):
         res2, _ = _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5hbm")
         for r in rescued:

@@ -54,6 +54,34 @@ def test_sketch_parity(dev, w, k):
         assert np.array_equal(g, want), (i, len(s))
 
 
+@pytest.mark.parametrize("view", [64, 512, 2560])
+def test_sketch_views_parity(dev, view):
+    """Query sketch views (odd k: reads longer than `view` bases are sketched as
+    views of `view` emitting bases after a warm-up, one wave each, then
+    concatenated; DESIGN.md "Query sketch views") equal the oracle's
+    sketch_sequence, also across N runs, lowercase and periodic stretches at
+    view edges; even k keeps the whole-read path."""
+    rng = random.Random(77 + view)
+    seqs = []
+    for i in range(24):
+        n = rng.choice([60, 700, 3000, 10000, 31000])
+        s = bytearray(_rand_seq(rng, n, p_n=0.002 if i % 3 else 0.0))
+        if i % 4 == 1:   # a periodic stretch (ties) and an N run around a view edge
+            st = min(len(s) - 1, view - 40) if len(s) > view else 0
+            unit = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(1, 6)))
+            for j in range(st, min(len(s), st + 300)):
+                s[j] = unit[(j - st) % len(unit)]
+            for j in range(min(len(s), st + 310), min(len(s), st + 330)):
+                s[j] = ord("N")
+        seqs.append(bytes(s))
+    with knobs(dev, sketch_view=view):
+        for w, k in ((10, 15), (5, 11), (19, 19), (1, 3), (255, 21), (3, 16)):
+            got = dev.sketch_sequences(seqs, w, k, rid=0)
+            for i, s in enumerate(seqs):
+                want = O.sketch(s, w, k, 0, False)
+                assert np.array_equal(got[i], want), (view, w, k, i, len(s))
+
+
 def test_sketch_rid(dev):
     rng = random.Random(5)
     seqs = [_rand_seq(rng, 3000, p_n=0.01) for _ in range(3)]
@@ -116,8 +144,8 @@ def test_pipeline_parity(dev, small_world, tmp_path):
     assert _map_nodebug(dev, rnames, rseqs)[0] == got          # production path (singleton filter on)
 
 
-@pytest.mark.parametrize("mid_occ", [None, 20, 5000])
-def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ):
+@pytest.mark.parametrize("mid_occ,mw", [(None, 0), (20, 0), (5000, 0), (None, 64), (20, 64), (5000, 128)])
+def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ, mw):
     """The production DP shortcuts keep every f/pprev exact: k_chain_long's
     simple paths (no mark source can break the loop; a chain's maximum visited
     early with a break proven inside the first window) and lazy windows, and
@@ -129,7 +157,8 @@ def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ):
     idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
     mid = max(idx.calc_mid_occ(2e-4), 10) if mid_occ is None else mid_occ
     dev.upload_index(idx, mid)
-    with knobs(dev, lazy=2, giant_min=64):
+    # mw: pass-0 segments of >= mw anchors take k_chain_long_mw (8 waves, speculative windows of 512)
+    with knobs(dev, lazy=2, giant_min=64, mw_min=mw):
         dev.set_debug(True)
         dev.set_reads(rseqs)
         res = dev.map(M.map_opts())

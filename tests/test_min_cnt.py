@@ -2,7 +2,7 @@
 
 The backtrack of chain_dp_all (/root/reference/src/lchain.rs:92-160) sets
 t[i] = 2 and then tests t[i] == 0 in the same iteration of mg_chain_bk_end's
-loop (lchain.rs:112-115), so the loop always stops after one step: every chain
+loop (lchain.rs:110,114 and 140,144), so the loop always stops after one step: every chain
 it extracts is the single anchor i0, with score f[i0] - f[pprev[i0]] (or f[i0]
 = span when pprev is -1), never above the span.  Hence:
   * -m above the span (the default 40 > k <= 28): no backtrack chain passes
