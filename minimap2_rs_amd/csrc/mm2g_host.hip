@@ -133,7 +133,7 @@ struct mm2g_ctx {
     DevBuf tab_off, tab_key, tab_cnt;
     DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
     DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist, ncand;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, item_read, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist, ncand;
     DevBuf dstat;                          // batch status block (BS_* word, workspace needs, counters)
     DevBuf chain_rdoff;                    // mm2g_chain_batch: prefix sums of the caller's qlen
     uint64_t cap_tab = 0, cap_A = 0;       // filter-table entries / anchors the workspaces hold
@@ -205,16 +205,17 @@ struct ProfScope {
 
 // MM2G_KNOB_SORT_PROF: phase times of k_sort_read (wall clock, 100 MHz) to stderr
 static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
-    std::vector<uint64_t> h((size_t)n * 16);
+    std::vector<uint64_t> h((size_t)n * 24);
     if (hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) return;
     (void)hipFree(d);
     double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0, nleg = 0, nbigp = 0, ktiny = 0, klong = 0, ksrch = 0;
+    double lb_scan = 0, lb_all = 0, n_lb = 0, n_cand = 0, n_over = 0;
     uint64_t t_lo = ~0ULL, t_hi = 0;
     uint32_t m = 0;
     std::vector<uint32_t> q0, q2, q3;
     for (uint32_t r = 0; r < n; ++r) {
-        const uint64_t* p = &h[(size_t)r * 16];
+        const uint64_t* p = &h[(size_t)r * 24];
         if (!p[11]) continue;
         q3.push_back((uint32_t)p[13]);
         ++m;
@@ -227,6 +228,8 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
         t_lo = std::min(t_lo, p[10]); t_hi = std::max(t_hi, p[11]);
         q0.push_back((uint32_t)p[8]); q2.push_back((uint32_t)p[9]);
         ktiny += (double)(uint32_t)p[14]; klong += (double)(p[14] >> 32); ksrch += (double)p[15];
+        lb_scan += (double)p[16]; lb_all += (double)p[17];
+        if (p[17]) { ++n_lb; n_cand += (double)p[18]; if (p[18] > (uint64_t)(p[9] & 0xffffffffu) / 32 + 8) ++n_over; }
     }
     if (!m) return;
     std::sort(q0.begin(), q0.end()); std::sort(q2.begin(), q2.end()); std::sort(q3.begin(), q3.end());
@@ -239,6 +242,9 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
             ph[5] / m / 100, ph[6] / m / 100, tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
     fprintf(stderr, "[sort_prof] keys per read in segments <= %u: %.0f, 17..64: %.0f, > 64: %.0f (%.2f other-chunk searches each)\n",
             16u, ktiny / m, (a2 - ktiny - klong) / m, klong / m, klong > 0 ? ksrch / klong : 0.0);
+    if (n_lb > 0)
+        fprintf(stderr, "[sort_prof] LB pass on %.0f reads: scan %.1f us, with candidates %.1f us per read; candidates per read %.2f, "
+                        "over budget (streamed) %.0f reads\n", n_lb, lb_scan / n_lb / 100, lb_all / n_lb / 100, n_cand / n_lb, n_over);
 }
 
 // MM2G_SKETCH_PROF: phase times of k_sketch summed over each read's tiles
@@ -894,6 +900,12 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     uint32_t* item_off;
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
+    {   // items per read <= max(ceil(A / seg_chunk), the sort's candidate budget A / 32 + 8)
+        const uint64_t icap = std::min<uint64_t>(A_cap / 32 + 8ull * n + 1024, 0xffffffffull);
+        uint32_t* ir;
+        ENSURE(c->item_read, uint32_t, icap, ir);
+        ca.item_read = ir; ca.item_cap = (uint32_t)icap;
+    }
     ca.seg_chunk = std::max<uint32_t>(64u, (uint32_t)K[MM2G_KNOB_SEG_CHUNK] & ~63u);
     ca.spec_rounds = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(16, K[MM2G_KNOB_SPEC_ROUNDS]));
     // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
@@ -914,7 +926,10 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         if (mb <= 0) mb = 1024;
         sb = std::max(1, std::min((int)((n * 4 + 3) / 4), sb));   // items: up to ~4 chunks per read
         HIPCHK(hipMemsetAsync(rbest, 0, (size_t)n * 8, c->stream));
-        HIPCHK(hipMemsetAsync(lseg_n, 0, 16, c->stream));   // long count (pass 0/1 slot), medium count, medium taken
+        // long count (pass 0/1 slot), medium count, medium taken; pass 0's long count may hold the
+        // sort's candidate segments already (zeroed before the sort, sort_lb_cands)
+        if (pass == 0 && sort_fmin) HIPCHK(hipMemsetAsync(lseg_n + 2, 0, 8, c->stream));
+        else HIPCHK(hipMemsetAsync(lseg_n + pass, 0, 16 - 4 * (size_t)pass, c->stream));
         static const char* names[2][5] = {{"chain_seg", "chain_med", "chain_lorder", "chain_long", "chain_fin"},
                                           {"chain_seg_rescue", "chain_med_rescue", "chain_lorder_rescue", "chain_long_rescue", "chain_fin_rescue"}};
         const int blocks[5] = {sb, mb, 1, lb, 0};
@@ -1202,6 +1217,14 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
             lut_sort = l;
         }
     }
+    // the long-segment queue: the sort's LB pass appends pass 0's long candidate segments to it
+    uint4* lseg_q = nullptr; uint32_t* lseg_nq = nullptr;
+    const uint32_t lcap_q = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_MED + 1) + 64, 0xffffffffu);
+    if (lut_sort) {
+        uint32_t* lo_;
+        ENSURE(c->lseg, uint4, lcap_q, lseg_q); ENSURE(c->lseg_order, uint32_t, lcap_q, lo_); ENSURE(c->lseg_n, uint32_t, 4, lseg_nq);
+        HIPCHK(hipMemsetAsync(lseg_nq, 0, 16, c->stream));
+    }
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
                 filt ? c->dix->cells : 0u, cnt2, smax, (uint32_t)std::min<int64_t>(K[MM2G_KNOB_SORT_SMALL], 4096), nullptr, 0u,
                 (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_SEG_SMALL], SEG_THREAD)), nullptr};
@@ -1211,8 +1234,9 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     so.ncand = ncand; so.fmin = fmin_buf; so.lut = lut_sort; so.P = P; so.lb_mode = (uint32_t)K[MM2G_KNOB_SORT_LB];
+    so.lseg = lseg_q; so.lseg_n = lseg_nq; so.lseg_cap = lcap_q;
     uint64_t* sprof = nullptr;
-    if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 128)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 128, c->stream)); so.prof = sprof; }
+    if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 192)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 192, c->stream)); so.prof = sprof; }
     if (stop_at != 1) {
     {
         ProfScope ps(c, "sort_small");

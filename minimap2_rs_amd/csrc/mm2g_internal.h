@@ -182,6 +182,9 @@ struct SortArgs {
     uint32_t lb_mode = 1;              // EXPERIMENT: 2 = only drain stores + barrier, 3 = LB without candidates
     const int16_t* lut = nullptr;      // comput_sc pen LUT of pass 0 (lut_n entries)
     ChainKParams P{};                  // pass-0 chain parameters (max_dist_x/y, bw, span, lut_n)
+    uint4* lseg = nullptr;             // pass 0's long-segment queue (ChainArgs::lseg): candidates of more than
+    uint32_t* lseg_n = nullptr;        //   CHAIN_TINY anchors go there directly, only shorter ones to k_chain_seg
+    uint32_t lseg_cap = 0;
 };
 constexpr uint32_t NC_STREAM = 0xffffffffu;      // no LB from the sort: k_chain_lb + streaming k_chain_seg
 constexpr uint32_t NC_STREAM_LB = 0xfffffffeu;   // fmin from the sort (k_chain_lb skips the read), streaming k_chain_seg
@@ -217,6 +220,8 @@ struct ChainArgs {
     uint32_t lseg_prof;      // MM2G_LSEG_PROF: k_chain_long stores each long segment's wall-clock ticks in lseg[].w
     uint32_t lazy;           // k_chain_long: skip deep windows no predecessor of which can beat max_f (not in debug mode)
     uint32_t* item_off;      // k_seg_items: first work item (chunk) of order[t]; [n] = total
+    uint32_t* item_read = nullptr;   // k_seg_items: per work item its position t in order (null: search item_off)
+    uint32_t item_cap = 0;           // entries of item_read
     uint32_t seg_chunk;      // anchors per work item (multiple of 64; SEG_CHUNK)
     uint32_t giant_min;      // long segments of at least this many anchors try k_chain_giant first (rescue: 128)
     uint32_t giant_lcap;     // tests: cap of the LDS variant below its LDS capacity (0 = none)

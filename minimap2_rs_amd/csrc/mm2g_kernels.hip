@@ -230,6 +230,11 @@ struct SeqNt4 {
         if (am && ((am[p >> 3] >> (p & 7)) & 1u)) return 4u;
         return ((uint32_t)s2[p >> 3] >> (2 * (p & 7))) & 3u;
     }
+    // 8 bases at p0 < 0 (a multiple of 8) of a query view: the read's bases before the view
+    DEVI uint64_t raw_back(int64_t p0) const {
+        const uint64_t v = s2[p0 >> 3], m = am ? am[p0 >> 3] : 0u;
+        return v | (m << 16) | (8ULL << 24);
+    }
 };
 
 template <bool K32, typename Src, bool HPC = false>
@@ -288,6 +293,15 @@ __global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
         uint32_t code16, valid8;
         src.decode(src.raw((int64_t)lane * SK_CH), code16, valid8);
         uint32_t halo = 0;
+        if constexpr (std::is_same<Src, SeqNt4>::value) {
+            // a query view: the 32 bases before it seed the first tile's k-mer registers (the fast
+            // path), instead of every view's lane 0 walking back over HBM base by base
+            if (pre >= 32 && lane >= 60) {
+                uint32_t c16, v8;
+                src.decode(src.raw_back((int64_t)(lane - 64) * SK_CH), c16, v8);
+                halo = c16 | (rev8(v8) << 16);
+            }
+        }
         for (int64_t t0 = 0; t0 < L; t0 += SK_TS) {
             // opaque per tile: keeps lane-derived values from being hoisted and held
             // in registers across the read loop (VGPR pressure)
@@ -1301,74 +1315,91 @@ DEVI void scan_lb(int32_t& a, int32_t& b) {
 // w4: 5 NW words of static LDS.
 template <int NT>
 DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, const uint64_t* O, uint32_t* Kc, uint32_t A, unsigned char* lds,
-                        uint32_t* w4, uint32_t* s_sc) {
+                        uint32_t* w4, uint32_t* s_sc, uint64_t* pq) {
     constexpr int NW = NT / 64;
     constexpr int32_t NEG = -(1 << 29);
-    constexpr int U = 8;                           // chunks whose loads are in flight together
+    constexpr int U = 8;                           // chunks per wave per round, all independent (loads in flight together)
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const ChainKParams P = a.P;                   // a copy: a reference into the kernel argument forces it to scratch
     int16_t* lut = (int16_t*)lds;
     uint64_t* isob = (uint64_t*)(lds + (((P.lut_n * 2) + 15) & ~15));
     load_lut(lut, a.lut, P.lut_n);
     __syncthreads();
+    const uint64_t t_lb0 = pq && tid == 0 ? wall_clock64() : 0;
     const uint32_t qb = a.qb, gsh = a.qb + a.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << a.rb) - 1;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
     const uint32_t nwd = (A + 63) >> 6;
-    const uint32_t wper = (nwd + NW - 1) / NW;
-    const uint32_t c_lo = min(nwd, (uint32_t)wv * wper), c_hi = min(nwd, c_lo + wper);
-    int32_t CA = 0, CB = NEG, MA = NEG, MB = NEG;   // the range's composition so far (identity), max prefix A / B
-    uint64_t prevk = 0;
-    if (c_lo < c_hi && c_lo > 0) prevk = uni64(O[c_lo * 64 - 1]);
-    for (uint32_t c0 = c_lo; c0 < c_hi; c0 += U) {
-        uint64_t kk[U];
+    int32_t* wca = (int32_t*)w4;                  // [NW] the waves' round compositions (a, b)
+    int32_t* wcb = wca + NW;
+    // Rounds of NW * U chunks: wave w takes chunks c = c0 + w*U + u.  Each chunk's
+    // inclusive composition scan (lane l: the composition of its lanes 0..l) stays
+    // in registers until the LB entering the chunk is known (a scan over the
+    // chunks' totals: in the wave, then across the waves through LDS); nothing
+    // is carried from chunk to chunk inside a wave.
+    int32_t carry = NEG, best = span;
+    for (uint32_t c0 = 0; c0 < nwd; c0 += NW * U) {
+        int32_t sa[U], sb[U];
+        uint64_t kk[U], pv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t i = (c0 + (uint32_t)u) * 64 + (uint32_t)lane;
-            kk[u] = (c0 + (uint32_t)u < c_hi && i < A) ? O[i] : 0;
+            const uint32_t cc = c0 + (uint32_t)(wv * U + u), i = cc * 64 + (uint32_t)lane;
+            kk[u] = (cc < nwd && i < A) ? O[i] : 0;
+            pv[u] = (cc < nwd && cc > 0) ? O[cc * 64 - 1] : 0;   // the chunk's predecessor key (same address on every lane)
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if (c0 + (uint32_t)u < c_hi) {         // wave-uniform; no break: kk[] stays in registers
-            const uint32_t i = (c0 + (uint32_t)u) * 64 + (uint32_t)lane;
-            const bool valid = i < A;
+            const uint32_t cc = c0 + (uint32_t)(wv * U + u), i = cc * 64 + (uint32_t)lane;
+            const bool valid = cc < nwd && i < A;
             const uint64_t ak = kk[u];
-            const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)(uint32_t)(prevk >> 32)) << 32) |
-                                (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)(uint32_t)prevk);
+            const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)(uint32_t)(pv[u] >> 32)) << 32) |
+                                (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)(uint32_t)pv[u]);
             const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
             const int32_t p = (int32_t)((ak >> qb) & rmask), pj = (int32_t)((pk >> qb) & rmask);
             const int32_t q = (int32_t)(ak & qmask), qj = (int32_t)(pk & qmask);
             const bool iso = valid && (i == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx));
-            int32_t sa = NEG;
+            int32_t xa = valid ? NEG : 0, xb = valid ? span : NEG;   // invalid lanes: the identity
             if (valid && !iso) {   // comput_sc (lchain.rs:17-34) of (i, i-1); the LUT is (gap*dd + 0.5*log2(dd+1)) as i32
                 const int32_t dq = q - qj, dr = p - pj;
                 const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
                 if (dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw) {
                     const int32_t dg = dr < dq ? dr : dq;
-                    sa = (span < dg ? span : dg) - (int32_t)lut[dd];
+                    xa = (span < dg ? span : dg) - (int32_t)lut[dd];
                 }
             }
-            int32_t sb = valid ? span : NEG;
-            scan_lb(sa, sb);
-            const int32_t Ai = max(CA + sa, NEG), Bi = max(CB + sa, sb);
-            if (valid) { MA = max(MA, Ai); MB = max(MB, Bi); }
+            scan_lb(xa, xb);
+            sa[u] = xa; sb[u] = valid ? xb : NEG;      // sb of an invalid lane never counts for the best
             const uint64_t im = ballot(iso);
-            if (lane == 0) isob[c0 + (uint32_t)u] = im;
-            CA = rdl(Ai, 63); CB = rdl(Bi, 63);
-            prevk = ((uint64_t)rdlu((uint32_t)(ak >> 32), 63) << 32) | rdlu((uint32_t)ak, 63);
-          }
+            if (lane == 0 && cc < nwd) isob[cc] = im;
         }
-    }
-    MA = rdl(scan_max(MA), 63); MB = rdl(scan_max(MB), 63);
-    int32_t* wca = (int32_t*)w4;
-    if (lane == 0) { wca[wv] = CA; wca[NW + wv] = CB; wca[2 * NW + wv] = MA; wca[3 * NW + wv] = MB; }
-    __syncthreads();
-    int32_t x = NEG, best = span;
+        // the wave's composition over its U chunks (lane 63 of each), in chunk order
+        int32_t ra = 0, rb = NEG;
 #pragma unroll
-    for (int t = 0; t < NW; ++t) {
-        best = max(best, max(x + wca[2 * NW + t], wca[3 * NW + t]));
-        x = max(max(x + wca[t], NEG), wca[NW + t]);
+        for (int u = 0; u < U; ++u) {
+            const int32_t ca = rdl(sa[u], 63), cb = rdl(sb[u], 63);
+            rb = max(rb + ca, cb); ra = max(ra + ca, NEG);
+        }
+        __syncthreads();                           // the previous round's readers are done with wca / wcb
+        if (lane == 0) { wca[wv] = ra; wcb[wv] = rb; }
+        __syncthreads();
+        int32_t x = carry;
+        for (int w2 = 0; w2 < wv; ++w2) x = max(max(x + wca[w2], NEG), wcb[w2]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            best = max(best, max(x + sa[u], sb[u]));
+            x = max(max(x + rdl(sa[u], 63), NEG), rdl(sb[u], 63));
+        }
+        int32_t xc = carry;
+        for (int w2 = 0; w2 < NW; ++w2) xc = max(max(xc + wca[w2], NEG), wcb[w2]);
+        carry = xc;
     }
+    __syncthreads();                               // bitmap complete
+    best = rdl(scan_max(best), 63);
+    int32_t* wmx = wca + 2 * NW;
+    if (lane == 0) wmx[wv] = best;
+    __syncthreads();
+    for (int w2 = 0; w2 < NW; ++w2) best = max(best, wmx[w2]);
+    if (pq && tid == 0) { const uint64_t t_ = wall_clock64(); pq[16] += t_ - t_lb0; }
     // segment starts: thread t takes bitmap words [t * wpt, t * wpt + wpt)
     const uint32_t wpt = (nwd + NT - 1) / NT;
     const uint32_t wa0 = min(nwd, (uint32_t)tid * wpt), wb0 = min(nwd, wa0 + wpt);
@@ -1409,10 +1440,26 @@ DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, const uint64_t* O, uint32
     if (a.lb_mode != 3) visit([&](uint32_t, uint32_t) { ++mine; });
     if (a.lb_mode == 3) mine = 0xffff;   // EXPERIMENT
     uint32_t tot;
-    uint32_t o = block_excl_sum<NW>(mine, tot, s_sc);
+    (void)block_excl_sum<NW>(mine, tot, s_sc);
     const uint32_t budget = A / 32u + 8u;
-    if (tot <= budget && mine) visit([&](uint32_t sk, uint32_t e) { Kc[o++] = sk | ((e - sk) << 16); });
-    if (tid == 0) { a.fmin[r] = best; a.ncand[r] = tot <= budget ? tot : NC_STREAM_LB; }
+    // long candidates (the usual one or two per read) go straight to pass 0's long-segment queue
+    // (k_chain_long, as k_chain_seg's route() would send them: production sends every segment over
+    // CHAIN_TINY anchors to a wave); k_chain_seg gets only the tiny ones as work items
+    uint32_t ntiny = 0;
+    if (tot <= budget) {                           // block-uniform: block_excl_sum holds barriers
+        uint32_t nt = 0;
+        if (mine) visit([&](uint32_t sk, uint32_t e) { if (e - sk <= (uint32_t)CHAIN_TINY || !a.lseg) ++nt; });
+        uint32_t ot = block_excl_sum<NW>(nt, ntiny, s_sc);
+        if (mine) visit([&](uint32_t sk, uint32_t e) {
+            if (e - sk <= (uint32_t)CHAIN_TINY || !a.lseg) Kc[ot++] = sk | ((e - sk) << 16);
+            else {
+                const uint32_t qq = atomicAdd(a.lseg_n, 1u);
+                if (qq < a.lseg_cap) a.lseg[qq] = make_uint4(r, sk, e, 0u);
+            }
+        });
+    }
+    if (tid == 0) { a.fmin[r] = best; a.ncand[r] = tot <= budget ? ntiny : NC_STREAM_LB; }
+    if (pq && tid == 0) { pq[17] += wall_clock64() - t_lb0; pq[18] = tot; }
 }
 
 // GL: the group offsets stay in HBM (2 n_seq + 2 > GOFF_LDS).  A template
@@ -1440,7 +1487,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
     const int tid = threadIdx.x, lane = lane_id();
     // MM2G_KNOB_SORT_PROF: per-phase wall-clock sums of thread 0 (after barriers),
     // accumulated in the read's 16 profile words (no registers held across the kernel)
-    uint64_t* const pq = a.prof ? a.prof + (uint64_t)r * 16 : nullptr;
+    uint64_t* const pq = a.prof ? a.prof + (uint64_t)r * 24 : nullptr;
     if (pq && tid == 0) pq[10] = pq[12] = wall_clock64();
 #define SORT_PH(k) do { if (pq && tid == 0) { const uint64_t t_ = wall_clock64(); pq[k] += t_ - pq[12]; pq[12] = t_; } } while (0)
 #define SORT_END(nb, nk) do { if (pq && tid == 0) { pq[8] = A0; pq[9] = ((uint64_t)(nb) << 32) | (nk); pq[11] = wall_clock64(); } } while (0)
@@ -1726,7 +1773,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
             if (a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
                 __syncthreads();                   // O complete (rank phase, P4b) and visible to the block
                 if (a.lb_mode == 2) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); __syncthreads(); }
-                else sort_lb_cands<NT>(a, r, O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc);
+                else sort_lb_cands<NT>(a, r, O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc, pq);
                 SORT_PH(3);
             }
             SORT_END(nbig, A);
@@ -1903,7 +1950,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
         const uint32_t A0 = (uint32_t)(a.a_off[r + 1] - base);
         uint64_t* K = a.keys + base;
         uint64_t* O = a.tmp + base;
-        uint64_t* const pq = a.prof ? a.prof + (uint64_t)r * 16 : nullptr;
+        uint64_t* const pq = a.prof ? a.prof + (uint64_t)r * 24 : nullptr;
         if (pq && tid == 0) pq[10] = pq[12] = wall_clock64();
 #define BIG_PH(k) do { if (pq && tid == 0) { const uint64_t t_ = wall_clock64(); pq[k] += t_ - pq[12]; pq[12] = t_; } } while (0)
         // ---- P1: seen / seen-twice bitmaps (staged: all cells, then all atomics)
@@ -2264,6 +2311,11 @@ __global__ __launch_bounds__(1024) void k_seg_items(ChainArgs a) {
         uint32_t pre = 0, tot = 0;
         for (int w = 0; w < 16; ++w) { pre += w < wv ? sc[w] : 0u; tot += sc[w]; }
         if (t < a.n) a.item_off[t] = carry + pre + ex;
+        // item -> position in order, so the streaming kernels need no search over item_off
+        if (a.item_read && t < a.n) {
+            const uint32_t o = carry + pre + ex;
+            for (uint32_t j = 0; j < c && o + j < a.item_cap; ++j) a.item_read[o + j] = t;
+        }
         carry += tot;
         __syncthreads();
     }
@@ -2314,7 +2366,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     const uint32_t nwaves = gridDim.x * DP_NW;
     const uint32_t n_items = (uint32_t)uni((int32_t)a.item_off[a.n]);
     for (uint32_t it = blockIdx.x * DP_NW + wv; it < n_items; it += nwaves) {
-        const uint32_t t = (uint32_t)uni((int32_t)item_owner(a.item_off, a.n, it));
+        const uint32_t t = (uint32_t)uni((int32_t)((a.item_read && it < a.item_cap) ? a.item_read[it] : item_owner(a.item_off, a.n, it)));
         const uint32_t r = (uint32_t)uni((int32_t)a.order[t]);
         const uint32_t j = it - (uint32_t)uni((int32_t)a.item_off[t]);
         const uint64_t t_start = wall_clock64();
@@ -2522,7 +2574,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
     const uint32_t n_items = (uint32_t)uni((int32_t)a.item_off[a.n]);
     for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + wave_id(); it < n_items; it += nwaves) {
-        const uint32_t t = (uint32_t)uni((int32_t)item_owner(a.item_off, a.n, it));
+        const uint32_t t = (uint32_t)uni((int32_t)((a.item_read && it < a.item_cap) ? a.item_read[it] : item_owner(a.item_off, a.n, it)));
         const uint32_t r = (uint32_t)uni((int32_t)a.order[t]);
         if (a.ncand && (uint32_t)uni((int32_t)a.ncand[r]) != NC_STREAM) continue;   // the sort set fmin[r] (a larger bound)
         const int32_t c0 = (int32_t)(it - (uint32_t)uni((int32_t)a.item_off[t])) * (int32_t)a.seg_chunk;
