@@ -304,7 +304,8 @@ enum {
                                     one wave each; 0 = one wave per read [2560]                             */
     MM2G_KNOB_MW_MIN = 28,       /* pass-0 segments of at least this many anchors (rounded up to a power of two)
                                     take an 8-wave workgroup each (k_chain_long_mw); 0 = off [0]             */
-    MM2G_KNOB_COUNT = 29
+    MM2G_KNOB_PRUNE_RESCUE = 29, /* the rescue pass prunes segments by pass 0's best-f lower bound [1]         */
+    MM2G_KNOB_COUNT = 30
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

@@ -102,6 +102,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SORT_LB: return 1;
     case MM2G_KNOB_SKETCH_VIEW: return 2560;
     case MM2G_KNOB_MW_MIN: return 0;
+    case MM2G_KNOB_PRUNE_RESCUE: return 1;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -939,8 +940,10 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         }
         // lower bound of each read's best f: prunes segments (pass 0, not in debug
         // mode; the rescue pass runs on few reads, where it costs more than it saves)
-        ca.fmin = pass == 0 ? fmin_buf : nullptr;
-        if (ca.fmin) {
+        // the rescue pass prunes by pass 0's bound: every pass-0 transition is accepted at bw_long
+        // with the same score, so its best f >= LB_1 >= LB_0 = fmin (no k_chain_lb of its own)
+        ca.fmin = (pass == 0 || K[MM2G_KNOB_PRUNE_RESCUE]) ? fmin_buf : nullptr;
+        if (ca.fmin && pass == 0) {
             if (!sort_fmin) HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
             ProfScope ps(c, "chain_lb");
             LCHK(launch_chain_stage(5, ca, 2048, c->stream));

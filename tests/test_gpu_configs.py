@@ -140,28 +140,32 @@ def test_c5_hg38_100kb(hg38, tmp_path):
         a, b = seqs[i], seqs[8 + i]
         seqs.append(a[:50000] + b[50000:])
         rn.append(f"chim{i}")
-    res, rec = _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5")
-    assert rec[:, 1].max() > 65535
-    rescued = [r for r in range(len(seqs)) if res[r].flags & 2]
-    assert len(rescued) >= 4
-    for r in rescued:
-        want, _ = oi.anchors(seqs[r], 10, 15, mid)
-        want = want[_singleton_keep(want)]
-        got = dev.debug_anchors(r)
-        assert np.array_equal(got, want), r
-        f, pp, _, _, _ = O.chain_dp(want, 15, bw=20000)
-        gf, gpp = dev.debug_dp(r)
-        n = len(want)
-        assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
-    # pass 0's 100 kb chains through k_chain_long_mw (one 8-wave workgroup per segment of >= 4096 anchors)
-    with knobs(dev, mw_min=4096):
-        _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5mw")
-    with knobs(dev, giant_lcap=64):
-        res2, _ = _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5hbm")
+    # the rescue pass's full DP arrays (its segment pruning off) against chain_dp_all at bw_long
+    with knobs(dev, prune_rescue=0):
+        res, rec = _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5")
+        assert rec[:, 1].max() > 65535
+        rescued = [r for r in range(len(seqs)) if res[r].flags & 2]
+        assert len(rescued) >= 4
         for r in rescued:
             want, _ = oi.anchors(seqs[r], 10, 15, mid)
             want = want[_singleton_keep(want)]
+            got = dev.debug_anchors(r)
+            assert np.array_equal(got, want), r
             f, pp, _, _, _ = O.chain_dp(want, 15, bw=20000)
             gf, gpp = dev.debug_dp(r)
             n = len(want)
             assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
+        with knobs(dev, giant_lcap=64):
+            _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5hbm")
+            for r in rescued:
+                want, _ = oi.anchors(seqs[r], 10, 15, mid)
+                want = want[_singleton_keep(want)]
+                f, pp, _, _, _ = O.chain_dp(want, 15, bw=20000)
+                gf, gpp = dev.debug_dp(r)
+                n = len(want)
+                assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
+    # production defaults (the rescue pass pruned by pass 0's bound): PAF and per-read outcome
+    _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5prune")
+    # pass 0's 100 kb chains through k_chain_long_mw (one 8-wave workgroup per segment of >= 4096 anchors)
+    with knobs(dev, mw_min=4096):
+        _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5mw")
