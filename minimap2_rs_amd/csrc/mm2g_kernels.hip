@@ -878,6 +878,10 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
 //   one 1024-thread workgroup per read, stable ranking by wave match.
 // ============================================================================
 constexpr int SORT_SMALL = 4096;
+constexpr int SMALL_LB_LUT = 1024;        // k_sort_small's LB pass: pen LUT entries it keeps in static LDS
+template <int NT, typename KP>
+DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint32_t A, unsigned char* lds,
+                        uint32_t* w4, uint32_t* s_sc, uint64_t* pq);
 
 __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) { *a.rcount = 0; if (a.rwork) *a.rwork = 0; }   // k_sort_read's list for k_sort_radix / k_sort_big
@@ -913,6 +917,13 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
         }
     }
     for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) a.tmp[CK(base + i, a.cap_keys)] = s[i];   // sorted keys live in tmp
+    // pass-0 LB and candidate segments from the sorted keys in LDS (as k_sort_read; the unsorted
+    // keys in HBM are dead now and receive the candidate list)
+    if (a.lut && a.fmin && a.ncand && a.P.lut_n <= SMALL_LB_LUT) {
+        __shared__ __align__(16) unsigned char s_lb[SMALL_LB_LUT * 2 + SORT_SMALL / 8];
+        __shared__ uint32_t s_w4[32], s_sc4[16];
+        sort_lb_cands<256>(a, r, (const uint64_t*)s, (uint32_t*)(K + base), A, s_lb, s_w4, s_sc4, nullptr);
+    }
 }
 
 // ---- per-read sort of the large reads (A0 > small_max): cell buckets.
@@ -1313,8 +1324,8 @@ DEVI void scan_lb(int32_t& a, int32_t& b) {
 // then streams the read: many one-segment items would cost more).  fmin[r] =
 // max LB either way.  LDS: the pen LUT, then ceil(A / 64) u64 bitmap words;
 // w4: 5 NW words of static LDS.
-template <int NT>
-DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, const uint64_t* O, uint32_t* Kc, uint32_t A, unsigned char* lds,
+template <int NT, typename KP>
+DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint32_t A, unsigned char* lds,
                         uint32_t* w4, uint32_t* s_sc, uint64_t* pq) {
     constexpr int NW = NT / 64;
     constexpr int32_t NEG = -(1 << 29);
@@ -1773,7 +1784,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
             if (a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
                 __syncthreads();                   // O complete (rank phase, P4b) and visible to the block
                 if (a.lb_mode == 2) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); __syncthreads(); }
-                else sort_lb_cands<NT>(a, r, O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc, pq);
+                else sort_lb_cands<NT>(a, r, (const uint64_t*)O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc, pq);
                 SORT_PH(3);
             }
             SORT_END(nbig, A);
