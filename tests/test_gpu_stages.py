@@ -86,6 +86,19 @@ def test_workspace_exact_fallback(small_world, dense_world):
         d.close()
 
 
+@pytest.mark.parametrize("kn", [dict(sort_lb=0), dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1),
+                                dict(mw_min=64), dict(sort_small=1, mw_min=128, sketch_view=300)])
+def test_round4_paths_vs_oracle(dev, small_world, dense_world, kn):
+    """Every round-4 production path, on and off, against the oracle (PAF and
+    per-read outcome, small and dense worlds at mid_occ 20 and 5000): the sort's
+    LB pass and candidate segments (sort_lb; sort_small=1 sends every read
+    through k_sort_read's, else most of these reads take k_sort_small's),
+    the rescue pass's pruning by pass 0's bound, query sketch views, and
+    k_chain_long_mw for pass 0's long segments."""
+    with knobs(dev, **kn):
+        _production_vs_oracle(dev, small_world, dense_world, tag=str(kn))
+
+
 @pytest.mark.parametrize("max_gap,bw_long", [(5000, 40000), (40000, 20000)])
 def test_wide_gaps_vs_oracle(dev, small_world, dense_world, max_gap, bw_long):
     """max_dist_x beyond the sort's 32 kb cells (-g 40000, -r 500,40000): the
