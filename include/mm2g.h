@@ -330,9 +330,11 @@ int mm2g_prof_reset(mm2g_ctx* ctx);
  * [2]=kept minimizers [3]=anchors [4]=rescued anchors [5]=dp pair evaluations
  * [6]=anchors entering the DP (after the sort's singleton filter); anchors in
  * the DP's long segments below the giant-kernel size [7] / from it on [8] and
- * in its medium segments [9] of pass 0, and [10], [11], [12] of the rescue pass.
+ * in its medium segments [9] of pass 0, and [10], [11], [12] of the rescue pass;
+ * DP anchors in reads that k_chain_seg streams (no candidate list from the
+ * sort) [13] and that k_chain_lb runs on (no lower bound from the sort) [14].
  * Copies min(n, MM2G_N_COUNTERS) values; returns how many. */
-#define MM2G_N_COUNTERS 13
+#define MM2G_N_COUNTERS 15
 int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus

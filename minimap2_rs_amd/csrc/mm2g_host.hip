@@ -71,7 +71,8 @@ static int ensure(DevBuf& b, size_t n, T** out) {
 struct ProfSlot { std::string name; double ms = 0; int64_t calls = 0; };
 // Batch status block (u64 words, device + pinned copy): [0] BS_* bits | dv
 // overflow, [1] filter-table entries, [2] anchors, [3] minimizers, [4] anchors
-// in the DP, [8 + 3 pass ..] anchors in long (< / >= giant_min) and medium
+// in the DP, [5] / [6] of them in reads k_chain_seg streams / k_chain_lb runs
+// on, [8 + 3 pass ..] anchors in long (< / >= giant_min) and medium
 // segments of each DP pass (k_lseg_order)
 constexpr int STAT_WORDS = 16;
 
@@ -1277,7 +1278,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         ProfScope ps(c, "dv");
         if (stop_at != 4) LCHK(launch_dv(da, c->stream));
     }
-    LCHK(launch_batch_sums(n, mz_cnt, cnt2, st, c->stream));
+    LCHK(launch_batch_sums(n, mz_cnt, cnt2, ncand, st, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_out, out, (size_t)n * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_stat, st, STAT_WORDS * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipEventRecord(c->ev_done, c->stream));
@@ -1369,6 +1370,8 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     for (int t = 0; t < 6; ++t) c->counters[t] = cnt[t];
     c->counters[6] = c->h_stat[4];    // anchors left after the sort's singleton filter (the DP input)
     for (int t = 0; t < 6; ++t) c->counters[7 + t] = c->h_stat[8 + t];   // anchors per chain kernel class and pass
+    c->counters[13] = c->h_stat[5];   // DP anchors in reads k_chain_seg streams (no candidate list from the sort)
+    c->counters[14] = c->h_stat[6];   // ... in reads k_chain_lb runs on (no LB from the sort)
     return 0;
 }
 

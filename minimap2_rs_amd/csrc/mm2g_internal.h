@@ -271,7 +271,7 @@ int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k, uint64_t cap, uint32_t* status,
                      uint32_t bit, int slot, hipStream_t st);
 // per-batch sums for the counters: status64[3] = sum mz_cnt, status64[4] = sum cnt2
-int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st);
+int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, const uint32_t* ncand, unsigned long long* status64, hipStream_t st);
 // minimizer slots: read r gets [rd_off[r] + 16r, rd_off[r+1] + 16(r+1)), or `slot` entries each when non-zero (tests)
 int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st);
 // query sketch views: per-read view counts; view table from their exclusive scan vo; per-read concatenation

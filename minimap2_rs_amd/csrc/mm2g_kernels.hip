@@ -4148,17 +4148,23 @@ __global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t
 }
 
 // per-batch sums for mm2g_batch_counters (st[3] = minimizers, st[4] = anchors in the DP)
-__global__ __launch_bounds__(1024) void k_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* st) {
-    __shared__ unsigned long long ws[2][16];
-    unsigned long long a = 0, b = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += 1024) { a += mz_cnt[i]; b += cnt2 ? cnt2[i] : 0u; }
-    a = wave_sum64(a); b = wave_sum64(b);
-    if (lane_id() == 0) { ws[0][threadIdx.x >> 6] = a; ws[1][threadIdx.x >> 6] = b; }
+__global__ __launch_bounds__(1024) void k_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, const uint32_t* ncand,
+                                                    unsigned long long* st) {
+    // st[3] minimizers, st[4] anchors in the DP, st[5] of them in reads k_chain_seg streams
+    // (no candidate list), st[6] in reads k_chain_lb runs on (no LB from the sort)
+    __shared__ unsigned long long ws[4][16];
+    unsigned long long v[4] = {0, 0, 0, 0};
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) {
+        const uint32_t c2 = cnt2 ? cnt2[i] : 0u, nc = ncand ? ncand[i] : NC_STREAM;
+        v[0] += mz_cnt[i]; v[1] += c2; v[2] += nc >= NC_STREAM_LB ? c2 : 0u; v[3] += nc == NC_STREAM ? c2 : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[k] = wave_sum64(v[k]); if (lane_id() == 0) ws[k][threadIdx.x >> 6] = v[k]; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long x = 0, y = 0;
-        for (int t = 0; t < 16; ++t) { x += ws[0][t]; y += ws[1][t]; }
-        st[3] = x; st[4] = y;
+    if (threadIdx.x < 4) {
+        unsigned long long x = 0;
+        for (int t = 0; t < 16; ++t) x += ws[threadIdx.x][t];
+        st[3 + threadIdx.x] = x;
     }
 }
 
@@ -4404,8 +4410,8 @@ int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, in
     LAUNCH_CHECK();
     return 0;
 }
-int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st) {
-    hipLaunchKernelGGL(k_batch_sums, dim3(1), dim3(1024), 0, st, n, mz_cnt, cnt2, status64);
+int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, const uint32_t* ncand, unsigned long long* status64, hipStream_t st) {
+    hipLaunchKernelGGL(k_batch_sums, dim3(1), dim3(1024), 0, st, n, mz_cnt, cnt2, ncand, status64);
     LAUNCH_CHECK();
     return 0;
 }
