@@ -875,7 +875,8 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     ENSURE(c->order, uint32_t, n, order);
     int32_t* tmark;
     ENSURE(c->tmark, int32_t, A_cap, tmark);
-    const uint32_t lcap = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_MED + 1) + 64, 0xffffffffu);
+    // every segment over CHAIN_TINY anchors may take a wave (med_pairs 0), and they are disjoint
+    const uint32_t lcap = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_TINY + 1) + 64, 0xffffffffu);
     uint4* lseg; uint32_t *lseg_n, *lseg_order; unsigned long long* rbest;
     ENSURE(c->lseg, uint4, lcap, lseg);
     ENSURE(c->lseg_order, uint32_t, lcap, lseg_order);
@@ -1223,7 +1224,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     }
     // the long-segment queue: the sort's LB pass appends pass 0's long candidate segments to it
     uint4* lseg_q = nullptr; uint32_t* lseg_nq = nullptr;
-    const uint32_t lcap_q = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_MED + 1) + 64, 0xffffffffu);
+    const uint32_t lcap_q = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_TINY + 1) + 64, 0xffffffffu);
     if (lut_sort) {
         uint32_t* lo_;
         ENSURE(c->lseg, uint4, lcap_q, lseg_q); ENSURE(c->lseg_order, uint32_t, lcap_q, lo_); ENSURE(c->lseg_n, uint32_t, 4, lseg_nq);
@@ -1237,7 +1238,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.rlist = rlist; so.rcount = rlist + n; so.rwork = rlist + n + 1;
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
-    so.ncand = ncand; so.fmin = fmin_buf; so.lut = lut_sort; so.P = P; so.lb_mode = (uint32_t)K[MM2G_KNOB_SORT_LB];
+    so.ncand = ncand; so.fmin = fmin_buf; so.lut = lut_sort; so.P = P;
     so.lseg = lseg_q; so.lseg_n = lseg_nq; so.lseg_cap = lcap_q;
     uint64_t* sprof = nullptr;
     if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 192)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 192, c->stream)); so.prof = sprof; }

@@ -179,7 +179,6 @@ struct SortArgs {
     // (dead) unsorted-key region; ncand: their count, or NC_STREAM / NC_STREAM_LB
     uint32_t* ncand = nullptr;         // per read (k_sort_small initialises every read to NC_STREAM)
     int32_t* fmin = nullptr;           // null: no LB / candidates (debug mode, pruning off)
-    uint32_t lb_mode = 1;              // EXPERIMENT: 2 = only drain stores + barrier, 3 = LB without candidates
     const int16_t* lut = nullptr;      // comput_sc pen LUT of pass 0 (lut_n entries)
     ChainKParams P{};                  // pass-0 chain parameters (max_dist_x/y, bw, span, lut_n)
     uint4* lseg = nullptr;             // pass 0's long-segment queue (ChainArgs::lseg): candidates of more than

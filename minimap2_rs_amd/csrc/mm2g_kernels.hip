@@ -1318,8 +1318,8 @@ DEVI void scan_lb(int32_t& a, int32_t& b) {
 //   best f or a tie of it (k_chain_seg's pruning rule, with the same bound).
 // The isolated anchors form a bitmap in LDS; each thread takes a run of its
 // words, finds the next start after its last one by a block suffix-min, and
-// the candidates go out as u16 start | u16 len << 16 to Kc (the read's own
-// unsorted-key region, dead now) in position order, with their count in
+// the candidates go out as u32 pairs (start, len) to Kc (the read's own
+// unsorted-key region, dead now: <= A segments, 2 words each) in position order, with their count in
 // ncand[r] -- or NC_STREAM_LB when there are more than `budget` (k_chain_seg
 // then streams the read: many one-segment items would cost more).  fmin[r] =
 // max LB either way.  LDS: the pen LUT, then ceil(A / 64) u64 bitmap words;
@@ -1448,8 +1448,7 @@ DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint3
         }
     };
     uint32_t mine = 0;
-    if (a.lb_mode != 3) visit([&](uint32_t, uint32_t) { ++mine; });
-    if (a.lb_mode == 3) mine = 0xffff;   // EXPERIMENT
+    visit([&](uint32_t, uint32_t) { ++mine; });
     uint32_t tot;
     (void)block_excl_sum<NW>(mine, tot, s_sc);
     const uint32_t budget = A / 32u + 8u;
@@ -1462,7 +1461,7 @@ DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint3
         if (mine) visit([&](uint32_t sk, uint32_t e) { if (e - sk <= (uint32_t)CHAIN_TINY || !a.lseg) ++nt; });
         uint32_t ot = block_excl_sum<NW>(nt, ntiny, s_sc);
         if (mine) visit([&](uint32_t sk, uint32_t e) {
-            if (e - sk <= (uint32_t)CHAIN_TINY || !a.lseg) Kc[ot++] = sk | ((e - sk) << 16);
+            if (e - sk <= (uint32_t)CHAIN_TINY || !a.lseg) { Kc[2 * ot] = sk; Kc[2 * ot + 1] = e - sk; ++ot; }
             else {
                 const uint32_t qq = atomicAdd(a.lseg_n, 1u);
                 if (qq < a.lseg_cap) a.lseg[qq] = make_uint4(r, sk, e, 0u);
@@ -1783,8 +1782,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
             // pass-0 LB and candidate segments (k_chain_lb / k_chain_seg's scan, fused)
             if (a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
                 __syncthreads();                   // O complete (rank phase, P4b) and visible to the block
-                if (a.lb_mode == 2) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); __syncthreads(); }
-                else sort_lb_cands<NT>(a, r, (const uint64_t*)O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc, pq);
+                sort_lb_cands<NT>(a, r, (const uint64_t*)O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc, pq);
                 SORT_PH(3);
             }
             SORT_END(nbig, A);
@@ -1932,6 +1930,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
     __shared__ uint32_t s_sc[16], s_read, s_nbig;
     __shared__ uint2 s_big[BIG_MAX];
     __shared__ uint32_t s_goff[GOFF_LDS];
+    __shared__ uint32_t s_w4[5 * 16];              // sort_lb_cands' wave words (s_goff stays live across reads)
     extern __shared__ uint64_t dyn64[];
     uint32_t* dyn = (uint32_t*)dyn64;
     const int tid = threadIdx.x, lane = lane_id();
@@ -2179,6 +2178,11 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
             BIG_PH(6);
             ba = bb;
         }
+        // pass-0 LB and candidate segments, as k_sort_read (K, radix_big's scratch, is dead now)
+        if (a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
+            __syncthreads();
+            sort_lb_cands<1024>(a, r, (const uint64_t*)O, (uint32_t*)K, A, (unsigned char*)dyn64, s_w4, s_sc, pq);
+        }
         if (pq && tid == 0) { pq[8] = A0; pq[9] = (0xfffeULL << 32) | A; pq[11] = wall_clock64(); }
 #undef BIG_PH
     }
@@ -2390,8 +2394,8 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
             // one candidate segment [s, s + len) of the sort (sort_lb_cands), in the
             // read's dead unsorted-key region (now a.chain's): streamed as if it
             // were the whole read, so exactly it is routed
-            const uint32_t cv = (uint32_t)uni((int32_t)a.chain[2 * base + j]);
-            c0 = (int32_t)(cv & 0xffffu); A = c0 + (int32_t)(cv >> 16); c1 = A;
+            c0 = uni((int32_t)a.chain[2 * base + 2 * j]);
+            A = c0 + uni((int32_t)a.chain[2 * base + 2 * j + 1]); c1 = A;
         } else {
             c0 = (int32_t)j * (int32_t)a.seg_chunk;
             A = (int32_t)uni((int32_t)a.cnt2[r]);      // anchors kept by the singleton filter
