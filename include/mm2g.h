@@ -100,7 +100,8 @@ void mm2g_ctx_destroy(mm2g_ctx* ctx);
 int mm2g_ctx_upload_index(mm2g_ctx* ctx, const mm2g_index* idx, int32_t mid_occ);
 /* The same for n contexts (normally one per GPU: `mm2rs align --devices`):
  * the host layout is built once and the devices' copies are made in parallel
- * host threads. */
+ * host threads.  All or nothing: on an error no context changes its index
+ * (each keeps the one it had). */
 int mm2g_ctx_upload_index_many(mm2g_ctx* const* ctxs, int n, const mm2g_index* idx, int32_t mid_occ);
 /* Use the device index of `src` (same device) in `dst` without another copy:
  * several contexts — one per host thread, each with its own stream and batch

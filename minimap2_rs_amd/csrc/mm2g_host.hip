@@ -476,17 +476,22 @@ static int flatten_index(const mm2g_index* idx, FlatIndex& F) {
     return 0;
 }
 
-static int upload_flat(mm2g_ctx* c, const HostIndex& H, const FlatIndex& F, int32_t mid_occ) {
+// The device copy is built into a staged DevIndex; the context switches to it
+// (commit_flat) only once it is complete, so a failed upload leaves the context
+// on its previous index.
+struct StagedIndex { std::shared_ptr<mm2g_ctx::DevIndex> dix; uint32_t l2 = 0; };
+
+static int stage_flat(mm2g_ctx* c, const HostIndex& H, const FlatIndex& F, StagedIndex& S) {
     HIPCHK(hipSetDevice(c->device));
     const uint64_t nk = F.keys.size();
     uint32_t l2 = 1;
     while ((1ULL << l2) < 2 * std::max<uint64_t>(nk, 1)) ++l2;     // load factor <= 0.5
     if (l2 > 31) return set_err(MM2G_E_UNSUP, "index too large for the device table");
-    c->mapped = false;
     IxEntry* tab; uint64_t* dpos;
-    c->dix = std::make_shared<mm2g_ctx::DevIndex>();    // a fresh copy (contexts sharing the old one keep it)
-    ENSURE(c->dix->tab, IxEntry, (size_t)1 << l2, tab);
-    ENSURE(c->dix->ix_pos, uint64_t, F.pos.size(), dpos);
+    S.dix = std::make_shared<mm2g_ctx::DevIndex>();     // a fresh copy (contexts sharing the old one keep it)
+    S.l2 = l2;
+    ENSURE(S.dix->tab, IxEntry, (size_t)1 << l2, tab);
+    ENSURE(S.dix->ix_pos, uint64_t, F.pos.size(), dpos);
     HIPCHK(hipMemsetAsync(tab, 0xff, sizeof(IxEntry) << l2, c->stream));
     if (!F.pos.empty()) HIPCHK(hipMemcpyAsync(dpos, F.pos.data(), F.pos.size() * 8, hipMemcpyHostToDevice, c->stream));
     DevBuf dk, doff, dn;
@@ -511,28 +516,37 @@ static int upload_flat(mm2g_ctx* c, const HostIndex& H, const FlatIndex& F, int3
         run += ((uint64_t)H.max_len >> CELL_SHIFT) + 3;
         goff[2 * H.n_seq + 1] = (uint32_t)std::min<uint64_t>(run, 0xffffffffu);
         // two bitmaps must fit the LDS budget of k_sort_read next to its static arrays
-        c->dix->cells = (run <= (uint64_t)MAX_CELLS) ? (uint32_t)run : 0u;
+        S.dix->cells = (run <= (uint64_t)MAX_CELLS) ? (uint32_t)run : 0u;
         uint32_t* dg;
-        ENSURE(c->dix->goff, uint32_t, goff.size(), dg);
+        ENSURE(S.dix->goff, uint32_t, goff.size(), dg);
         HIPCHK(hipMemcpyAsync(dg, goff.data(), goff.size() * 4, hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
-    c->log2cap = l2;
+    return 0;
+}
+
+static void commit_flat(mm2g_ctx* c, const HostIndex& H, StagedIndex& S, int32_t mid_occ) {
+    c->mapped = false;
+    c->dix = std::move(S.dix);
+    c->log2cap = S.l2;
     c->hidx = &H;
     c->mid_occ = mid_occ;
     c->have_index = true;
-    return 0;
 }
 
 int mm2g_ctx_upload_index(mm2g_ctx* c, const mm2g_index* idx, int32_t mid_occ) {
     if (!c || !idx) return set_err(MM2G_E_ARG, "null argument");
     FlatIndex F;
     if (int e = flatten_index(idx, F)) return e;
-    return upload_flat(c, idx->h, F, mid_occ);
+    StagedIndex S;
+    if (int e = stage_flat(c, idx->h, F, S)) return e;
+    commit_flat(c, idx->h, S, mid_occ);
+    return 0;
 }
 
 // One flatten, then every context's copy (normally one per GPU) in its own
-// host thread: the H2D copies and table builds of the devices overlap.
+// host thread: the H2D copies and table builds of the devices overlap.  All or
+// nothing: the contexts switch to the new index only when every copy is done.
 int mm2g_ctx_upload_index_many(mm2g_ctx* const* ctxs, int n, const mm2g_index* idx, int32_t mid_occ) {
     if (!ctxs || n < 0 || !idx) return set_err(MM2G_E_ARG, "null argument");
     for (int i = 0; i < n; ++i) if (!ctxs[i]) return set_err(MM2G_E_ARG, "null context %d", i);
@@ -540,12 +554,14 @@ int mm2g_ctx_upload_index_many(mm2g_ctx* const* ctxs, int n, const mm2g_index* i
     if (int e = flatten_index(idx, F)) return e;
     std::vector<int> rc(n, 0);
     std::vector<std::string> msg(n);
+    std::vector<StagedIndex> S(n);
     std::vector<std::thread> th;
     for (int i = 0; i < n; ++i)
-        th.emplace_back([&, i] { rc[i] = upload_flat(ctxs[i], idx->h, F, mid_occ); if (rc[i]) msg[i] = g_err; });
+        th.emplace_back([&, i] { rc[i] = stage_flat(ctxs[i], idx->h, F, S[i]); if (rc[i]) msg[i] = g_err; });
     for (auto& t : th) t.join();
     for (int i = 0; i < n; ++i)
         if (rc[i]) return set_err(rc[i], "device %d: %s", ctxs[i]->device, msg[i].c_str());
+    for (int i = 0; i < n; ++i) commit_flat(ctxs[i], idx->h, S[i], mid_occ);
     return 0;
 }
 
