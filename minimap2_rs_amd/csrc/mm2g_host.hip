@@ -484,7 +484,7 @@ struct StagedIndex { std::shared_ptr<mm2g_ctx::DevIndex> dix; uint32_t l2 = 0; }
 static int stage_flat(mm2g_ctx* c, const HostIndex& H, const FlatIndex& F, StagedIndex& S) {
     HIPCHK(hipSetDevice(c->device));
     const uint64_t nk = F.keys.size();
-    uint32_t l2 = 1;
+    uint32_t l2 = 2;                                               // >= one 4-slot probe group (k_seed_count)
     while ((1ULL << l2) < 2 * std::max<uint64_t>(nk, 1)) ++l2;     // load factor <= 0.5
     if (l2 > 31) return set_err(MM2G_E_UNSUP, "index too large for the device table");
     IxEntry* tab; uint64_t* dpos;

@@ -743,7 +743,7 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
         int kn = 1;                        // next seed_write part boundary
         // SC_U chunks of 64 minimizers at a time: their table probes are
         // independent, so SC_U loads per lane are in flight together
-        constexpr int SC_U = 4;
+        constexpr int SC_U = 2;
         for (uint32_t b0 = 0; b0 < m; b0 += 64 * SC_U) {
             uint64_t h[SC_U];
             uint32_t sl[SC_U], n[SC_U], off[SC_U];
@@ -757,16 +757,31 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
                 h[u] = act ? (a.mz_x[mb + i] >> 8) : 0;
                 sl[u] = ix_slot(h[u], a.log2cap); n[u] = 0; off[u] = 0;
             }
-            while (any(!(done[0] && done[1] && done[2] && done[3]))) {
-                IxEntry e[SC_U];
+            // linear probing, read a 64-B group of 4 slots at a time (one request,
+            // all four loads in flight): at load <= 0.5 the first group nearly
+            // always ends the probe, where slot-by-slot took ~1.5 dependent loads
+            for (;;) {
+                bool all = true;
 #pragma unroll
-                for (int u = 0; u < SC_U; ++u) if (!done[u]) e[u] = a.tab[sl[u]];
+                for (int u = 0; u < SC_U; ++u) all = all && done[u];
+                if (!any(!all)) break;
+                IxEntry e[SC_U][4];
+#pragma unroll
+                for (int u = 0; u < SC_U; ++u)
+                    if (!done[u]) {
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) e[u][g] = a.tab[(sl[u] & ~3u) + (uint32_t)g];
+                    }
 #pragma unroll
                 for (int u = 0; u < SC_U; ++u) {
                     if (done[u]) continue;
-                    if (e[u].key == h[u]) { off[u] = e[u].off; n[u] = e[u].n; done[u] = true; }
-                    else if (e[u].key == U64MAX) done[u] = true;
-                    else sl[u] = (sl[u] + 1) & cmask;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        if (done[u] || g < (int)(sl[u] & 3u)) continue;
+                        if (e[u][g].key == h[u]) { off[u] = e[u][g].off; n[u] = e[u][g].n; done[u] = true; }
+                        else if (e[u][g].key == U64MAX) done[u] = true;
+                    }
+                    sl[u] = ((sl[u] & ~3u) + 4u) & cmask;
                 }
             }
 #pragma unroll
@@ -1479,6 +1494,7 @@ DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint3
 template <bool GL, int NT>
 __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
     constexpr int NW = NT / 64;
+    constexpr int RK_KPT = (SORT_LDS / 8 + NT - 1) / NT < 20 ? (SORT_LDS / 8 + NT - 1) / NT : 20;   // window keys per thread
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t red[32];
     __shared__ uint32_t s_sc[16], s_kept, s_nbig;
@@ -1572,7 +1588,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
         // top 16 bits, which the key layout must leave free.
         const uint32_t cofs = LW >= cw + 2 ? (LW - cw) & ~1u : 0u;
         const uint32_t kbits = gsh + (32u - (uint32_t)__builtin_clz(2u * a.n_seq | 1u));
-        const uint32_t W = cofs >> 1;                        // keys per window
+        const uint32_t W = min(cofs >> 1, (uint32_t)(RK_KPT * NT));   // keys per window (the rank phase holds RK_KPT per thread)
         if (kbits > 48u || qb + CELL_SHIFT > 32u || cofs < 2 * nw || W < SEG_RANK) { defer(); return; }
         {
             constexpr uint64_t kmask = (1ULL << 48) - 1;
@@ -1704,43 +1720,63 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 // B: ranks inside the segments.  Keys of one segment share every bit
                 // above the cell-local lb <= 32 (rank, group, cell), so they compare
                 // by their low dwords.
+                // Each thread keeps its keys and their destinations in registers (a
+                // shift register: constant indices, no scratch); after a barrier they
+                // are permuted in place in S and leave for O in whole lines -- scattered
+                // 8-B stores to O cost one request per key in the TA.
                 const uint32_t* S32 = (const uint32_t*)S;
                 uint32_t pc_tiny = 0, pc_long = 0, pc_srch = 0;     // MM2G_KNOB_SORT_PROF segment classes
-                for (uint32_t i = tid; i < nwin; i += NT) {
-                    const uint64_t x = S[i];
-                    uint32_t s, e;
-                    seg_of(x, s, e);
-                    const uint32_t L = e - s;
-                    if (L > a.seg_small) {             // P4b; copied unsorted
-                        O[oa + i] = x & kmask;
-                        if (i == s) {
-                            const uint32_t slot = atomicAdd(&s_nbig, 1u);
-                            if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s, oa + e);
+                uint64_t xk[RK_KPT];
+                uint32_t pk[RK_KPT];
+                for (int u = 0; u < RK_KPT; ++u) {
+                    const uint32_t i = (uint32_t)tid + (uint32_t)u * NT;
+                    uint64_t xo = 0;
+                    uint32_t po = 0;
+                    if (i < nwin) {
+                        const uint64_t x = S[i];
+                        uint32_t s, e;
+                        seg_of(x, s, e);
+                        const uint32_t L = e - s;
+                        xo = x & kmask;
+                        if (L > a.seg_small) {             // P4b; stays unsorted
+                            po = i;
+                            if (i == s) {
+                                const uint32_t slot = atomicAdd(&s_nbig, 1u);
+                                if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s, oa + e);
+                            }
+                        } else {
+                            const uint32_t xl = (uint32_t)x;
+                            uint32_t rank = 0;
+                            if (pq) {
+                                if (L <= SEG_TINY) ++pc_tiny;
+                                else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
+                            }
+                            if (L <= SEG_TINY) {
+                                for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
+                            } else {
+                                const uint32_t co = i >> 6;
+                                rank = i - max(s, co << 6);
+                                for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
+                                    if (c == co) continue;
+                                    rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
+                                }
+                            }
+                            po = s + rank;
                         }
-                        continue;
                     }
-                    const uint32_t xl = (uint32_t)x;
-                    uint32_t rank = 0;
-                    if (pq) {
-                        if (L <= SEG_TINY) ++pc_tiny;
-                        else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
-                    }
-                    if (L <= SEG_TINY) {
-                        for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
-                    } else {
-                        const uint32_t co = i >> 6;
-                        rank = i - max(s, co << 6);
-                        for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
-                            if (c == co) continue;
-                            rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
-                        }
-                    }
-                    O[oa + s + rank] = x & kmask;
+#pragma unroll
+                    for (int v = 0; v + 1 < RK_KPT; ++v) { xk[v] = xk[v + 1]; pk[v] = pk[v + 1]; }
+                    xk[RK_KPT - 1] = xo; pk[RK_KPT - 1] = po;
                 }
                 if (pq) {
                     const uint64_t v14 = wave_sum64(((uint64_t)pc_long << 32) | pc_tiny), v15 = wave_sum64(pc_srch);
                     if (lane == 0) { atomicAdd((unsigned long long*)&pq[14], (unsigned long long)v14); atomicAdd((unsigned long long*)&pq[15], (unsigned long long)v15); }
                 }
+                __syncthreads();                   // every compare has read S
+#pragma unroll
+                for (int u = 0; u < RK_KPT; ++u) if ((uint32_t)tid + (uint32_t)u * NT < nwin) S[pk[u]] = xk[u];
+                __syncthreads();
+                for (uint32_t i = tid; i < nwin; i += NT) O[oa + i] = S[i];
                 __syncthreads();
                 SORT_PH(5);
                 ra = rb;
