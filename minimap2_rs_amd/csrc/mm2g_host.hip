@@ -880,7 +880,8 @@ static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_
 static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const ChainKParams& P0, float gap, int npass, int32_t mdx1,
                      int32_t mdy1, int32_t bw_long, uint64_t A_cap, const uint64_t* a_off, const uint32_t* a_cnt, uint64_t* keys,
                      uint64_t* ktmp, const uint32_t* cnt2, const uint64_t* smax, ReadOut* out, const uint32_t* abort, bool full,
-                     unsigned long long* stat = nullptr, const uint32_t* ncand = nullptr, int32_t* sort_fmin = nullptr) {
+                     unsigned long long* stat = nullptr, const uint32_t* ncand = nullptr, int32_t* sort_fmin = nullptr,
+                     bool sort_lq = false) {
     int32_t *fb, *pb;
     ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
     int16_t* lut; uint32_t* work;
@@ -947,7 +948,8 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         HIPCHK(hipMemsetAsync(rbest, 0, (size_t)n * 8, c->stream));
         // long count (pass 0/1 slot), medium count, medium taken; pass 0's long count may hold the
         // sort's candidate segments already (zeroed before the sort, sort_lb_cands)
-        if (pass == 0 && sort_fmin) HIPCHK(hipMemsetAsync(lseg_n + 2, 0, 8, c->stream));
+        // (only when the sort ran its LB pass: with sort_lb off a stale count would replay another batch's segments)
+        if (pass == 0 && sort_lq) HIPCHK(hipMemsetAsync(lseg_n + 2, 0, 8, c->stream));
         else HIPCHK(hipMemsetAsync(lseg_n + pass, 0, 16 - 4 * (size_t)pass, c->stream));
         static const char* names[2][5] = {{"chain_seg", "chain_med", "chain_lorder", "chain_long", "chain_fin"},
                                           {"chain_seg_rescue", "chain_med_rescue", "chain_lorder_rescue", "chain_long_rescue", "chain_fin_rescue"}};
@@ -1279,7 +1281,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     if (chain) {
         // 5. chain DP + fallback + rescue
         if (int e = run_chain(c, n, c->d_rd_off, P, gap, npass, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
-                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug, st, ncand, fmin_buf))
+                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug, st, ncand, fmin_buf, lut_sort != nullptr))
             return e;
         // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
         const bool sep = (H.w != o->w || H.k != o->k);

@@ -514,14 +514,333 @@ struct DpResult { std::vector<std::vector<size_t>> chains; std::vector<int32_t> 
 
 static void sort_chains_stable(const std::vector<Anchor>& anchors, std::vector<std::vector<size_t>>& chains, std::vector<int32_t>& scores);
 
-// Tie order of Rust's sort_unstable_by_key (lchain.rs:97 z by f, :267 / :292
-// merge items by qs): unspecified by Rust and not restated here.  0: std::sort;
-// 1 / 2: stable, equal keys in ascending / descending input order -- the two
-// extremes, for measuring which outputs depend on it (orc_set_tie_order).
-static int g_tie_order = 0;
+// ----------------------------------------------------------- Rust sort_unstable
+// `slice::sort_unstable_by_key` (lchain.rs:97 z by f, :267 / :292 merge items by
+// qs) leaves the order of equal keys to the std algorithm, which changed in
+// rustc 1.81.  Both are restated here from rust-lang/rust library/core (no Rust
+// toolchain in this image: unpinned, DESIGN.md §2 "-n <= 1"); the element type
+// is the reference's `(i32, usize)` (16 B, Copy) with is_less = key a < key b.
+//   ipnsort   (1.81+): core/src/slice/sort/unstable/{mod,quicksort,heapsort}.rs,
+//                      shared/pivot.rs, shared/smallsort.rs
+//   pdqsort (<= 1.80): core/src/slice/sort.rs (quicksort / recurse)
+namespace rsort {
+template <typename E, typename L>
+static void insert_tail(E* v, size_t i, L& lt) {   // v[..i] sorted; insert v[i] (stable)
+    if (!lt(v[i], v[i - 1])) return;
+    E tmp = v[i];
+    size_t j = i;
+    do { v[j] = v[j - 1]; --j; } while (j > 0 && lt(tmp, v[j - 1]));
+    v[j] = tmp;
+}
+template <typename E, typename L>
+static void insertion_sort_shift_left(E* v, size_t len, size_t offset, L& lt) {
+    for (size_t i = offset; i < len; ++i) insert_tail(v, i, lt);
+}
+template <typename E, typename L>
+static void insert_head(E* v, size_t len, L& lt) {   // v[1..] sorted; insert v[0] (insertion_sort_shift_right, offset 1)
+    if (len < 2 || !lt(v[1], v[0])) return;
+    E tmp = v[0];
+    size_t i = 1;
+    v[0] = v[1];
+    while (i + 1 < len && lt(v[i + 1], tmp)) { v[i] = v[i + 1]; ++i; }
+    v[i] = tmp;
+}
+// heapsort: 1.81's single loop and the older build-then-pop loops perform the
+// same sift-downs in the same order
+template <typename E, typename L>
+static void sift_down(E* v, size_t len, size_t node, L& lt) {
+    for (;;) {
+        size_t child = 2 * node + 1;
+        if (child >= len) break;
+        if (child + 1 < len) child += lt(v[child], v[child + 1]) ? 1 : 0;
+        if (!lt(v[node], v[child])) break;
+        std::swap(v[node], v[child]);
+        node = child;
+    }
+}
+template <typename E, typename L>
+static void heapsort(E* v, size_t len, L& lt) {
+    for (size_t i = len + len / 2; i-- > 0;) {
+        size_t sift_idx;
+        if (i >= len) sift_idx = i - len;
+        else { std::swap(v[0], v[i]); sift_idx = 0; }
+        sift_down(v, std::min(i, len), sift_idx, lt);
+    }
+}
+
+// ---- ipnsort (1.81+)
+// small_sort_general (smallsort.rs): sort8_stable / sort4_stable presorting, insert_tail and
+// bidirectional_merge are all stable, so for a strict weak order it is a stable sort of the slice.
+template <typename E, typename L>
+static void small_sort_general(E* v, size_t len, L& lt) {
+    std::stable_sort(v, v + len, [&](const E& a, const E& b) { return lt(a, b); });
+}
+template <typename E, typename L>
+static size_t median3(const E* v, size_t a, size_t b, size_t c, L& lt) {   // pivot.rs median3
+    const bool x = lt(v[a], v[b]), y = lt(v[a], v[c]);
+    if (x == y) { const bool z = lt(v[b], v[c]); return (z ^ x) ? c : b; }
+    return a;
+}
+template <typename E, typename L>
+static size_t median3_rec(const E* v, size_t a, size_t b, size_t c, size_t n, L& lt) {
+    if (n * 8 >= 64) {
+        const size_t n8 = n / 8;
+        a = median3_rec(v, a, a + n8 * 4, a + n8 * 7, n8, lt);
+        b = median3_rec(v, b, b + n8 * 4, b + n8 * 7, n8, lt);
+        c = median3_rec(v, c, c + n8 * 4, c + n8 * 7, n8, lt);
+    }
+    return median3(v, a, b, c, lt);
+}
+template <typename E, typename L>
+static size_t choose_pivot_ipn(const E* v, size_t len, L& lt) {   // pivot.rs choose_pivot (len >= 8)
+    const size_t d8 = len / 8, a = 0, b = d8 * 4, c = d8 * 7;
+    return len < 64 ? median3(v, a, b, c, lt) : median3_rec(v, a, b, c, d8, lt);
+}
+// partition_lomuto_branchless_cyclic (quicksort.rs; sizeof(T) <= 96), on w = v[1..]
+template <typename E, typename P>
+static size_t lomuto_cyclic(E* w, size_t n, const E& pivot, P& lt) {
+    if (n == 0) return 0;
+    E tmp = w[0];
+    size_t gap = 0, num_lt = 0;
+    for (size_t right = 1; right <= n; ++right) {
+        const E rv = right < n ? w[right] : tmp;   // the last step takes the saved first element
+        const bool is_lt = lt(rv, pivot);
+        w[gap] = w[num_lt];
+        w[num_lt] = rv;
+        gap = right;                               // (after the last step the gap is the temporary)
+        num_lt += is_lt ? 1 : 0;
+    }
+    return num_lt;
+}
+template <typename E, typename P>
+static size_t partition_ipn(E* v, size_t len, size_t pivot, P& lt) {
+    std::swap(v[0], v[pivot]);
+    const E pv = v[0];
+    const size_t num_lt = lomuto_cyclic(v + 1, len - 1, pv, lt);
+    std::swap(v[0], v[num_lt]);
+    return num_lt;
+}
+template <typename E, typename L>
+static void quicksort_ipn(E* v, size_t len, const E* ancestor, uint32_t limit, L& lt) {
+    E anc_val{};
+    bool has_anc = ancestor != nullptr;
+    if (has_anc) anc_val = *ancestor;
+    for (;;) {
+        if (len <= 32) { small_sort_general(v, len, lt); return; }   // SMALL_SORT_GENERAL_THRESHOLD (16-B Copy type)
+        if (limit == 0) { heapsort(v, len, lt); return; }
+        limit -= 1;
+        const size_t pp = choose_pivot_ipn(v, len, lt);
+        if (has_anc && !lt(anc_val, v[pp])) {
+            auto le = [&](const E& a, const E& b) { return !lt(b, a); };
+            const size_t num_le = partition_ipn(v, len, pp, le);
+            v += num_le + 1; len -= num_le + 1;
+            has_anc = false;
+            continue;
+        }
+        const size_t num_lt = partition_ipn(v, len, pp, lt);
+        quicksort_ipn(v, num_lt, has_anc ? &anc_val : nullptr, limit, lt);
+        anc_val = v[num_lt]; has_anc = true;
+        v += num_lt + 1; len -= num_lt + 1;
+    }
+}
+template <typename E, typename L>
+static void ipnsort(E* v, size_t len, L lt) {   // unstable/mod.rs sort + ipnsort
+    if (len < 2) return;
+    if (len <= 20) { insertion_sort_shift_left(v, len, 1, lt); return; }
+    size_t run = 2;                                 // find_existing_run
+    const bool desc = lt(v[1], v[0]);
+    if (desc) while (run < len && lt(v[run], v[run - 1])) ++run;
+    else while (run < len && !lt(v[run], v[run - 1])) ++run;
+    if (run == len) { if (desc) std::reverse(v, v + len); return; }
+    uint32_t lg = 0;
+    for (size_t x = len | 1; x > 1; x >>= 1) ++lg;
+    quicksort_ipn(v, len, (const E*)nullptr, 2 * lg, lt);
+}
+
+// ---- pdqsort (<= 1.80)
+template <typename E>
+static void break_patterns(E* v, size_t len) {
+    if (len < 8) return;
+    uint64_t seed = (uint64_t)len;
+    auto gen = [&]() { uint64_t r = seed; r ^= r << 13; r ^= r >> 7; r ^= r << 17; seed = r; return r; };
+    size_t modulus = 1;
+    while (modulus < len) modulus <<= 1;           // next_power_of_two
+    const size_t pos = len / 4 * 2;
+    for (size_t i = 0; i < 3; ++i) {
+        size_t other = (size_t)(gen() & (modulus - 1));
+        if (other >= len) other -= len;
+        std::swap(v[pos - 1 + i], v[other]);
+    }
+}
+template <typename E, typename L>
+static size_t choose_pivot_pdq(E* v, size_t len, L& lt, bool& likely_sorted) {
+    size_t a = len / 4 * 1, b = len / 4 * 2, c = len / 4 * 3;
+    size_t swaps = 0;
+    if (len >= 8) {
+        auto sort2 = [&](size_t& x, size_t& y) { if (lt(v[y], v[x])) { std::swap(x, y); ++swaps; } };
+        auto sort3 = [&](size_t& x, size_t& y, size_t& z) { sort2(x, y); sort2(y, z); sort2(x, y); };
+        if (len >= 50) {
+            auto adj = [&](size_t& x) { size_t lo = x - 1, hi = x + 1; sort3(lo, x, hi); };
+            adj(a); adj(b); adj(c);
+        }
+        sort3(a, b, c);
+    }
+    if (swaps < 12) { likely_sorted = swaps == 0; return b; }
+    std::reverse(v, v + len);
+    likely_sorted = true;
+    return len - 1 - b;
+}
+template <typename E, typename L>
+static bool partial_insertion_sort(E* v, size_t len, L& lt) {
+    size_t i = 1;
+    for (int step = 0; step < 5; ++step) {
+        while (i < len && !lt(v[i], v[i - 1])) ++i;
+        if (i == len) return true;
+        if (len < 50) return false;
+        std::swap(v[i - 1], v[i]);
+        if (i >= 2) {
+            insertion_sort_shift_left(v, i, i - 1, lt);   // the smaller element to the left
+            insert_head(v + i, len - i, lt);             // the greater element to the right
+        }
+    }
+    return false;
+}
+template <typename E, typename L>
+static size_t partition_in_blocks(E* v, size_t n, const E& pivot, L& lt) {
+    constexpr size_t BLOCK = 128;
+    size_t l = 0, r = n;                           // element indices into v
+    size_t block_l = BLOCK, block_r = BLOCK;
+    uint8_t offs_l[BLOCK], offs_r[BLOCK];
+    size_t sl = 0, el = 0, sr = 0, er = 0;         // start/end into offs_*
+    for (;;) {
+        const bool is_done = r - l <= 2 * BLOCK;
+        if (is_done) {
+            size_t rem = r - l;
+            if (sl < el || sr < er) rem -= BLOCK;
+            if (sl < el) block_r = rem;
+            else if (sr < er) block_l = rem;
+            else { block_l = rem / 2; block_r = rem - block_l; }
+        }
+        if (sl == el) {
+            sl = el = 0;
+            for (size_t i = 0; i < block_l; ++i) { offs_l[el] = (uint8_t)i; el += !lt(v[l + i], pivot) ? 1 : 0; }
+        }
+        if (sr == er) {
+            sr = er = 0;
+            for (size_t i = 0; i < block_r; ++i) { offs_r[er] = (uint8_t)i; er += lt(v[r - 1 - i], pivot) ? 1 : 0; }
+        }
+        const size_t count = std::min(el - sl, er - sr);
+        if (count > 0) {                           // cyclic permutation
+            auto L_ = [&]() -> E& { return v[l + offs_l[sl]]; };
+            auto R_ = [&]() -> E& { return v[r - 1 - offs_r[sr]]; };
+            E tmp = L_();
+            L_() = R_();
+            for (size_t c = 1; c < count; ++c) {
+                ++sl; R_() = L_();
+                ++sr; L_() = R_();
+            }
+            R_() = tmp;
+            ++sl; ++sr;
+        }
+        if (sl == el) l += block_l;
+        if (sr == er) r -= block_r;
+        if (is_done) break;
+    }
+    if (sl < el) {
+        while (sl < el) { --el; std::swap(v[l + offs_l[el]], v[r - 1]); --r; }
+        return r;
+    } else if (sr < er) {
+        while (sr < er) { --er; std::swap(v[l], v[r - 1 - offs_r[er]]); ++l; }
+        return l;
+    }
+    return l;
+}
+template <typename E, typename L>
+static size_t partition_pdq(E* v, size_t len, size_t pivot, L& lt, bool& was_partitioned) {
+    std::swap(v[0], v[pivot]);
+    const E pv = v[0];
+    E* w = v + 1;
+    const size_t n = len - 1;
+    size_t l = 0, r = n;
+    while (l < r && lt(w[l], pv)) ++l;
+    while (l < r && !lt(w[r - 1], pv)) --r;
+    was_partitioned = l >= r;
+    const size_t mid = l + partition_in_blocks(w + l, r - l, pv, lt);
+    std::swap(v[0], v[mid]);
+    return mid;
+}
+template <typename E, typename L>
+static size_t partition_equal(E* v, size_t len, size_t pivot, L& lt) {
+    std::swap(v[0], v[pivot]);
+    const E pv = v[0];
+    E* w = v + 1;
+    const size_t n = len - 1;
+    if (n == 0) return 0;
+    size_t l = 0, r = n;
+    for (;;) {
+        while (l < r && !lt(pv, w[l])) ++l;
+        while (l < r && lt(pv, w[r - 1])) --r;
+        if (l >= r) break;
+        --r;
+        std::swap(w[l], w[r]);
+        ++l;
+    }
+    return l + 1;
+}
+template <typename E, typename L>
+static void pdq_recurse(E* v, size_t len, L& lt, const E* pred, uint32_t limit) {
+    E pred_val{};
+    bool has_pred = pred != nullptr;
+    if (has_pred) pred_val = *pred;
+    bool was_balanced = true, was_partitioned = true;
+    for (;;) {
+        if (len <= 20) { if (len >= 2) insertion_sort_shift_left(v, len, 1, lt); return; }
+        if (limit == 0) { heapsort(v, len, lt); return; }
+        if (!was_balanced) { break_patterns(v, len); limit -= 1; }
+        bool likely_sorted = false;
+        const size_t pivot = choose_pivot_pdq(v, len, lt, likely_sorted);
+        if (was_balanced && was_partitioned && likely_sorted)
+            if (partial_insertion_sort(v, len, lt)) return;
+        if (has_pred && !lt(pred_val, v[pivot])) {
+            const size_t mid = partition_equal(v, len, pivot, lt);
+            v += mid; len -= mid;
+            continue;
+        }
+        bool was_p = false;
+        const size_t mid = partition_pdq(v, len, pivot, lt, was_p);
+        was_balanced = std::min(mid, len - mid) >= len / 8;
+        was_partitioned = was_p;
+        const size_t nl = mid, nr = len - mid - 1;
+        if (nl < nr) {
+            pdq_recurse(v, nl, lt, has_pred ? &pred_val : nullptr, limit);
+            pred_val = v[mid]; has_pred = true;
+            v += mid + 1; len = nr;
+        } else {
+            const E pv = v[mid];
+            pdq_recurse(v + mid + 1, nr, lt, &pv, limit);
+            len = nl;
+        }
+    }
+}
+template <typename E, typename L>
+static void pdqsort(E* v, size_t len, L lt) {
+    uint32_t limit = 0;
+    for (size_t x = len; x; x >>= 1) ++limit;      // usize::BITS - leading_zeros
+    pdq_recurse(v, len, lt, (const E*)nullptr, limit);
+}
+}  // namespace rsort
+
+// Tie order of sort_unstable_by_key (orc_set_tie_order): 3 = ipnsort (rustc
+// 1.81+, the default, matching the rustc >= 1.82 assumed for binary_search),
+// 4 = pdqsort (rustc 1.78-1.80; Cargo.lock v4 needs >= 1.78); 0 = std::sort,
+// 1 / 2 = stable with equal keys in ascending / descending input order (the
+// two extremes, for measuring which outputs depend on the order).
+static int g_tie_order = 3;
 template <typename T>
 static void sort_unstable_by_first(std::vector<std::pair<int32_t, T>>& v) {
     auto lt = [](const std::pair<int32_t, T>& a, const std::pair<int32_t, T>& b) { return a.first < b.first; };
+    if (g_tie_order == 3) { rsort::ipnsort(v.data(), v.size(), lt); return; }
+    if (g_tie_order == 4) { rsort::pdqsort(v.data(), v.size(), lt); return; }
     if (g_tie_order == 0) { std::sort(v.begin(), v.end(), lt); return; }
     if (g_tie_order == 2) std::reverse(v.begin(), v.end());
     std::stable_sort(v.begin(), v.end(), lt);
@@ -940,8 +1259,20 @@ static void align_one(const Index& idx, int32_t mid_occ, const AlignOpts& o, con
     DpResult resc = rescue_long_join(anchors, all, p, (int32_t)qlen, &rescued, rc ? &cs : nullptr);
     if (rr && rescued) rr->flags |= 2;
     if (rc) { rc->rescued += rescued ? anchors.size() : 0; rc->inner_iters += cs.inner_iters; }
+    // merge_adjacent_chains_with_gap unwraps last()/first() of the chains it meets after the first
+    // (lchain.rs:297-298): an empty chain (only min_cnt <= 0 lets one through) among two or more panics
+    if (resc.chains.size() >= 2) {
+        for (const auto& ch : resc.chains)
+            if (ch.empty()) {
+                if (!g_quiet) fprintf(stderr, "oracle: read %s: reference panics (unwrap on an empty chain)\n", qname.c_str());
+                if (rc) rc->panics += 1;
+                if (rr) rr->flags |= 8;
+                return;
+            }
+    }
     std::vector<std::vector<size_t>> merged = merge_adjacent_chains_with_gap(anchors, resc.chains, p.max_dist_y, p.max_dist_y);
     std::vector<std::vector<size_t>> chains; int32_t s1, s2;
+    const size_t lines0 = lines.size();
     select_and_filter_chains(anchors, merged, resc.scores, o.mask_level, o.pri_ratio, o.best_n, chains, s1, s2);
     for (size_t ci = 0; ci < chains.size(); ++ci) {   // paf.rs:238-248
         PafRecord rec;
@@ -958,10 +1289,13 @@ static void align_one(const Index& idx, int32_t mid_occ, const AlignOpts& o, con
             lines.push_back(write_paf(rec));
             if (rc) rc->lines += 1;
         } else if (rec.panic) {
-            // The reference aborts the whole process here; per-read concatenation
+            // The reference aborts the whole process here, before it prints any
+            // of the read's lines (main.rs:218-226); per-read concatenation
             // semantics: this read yields no line (and is counted).
             if (!g_quiet) fprintf(stderr, "oracle: read %s: reference panics (index out of bounds: rid 2147483647)\n", qname.c_str());
-            if (rc) rc->panics += 1;
+            if (rc) { rc->panics += 1; rc->lines -= (u64)(lines.size() - lines0); }
+            if (rr) rr->flags |= 8;
+            lines.resize(lines0);
             break;
         }
     }
@@ -1119,6 +1453,16 @@ void orc_set_quiet(int q) { g_quiet = q != 0; }
 // paf.rs:178's binary_search as rustc 1.52-1.81 (1) or >= 1.82 (0, default) compiles it
 void orc_set_binary_search(int pre182) { g_binsearch_pre182 = pre182 != 0; }
 void orc_set_tie_order(int mode) { g_tie_order = mode; }
+// Rust's sort_unstable_by_key on (keys[i], i) pairs under tie order `mode`; the indices in output order.
+void orc_rust_sort(const int32_t* keys, uint64_t n, int mode, uint64_t* perm) {
+    std::vector<std::pair<int32_t, size_t>> v(n);
+    for (uint64_t i = 0; i < n; ++i) v[i] = {keys[i], (size_t)i};
+    const int keep = g_tie_order;
+    g_tie_order = mode;
+    sort_unstable_by_first(v);
+    g_tie_order = keep;
+    for (uint64_t i = 0; i < n; ++i) perm[i] = v[i].second;
+}
 // the two algorithms on a caller array (tests): returns found, *idx = Ok / Err index
 int orc_binary_search(const int32_t* v, uint64_t n, int32_t target, int pre182, uint64_t* idx) {
     std::vector<int32_t> a(v, v + n);

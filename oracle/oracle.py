@@ -66,6 +66,7 @@ def lib() -> C.CDLL:
         L.orc_set_quiet.argtypes = [C.c_int]
         L.orc_set_binary_search.argtypes = [C.c_int]
         L.orc_set_tie_order.argtypes = [C.c_int]
+        L.orc_rust_sort.argtypes = [C.POINTER(C.c_int32), C.c_uint64, C.c_int, _P64]
         L.orc_binary_search.restype = C.c_int
         L.orc_binary_search.argtypes = [C.POINTER(C.c_int32), C.c_uint64, C.c_int32, C.c_int, _P64]
         L.orc_align_records.restype = C.c_longlong
@@ -243,10 +244,22 @@ def set_binary_search(pre182: bool) -> None:
     lib().orc_set_binary_search(1 if pre182 else 0)
 
 
+TIE_IPNSORT, TIE_PDQSORT = 3, 4
+
+
 def set_tie_order(mode: int) -> None:
-    """Tie order of the reference's two sort_unstable_by_key calls (lchain.rs:97, :292): 0 std::sort, 1 / 2
-    stable with equal keys in ascending / descending input order (the extremes, for exposure counts)."""
+    """Tie order of the reference's two sort_unstable_by_key calls (lchain.rs:97, :292): 3 rustc 1.81+
+    ipnsort (the default), 4 rustc 1.78-1.80 pdqsort, 0 std::sort, 1 / 2 stable with equal keys in
+    ascending / descending input order (the extremes, for exposure counts)."""
     lib().orc_set_tie_order(int(mode))
+
+
+def rust_sort_perm(keys, mode: int = TIE_IPNSORT):
+    """Order of indices after Rust's sort_unstable_by_key on (keys[i], i) (tie order `mode`)."""
+    k = np.ascontiguousarray(np.asarray(keys, dtype=np.int32))
+    out = np.zeros(len(k), dtype=np.uint64)
+    lib().orc_rust_sort(k.ctypes.data_as(C.POINTER(C.c_int32)), len(k), int(mode), out.ctypes.data_as(_P64))
+    return out
 
 
 def binary_search(v, target: int, pre182: bool = False):

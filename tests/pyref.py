@@ -420,3 +420,338 @@ def align_one(index, qname, q, mid_occ, w=10, k=15):
         chain, score = fallback_chain(f, pprev, v)
     line, panic = paf_line(index, anchors, chain, qname, q, score)
     return line, panic, rescued
+
+
+# ---------------------------------------------------------------- Rust sort_unstable
+# Second restatement (the oracle's is C++, rsort:: in oracle/mm2rs_oracle.cpp) of
+# `slice::sort_unstable_by_key` as rustc compiles lchain.rs:97 / :267 / :292, on a
+# list of (key, payload) with is_less = key(a) < key(b).  Written against
+# rust-lang/rust library/core: ipnsort (1.81+) sort/unstable/{mod,quicksort,
+# heapsort}.rs + sort/shared/{pivot,smallsort}.rs; pdqsort (<= 1.80) slice/sort.rs.
+
+def _lt(a, b):
+    return a[0] < b[0]
+
+
+def _insertion_left(v, lo, hi, offset, lt):  # insertion_sort_shift_left(v[lo:hi], offset)
+    for i in range(lo + offset, hi):
+        tmp = v[i]
+        if lt(tmp, v[i - 1]):
+            j = i
+            while True:
+                v[j] = v[j - 1]
+                j -= 1
+                if j == lo or not lt(tmp, v[j - 1]):
+                    break
+            v[j] = tmp
+
+
+def _heapsort(v, lo, hi, lt):  # unstable/heapsort.rs (same sift order as the <= 1.80 heapsort)
+    n = hi - lo
+
+    def sift(end, node):
+        while True:
+            child = 2 * node + 1
+            if child >= end:
+                return
+            if child + 1 < end and lt(v[lo + child], v[lo + child + 1]):
+                child += 1
+            if not lt(v[lo + node], v[lo + child]):
+                return
+            v[lo + node], v[lo + child] = v[lo + child], v[lo + node]
+            node = child
+
+    for i in range(n + n // 2 - 1, -1, -1):
+        if i >= n:
+            sift(n, i - n)
+        else:
+            v[lo], v[lo + i] = v[lo + i], v[lo]
+            sift(i, 0)
+
+
+def _small_sort_general(v, lo, hi, lt):
+    # sort8_stable/sort4_stable + insert_tail + bidirectional_merge: a stable sort
+    v[lo:hi] = sorted(v[lo:hi], key=lambda e: e[0])
+
+
+def _median3(v, a, b, c, lt):
+    x = lt(v[a], v[b])
+    y = lt(v[a], v[c])
+    if x == y:
+        z = lt(v[b], v[c])
+        return c if (z != x) else b
+    return a
+
+
+def _median3_rec(v, a, b, c, n, lt):
+    if n * 8 >= 64:
+        n8 = n // 8
+        a = _median3_rec(v, a, a + n8 * 4, a + n8 * 7, n8, lt)
+        b = _median3_rec(v, b, b + n8 * 4, b + n8 * 7, n8, lt)
+        c = _median3_rec(v, c, c + n8 * 4, c + n8 * 7, n8, lt)
+    return _median3(v, a, b, c, lt)
+
+
+def _partition_lomuto(v, lo, hi, piv, lt):
+    """partition(): pivot to the front, partition_lomuto_branchless_cyclic on the rest, pivot to num_lt."""
+    v[lo], v[piv] = v[piv], v[lo]
+    p = v[lo]
+    base, n = lo + 1, hi - lo - 1
+    num_lt = 0
+    if n:
+        gap_val = v[base]
+        gap = base
+        srcs = list(range(base + 1, base + n)) + [None]
+        for s in srcs:
+            rv = gap_val if s is None else v[s]
+            is_lt = lt(rv, p)
+            v[gap] = v[base + num_lt]
+            v[base + num_lt] = rv
+            gap = s
+            num_lt += 1 if is_lt else 0
+    v[lo], v[lo + num_lt] = v[lo + num_lt], v[lo]
+    return num_lt
+
+
+def _quicksort_ipn(v, lo, hi, anc, limit, lt):
+    while True:
+        n = hi - lo
+        if n <= 32:
+            _small_sort_general(v, lo, hi, lt)
+            return
+        if limit == 0:
+            _heapsort(v, lo, hi, lt)
+            return
+        limit -= 1
+        d8 = n // 8
+        if n < 64:
+            pp = _median3(v, lo, lo + d8 * 4, lo + d8 * 7, lt)
+        else:
+            pp = _median3_rec(v, lo, lo + d8 * 4, lo + d8 * 7, d8, lt)
+        if anc is not None and not lt(anc, v[pp]):
+            num = _partition_lomuto(v, lo, hi, pp, lambda a, b: not lt(b, a))
+            lo += num + 1
+            anc = None
+            continue
+        num = _partition_lomuto(v, lo, hi, pp, lt)
+        _quicksort_ipn(v, lo, lo + num, anc, limit, lt)
+        anc = v[lo + num]
+        lo += num + 1
+
+
+def rust_sort_unstable_ipn(v, lt=_lt):
+    """rustc 1.81+ sort_unstable_by (in place)."""
+    n = len(v)
+    if n < 2:
+        return v
+    if n <= 20:
+        _insertion_left(v, 0, n, 1, lt)
+        return v
+    run = 2
+    desc = lt(v[1], v[0])
+    if desc:
+        while run < n and lt(v[run], v[run - 1]):
+            run += 1
+    else:
+        while run < n and not lt(v[run], v[run - 1]):
+            run += 1
+    if run == n:
+        if desc:
+            v.reverse()
+        return v
+    limit = 2 * ((n | 1).bit_length() - 1)
+    _quicksort_ipn(v, 0, n, None, limit, lt)
+    return v
+
+
+def _pdq_partition_in_blocks(v, lo, hi, p, lt):
+    BLOCK = 128
+    l, r = lo, hi
+    bl, br = BLOCK, BLOCK
+    offl, offr = [], []          # pending offsets (consumed from the front)
+    il = ir = 0
+    while True:
+        done = r - l <= 2 * BLOCK
+        if done:
+            rem = r - l
+            if il < len(offl) or ir < len(offr):
+                rem -= BLOCK
+            if il < len(offl):
+                br = rem
+            elif ir < len(offr):
+                bl = rem
+            else:
+                bl = rem // 2
+                br = rem - bl
+        if il == len(offl):
+            offl = [i for i in range(bl) if not lt(v[l + i], p)]
+            il = 0
+        if ir == len(offr):
+            offr = [i for i in range(br) if lt(v[r - 1 - i], p)]
+            ir = 0
+        cnt = min(len(offl) - il, len(offr) - ir)
+        if cnt:
+            L = lambda: l + offl[il]
+            R = lambda: r - 1 - offr[ir]
+            tmp = v[L()]
+            v[L()] = v[R()]
+            for _ in range(1, cnt):
+                il += 1
+                v[R()] = v[L()]
+                ir += 1
+                v[L()] = v[R()]
+            v[R()] = tmp
+            il += 1
+            ir += 1
+        if il == len(offl):
+            l += bl
+        if ir == len(offr):
+            r -= br
+        if done:
+            break
+    if il < len(offl):
+        end = len(offl)
+        while il < end:
+            end -= 1
+            a, b = l + offl[end], r - 1
+            v[a], v[b] = v[b], v[a]
+            r -= 1
+        return r - lo
+    if ir < len(offr):
+        end = len(offr)
+        while ir < end:
+            end -= 1
+            a, b = l, r - 1 - offr[end]
+            v[a], v[b] = v[b], v[a]
+            l += 1
+        return l - lo
+    return l - lo
+
+
+def _pdq_choose_pivot(v, lo, hi, lt):
+    n = hi - lo
+    idx = [n // 4, n // 4 * 2, n // 4 * 3]
+    swaps = [0]
+
+    def s2(i, j):
+        if lt(v[lo + idx[j]], v[lo + idx[i]]):
+            idx[i], idx[j] = idx[j], idx[i]
+            swaps[0] += 1
+
+    if n >= 8:
+        if n >= 50:
+            for t in range(3):
+                m = idx[t]
+                trip = [m - 1, m, m + 1]
+                for (i, j) in ((0, 1), (1, 2), (0, 1)):
+                    if lt(v[lo + trip[j]], v[lo + trip[i]]):
+                        trip[i], trip[j] = trip[j], trip[i]
+                        swaps[0] += 1
+                idx[t] = trip[1]
+        s2(0, 1)
+        s2(1, 2)
+        s2(0, 1)
+    if swaps[0] < 12:
+        return idx[1], swaps[0] == 0
+    v[lo:hi] = v[lo:hi][::-1]
+    return n - 1 - idx[1], True
+
+
+def _pdq_partial_insertion(v, lo, hi, lt):
+    n = hi - lo
+    i = 1
+    for _ in range(5):
+        while i < n and not lt(v[lo + i], v[lo + i - 1]):
+            i += 1
+        if i == n:
+            return True
+        if n < 50:
+            return False
+        v[lo + i - 1], v[lo + i] = v[lo + i], v[lo + i - 1]
+        if i >= 2:
+            _insertion_left(v, lo, lo + i, i - 1, lt)
+            # shift_head of v[i..]: v[i] moves right past smaller successors
+            j = lo + i
+            if j + 1 < hi and lt(v[j + 1], v[j]):
+                tmp = v[j]
+                while j + 1 < hi and lt(v[j + 1], tmp):
+                    v[j] = v[j + 1]
+                    j += 1
+                v[j] = tmp
+    return False
+
+
+def _pdq_recurse(v, lo, hi, pred, limit, lt):
+    balanced = partitioned = True
+    while True:
+        n = hi - lo
+        if n <= 20:
+            if n >= 2:
+                _insertion_left(v, lo, hi, 1, lt)
+            return
+        if limit == 0:
+            _heapsort(v, lo, hi, lt)
+            return
+        if not balanced:
+            if n >= 8:      # break_patterns: xorshift64 seeded with len
+                seed = n
+                mod = 1 << (n - 1).bit_length()
+                pos = n // 4 * 2
+                for i in range(3):
+                    r = seed
+                    r ^= (r << 13) & 0xFFFFFFFFFFFFFFFF
+                    r ^= r >> 7
+                    r ^= (r << 17) & 0xFFFFFFFFFFFFFFFF
+                    seed = r
+                    other = r & (mod - 1)
+                    if other >= n:
+                        other -= n
+                    a, b = lo + pos - 1 + i, lo + other
+                    v[a], v[b] = v[b], v[a]
+            limit -= 1
+        piv, likely = _pdq_choose_pivot(v, lo, hi, lt)
+        if balanced and partitioned and likely:
+            if _pdq_partial_insertion(v, lo, hi, lt):
+                return
+        pv = lo + piv
+        if pred is not None and not lt(pred, v[pv]):
+            v[lo], v[pv] = v[pv], v[lo]
+            p = v[lo]
+            l, r = lo + 1, hi
+            while True:
+                while l < r and not lt(p, v[l]):
+                    l += 1
+                while l < r and lt(p, v[r - 1]):
+                    r -= 1
+                if l >= r:
+                    break
+                r -= 1
+                v[l], v[r] = v[r], v[l]
+                l += 1
+            lo = l           # (l - (lo + 1)) + 1 elements equal to the pivot
+            continue
+        v[lo], v[pv] = v[pv], v[lo]
+        p = v[lo]
+        l, r = lo + 1, hi
+        while l < r and lt(v[l], p):
+            l += 1
+        while l < r and not lt(v[r - 1], p):
+            r -= 1
+        mid = (l - (lo + 1)) + _pdq_partition_in_blocks(v, l, r, p, lt)
+        was_p = l >= r
+        v[lo], v[lo + mid] = v[lo + mid], v[lo]
+        balanced = min(mid, n - mid) >= n // 8
+        partitioned = was_p
+        if mid < n - mid - 1:
+            _pdq_recurse(v, lo, lo + mid, pred, limit, lt)
+            pred = v[lo + mid]
+            lo = lo + mid + 1
+        else:
+            _pdq_recurse(v, lo + mid + 1, hi, v[lo + mid], limit, lt)
+            hi = lo + mid
+
+
+def rust_sort_unstable_pdq(v, lt=_lt):
+    """rustc <= 1.80 sort_unstable_by (pdqsort, in place)."""
+    _pdq_recurse(v, 0, len(v), None, len(v).bit_length(), lt)
+    return v

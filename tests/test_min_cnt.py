@@ -52,7 +52,7 @@ def test_min_cnt_le1_equals_default_when_m_above_span(world):
                     got = _paf(oi, reads, str(td / f"n{mc}_{m}_{mode}.paf"), min_cnt=mc, min_chain_score=m)
                     assert got == base, (mc, m, mode)
     finally:
-        O.set_tie_order(0)
+        O.set_tie_order(O.TIE_IPNSORT)
 
 
 def test_min_cnt_le1_low_m_depends_on_tie_order(world):
@@ -66,7 +66,7 @@ def test_min_cnt_le1_low_m_depends_on_tie_order(world):
             O.set_tie_order(mode)
             outs.append(_paf(oi, reads, str(td / f"low_m_{mode}.paf"), min_cnt=1, min_chain_score=15))
     finally:
-        O.set_tie_order(0)
+        O.set_tie_order(O.TIE_IPNSORT)
     by = [{} for _ in outs]
     for d, txt in zip(by, outs):
         for ln in txt.splitlines():
@@ -75,3 +75,32 @@ def test_min_cnt_le1_low_m_depends_on_tie_order(world):
     differ = sum(1 for q in names if by[0].get(q) != by[1].get(q))
     print(f"-n 1 -m 15: {differ} of {len(names)} reads' PAF depend on the sort_unstable tie order")
     assert differ > 0
+
+
+def _by_read(txt):
+    d = {}
+    for ln in txt.splitlines():
+        d.setdefault(ln.split("\t")[0], []).append(ln)
+    return d
+
+
+@pytest.mark.parametrize("m", [15, 0])
+def test_min_cnt_le1_ipnsort_vs_pdqsort(world, m):
+    """-n 1 -m <= k under the two restated rustc sorts (ipnsort, rustc 1.81+,
+    the default; pdqsort, rustc 1.78-1.80): how many reads' PAF depend on the
+    rustc version (reported; DESIGN.md §2 "-n <= 1")."""
+    ref, reads, td = world
+    oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+    outs = []
+    try:
+        for mode in (O.TIE_IPNSORT, O.TIE_PDQSORT):
+            O.set_tie_order(mode)
+            outs.append(_paf(oi, reads, str(td / f"rs_{m}_{mode}.paf"), min_cnt=1, min_chain_score=m))
+    finally:
+        O.set_tie_order(O.TIE_IPNSORT)
+    a, b = _by_read(outs[0]), _by_read(outs[1])
+    names = set(a) | set(b)
+    differ = sum(1 for q in names if a.get(q) != b.get(q))
+    lines = outs[0].count("\n")
+    print(f"-n 1 -m {m}: {differ} of {len(names)} reads' PAF differ between ipnsort and pdqsort ({lines} lines)")
+    assert lines > len(names)      # several chains per read: the multi-chain output is exercised
