@@ -201,6 +201,14 @@ int mm2g_batch_results(mm2g_ctx* ctx, mm2g_read_result* out, uint32_t n_reads);
 int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, const char* const* names, uint32_t n,
                         char* out, int64_t cap);
 
+/* PAF lines of the batch mm2g_batch_results collected last, for its first n
+ * reads in read order (names[r] = read r's name): write_paf_many_with_scores
+ * (src/paf.rs:238-248) of main.rs:209-218's chains -- one line per mapped read
+ * under -n >= 2 (the same text as mm2g_format_paf), several with tp:A:P/S and
+ * s2 under -n <= 1 -m <= k.  Reads on which the reference panics print nothing.
+ * Returns bytes written; out = NULL only sizes. */
+int64_t mm2g_batch_paf(mm2g_ctx* ctx, const char* const* names, uint32_t n, char* out, int64_t cap);
+
 /* ---------------------------------------------------------------- stages
  * Stage-level access for parity tests (each replaces one reference fn). */
 /* sketch_sequence(seq, w, k, rid, false, out) (src/sketch.rs:29-100) on the

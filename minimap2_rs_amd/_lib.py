@@ -98,6 +98,7 @@ SIGNATURES = {
     "mm2g_batch_map": (C.c_int, [_VP, C.POINTER(MapOpts)]),
     "mm2g_batch_results": (C.c_int, [_VP, C.POINTER(ReadResult), C.c_uint32]),
     "mm2g_format_paf": (C.c_int64, [_VP, C.POINTER(ReadResult), C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.c_int64]),
+    "mm2g_batch_paf": (C.c_int64, [_VP, C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.c_int64]),
     "mm2g_batch_sketch": (C.c_int, [_VP, C.c_int, C.c_int, C.c_uint32, _P64, _P64, _P64, C.c_uint64]),
     "mm2g_ctx_set_debug": (C.c_int, [_VP, C.c_int]),
     "mm2g_debug_anchors": (C.c_int64, [_VP, C.c_uint32, _P64, C.c_int64]),

@@ -357,6 +357,15 @@ class Device:
         got = check(load().mm2g_format_paf(self.index._h, res, arr, n, buf, need + 1), "format_paf")
         return buf.raw[:got].decode()
 
+    def batch_paf(self, names: Sequence[str]) -> str:
+        """PAF of the batch collected last (mm2g_batch_paf): also the several lines per read of -n <= 1 -m <= k."""
+        n = len(names)
+        arr = (C.c_char_p * max(n, 1))(*[x.encode() for x in names])
+        need = check(load().mm2g_batch_paf(self._h, arr, n, None, 0), "batch_paf")
+        buf = C.create_string_buffer(need + 1)
+        got = check(load().mm2g_batch_paf(self._h, arr, n, buf, need + 1), "batch_paf")
+        return buf.raw[:got].decode()
+
     def set_debug(self, on: bool) -> None:
         check(load().mm2g_ctx_set_debug(self._h, 1 if on else 0), "set_debug")
 
@@ -422,4 +431,4 @@ def align(index: Index, names: Sequence[str], seqs: Sequence[bytes], frac: float
         d.upload_index(index, mid)
     d.set_reads(seqs)
     res = d.map(opts)
-    return d.paf(list(names), res)
+    return d.batch_paf(list(names))

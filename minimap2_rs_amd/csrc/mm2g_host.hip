@@ -22,6 +22,7 @@
 #include "../../include/mm2g.h"
 #include "mm2g_index.h"
 #include "mm2g_internal.h"
+#include "mm2g_multi.h"
 #include "mm2g_reads.h"
 
 using namespace mm2g;
@@ -150,6 +151,10 @@ struct mm2g_ctx {
     mm2g_map_opts last_opts{};
     std::vector<int16_t> h_lut; float lut_gap = -1; int lut_n = 0; bool lut_dirty = true; void* lut_dev = nullptr;
     bool debug = false;
+    bool full_last = false;                // the last map kept every anchor (debug mode or multi-chain output)
+    bool multi_last = false;               // ... and its results come from the multi-chain epilogue (-n <= 1, -m <= k)
+    std::vector<mm2g::MultiRead> multi;    // per read of the last collected multi-chain batch
+    std::vector<mm2g_read_result> h_res;   // per-read results of the last collected batch (mm2g_batch_paf)
     // profiling
     bool prof = false;
     std::vector<ProfSlot> slots;
@@ -854,16 +859,12 @@ static int upload_lut(mm2g_ctx* c, float gap, int n, int16_t** out) {
     return 0;
 }
 
+// -n <= 1 with -m <= k (the query span): several chains reach the output (DESIGN.md "-n <= 1")
+static bool multi_chain_opts(const mm2g_map_opts* o) { return o->min_cnt < 2 && o->min_chain_score <= o->k; }
+
 // Argument checks of the Align flow (main.rs:189-230) shared by map and the stage entry points.
 static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_t& mdx1) {
     if (!(o->w > 0 && o->w < 256 && o->k > 0 && o->k <= 28)) return set_err(MM2G_E_ARG, "invalid w/k (0 < w < 256, 0 < k <= 28)");
-    // -n <= 1: the backtrack (lchain.rs:92-160) leaves mg_chain_bk_end after one step (:110,114: it has just set
-    // t[i] = 2), so every chain it yields is one anchor with score f[i] - f[pprev[i]] <= span (or f[i] = span);
-    // with -m above the span none passes and the fallback path is exactly -n >= 2's (DESIGN.md "-n <= 1").
-    // Otherwise the output hangs on Rust's sort_unstable tie order (z by f, merge by qs).
-    if (o->min_cnt < 2 && o->min_chain_score <= o->k)
-        return set_err(MM2G_E_UNSUP, "-n %d with -m %d <= k %d: the output depends on Rust's sort_unstable tie order (DESIGN.md \"-n <= 1\")",
-                       o->min_cnt, o->min_chain_score, o->k);
     if (o->bw < 0 || o->bw_long < 0) return set_err(MM2G_E_ARG, "negative bandwidth");
     mdx0 = std::max(o->max_gap, o->bw); mdx1 = std::max(o->max_gap, o->bw_long);
     if (std::max(o->bw, o->bw_long) + 1 > 60000) return set_err(MM2G_E_UNSUP, "bandwidth > 59999 not supported");
@@ -1106,6 +1107,13 @@ static int reserve_anchor_ws(mm2g_ctx* c, const unsigned long long* st, uint64_t
 static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort) {
     int32_t mdx0, mdx1;
     if (int e = check_opts(c, o, mdx0, mdx1)) return e;
+    // -n <= 1 with -m <= k: one-anchor backtrack chains pass (the backtrack leaves mg_chain_bk_end after one
+    // step, lchain.rs:110,114), so every anchor's f / pprev matters: full arrays, no singleton filter, and the
+    // host epilogue (mm2g_multi.cpp) runs the backtrack, merge and selection (DESIGN.md "-n <= 1")
+    const bool multi = !stop_after_sort && multi_chain_opts(o);
+    const bool full = c->debug || multi;
+    c->full_last = full || stop_after_sort;
+    c->multi_last = multi;
     HIPCHK(hipSetDevice(c->device));
     const HostIndex& H = *c->hidx;
     const uint32_t n = c->n_reads;
@@ -1219,12 +1227,13 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     ENSURE(c->cnt2, uint32_t, n, cnt2);
     ENSURE(c->rlist, uint32_t, n + 2, rlist);
     ENSURE(c->smax, uint64_t, n, smax);
-    const bool filt = !c->debug && !stop_after_sort && K[MM2G_KNOB_FILTER] && std::max(mdx0, mdx1) <= (1 << CELL_SHIFT);
+    const bool filt = !full && !stop_after_sort && K[MM2G_KNOB_FILTER] && std::max(mdx0, mdx1) <= (1 << CELL_SHIFT);
     const int64_t stop_at = K[MM2G_KNOB_STOP_AT];   // measurement only: later stages skipped, results invalid
     // pass-0 chain parameters (main.rs:201-214): the sort's LB pass uses them too
     ChainKParams P{};
     P.max_dist_x = mdx0; P.max_dist_y = std::max(o->max_gap, o->bw); P.bw = o->bw; P.max_iter = 5000; P.max_skip = 25;
     P.span = o->k; P.rescue_size = 1000; P.rescue_ratio_f = 1.0f - 0.1f; P.pass = 0; P.lut_n = o->bw + 1;
+    P.multi = multi ? 1 : 0;
     const float gap = 0.01f * 0.8f * (float)o->k;
     const int npass = stop_at == 3 ? 1 : 2;
     const bool chain = !stop_after_sort && stop_at != 1 && stop_at != 2;
@@ -1232,7 +1241,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     ENSURE(c->ncand, uint32_t, n, ncand);
     int32_t* fmin_buf = nullptr;
     const int16_t* lut_sort = nullptr;
-    if (chain && !c->debug && K[MM2G_KNOB_PRUNE]) {
+    if (chain && !full && K[MM2G_KNOB_PRUNE]) {
         ENSURE(c->fmin, int32_t, n, fmin_buf);
         if (filt && K[MM2G_KNOB_SORT_LB] && P.lut_n <= SORT_LB_LUT) {
             int16_t* l;
@@ -1281,7 +1290,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     if (chain) {
         // 5. chain DP + fallback + rescue
         if (int e = run_chain(c, n, c->d_rd_off, P, gap, npass, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
-                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, c->debug, st, ncand, fmin_buf, lut_sort != nullptr))
+                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, full, st, ncand, fmin_buf, lut_sort != nullptr))
             return e;
         // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
         const bool sep = (H.w != o->w || H.k != o->k);
@@ -1340,6 +1349,70 @@ int mm2g_batch_map(mm2g_ctx* c, const mm2g_map_opts* o) {
     return map_enqueue(c, o, false);
 }
 
+static void unpack_keys(const KeyLayout& kl, uint64_t span, const uint64_t* k, int64_t A, uint64_t* xy);
+
+// -n <= 1 with -m <= k: the backtrack, merge, selection and PAF records of every
+// read on the host (mm2g_multi.cpp) from the full sorted anchors and the final
+// DP pass's f / pprev; the read's result describes its first (primary) line.
+static int multi_epilogue(mm2g_ctx* c) {
+    const uint32_t n = c->n_reads;
+    const HostIndex& H = *c->hidx;
+    const mm2g_map_opts& o = c->last_opts;
+    std::vector<uint64_t> aoff((size_t)n + 1);
+    HIPCHK(hipMemcpy(aoff.data(), c->a_off.p, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost));
+    const uint64_t A = aoff[n];
+    std::vector<uint64_t> keys(A), xy(2 * A);
+    std::vector<int32_t> f(A), pp(A);
+    if (A) {
+        HIPCHK(hipMemcpy(keys.data(), c->keys.p, A * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(f.data(), c->fbuf.p, A * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(pp.data(), c->ppbuf.p, A * 4, hipMemcpyDeviceToHost));
+    }
+    unpack_keys(c->kl, (uint64_t)o.k, keys.data(), (int64_t)A, xy.data());
+    // query minimizer positions of the dv sketch (idx.w, idx.k; paf.rs:155-160)
+    const SketchBufs& D = c->dv_separate ? c->sk2 : c->sk1;
+    std::vector<uint64_t> mb(n);
+    std::vector<uint32_t> mc(n);
+    if (n) {
+        HIPCHK(hipMemcpy(mb.data(), D.base.p, (size_t)n * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(mc.data(), D.cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    }
+    uint64_t yend = 0;
+    for (uint32_t i = 0; i < n; ++i) yend = std::max<uint64_t>(yend, mb[i] + mc[i]);
+    std::vector<uint32_t> my(yend);
+    if (yend) HIPCHK(hipMemcpy(my.data(), D.y.p, yend * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> tlen(H.n_seq);
+    for (uint32_t t = 0; t < H.n_seq; ++t) tlen[t] = H.seq[t].len;
+    const int32_t kdv = c->dv_separate ? H.k : o.k;
+    mm2g::MultiParams P{o.min_cnt, o.min_chain_score, 500, o.max_gap, o.mask_level, o.pri_ratio, o.best_n};
+    c->multi.assign(n, mm2g::MultiRead{});
+    std::vector<int32_t> mp;
+    for (uint32_t i = 0; i < n; ++i) {
+        mm2g_read_result& r = c->h_res[i];
+        if (!(r.flags & MM2G_R_MAPPED)) continue;
+        const uint64_t a0 = aoff[i], na = aoff[i + 1] - aoff[i];
+        mp.resize(mc[i]);
+        for (uint32_t t = 0; t < mc[i]; ++t) mp[t] = (int32_t)(my[mb[i] + t] >> 1);
+        // avg_k = sum of spans / count in f32 (query spans are all k, non-HPC)
+        const float avg_k = mc[i] ? (float)((uint64_t)mc[i] * (uint64_t)kdv) / (float)mc[i] : (float)H.k;
+        mm2g::MultiRead& M = c->multi[i];
+        mm2g::multi_chain_read(xy.data() + 2 * a0, f.data() + a0, pp.data() + a0, (int64_t)na, r.qlen, mp.data(), (int64_t)mc[i],
+                               avg_k, kdv, tlen.data(), H.n_seq, P, M);
+        const int32_t keep = r.flags & MM2G_R_RESCUED;
+        const int32_t qlen = r.qlen, nanc = r.n_anchors;
+        memset(&r, 0, sizeof r);
+        r.qlen = qlen; r.n_anchors = nanc;
+        r.m_dv = (int32_t)mc[i]; r.sum_k = (int64_t)mc[i] * kdv;
+        if (M.panic) { r.flags = MM2G_R_MAPPED | MM2G_R_PANIC | keep; continue; }
+        if (M.lines.empty()) continue;
+        const mm2g::MultiLine& L = M.lines[0];
+        r.flags = MM2G_R_MAPPED | keep | (L.dv_found ? MM2G_R_DV_FOUND : 0);
+        r.score = M.s1; r.cm = L.cm; r.qs = L.qs; r.qe = L.qe; r.ts = L.ts; r.te = L.te; r.rid = L.rid; r.rev = L.rev;
+        r.n_match = L.n_match; r.dv_st = L.dv_st; r.dv_en = L.dv_en; r.dv = L.dv;
+    }
+    return 0;
+}
+
 int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     if (!c) return set_err(MM2G_E_ARG, "null context");
     if (!c->mapped || c->stop_after_sort) return set_err(MM2G_E_STATE, "batch not mapped");
@@ -1349,13 +1422,13 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     const HostIndex& H = *c->hidx;
     const int kdv = c->dv_separate ? H.k : c->last_opts.k;
     uint64_t cnt[6] = {c->total_bases, c->h_stat[3], 0, c->n_anchors, 0, 0};
+    c->h_res.resize(c->n_reads);
     for (uint32_t i = 0; i < c->n_reads; ++i) {
         const ReadOut& o = c->h_out[i];
         cnt[4] += (o.flags & RF_RESCUED) ? (uint64_t)o.n_anchors : 0;
         cnt[5] += o.dp_pairs;
         cnt[2] += (uint64_t)o.m_kept;
-        if (i >= n || !res) continue;
-        mm2g_read_result& r = res[i];
+        mm2g_read_result& r = c->h_res[i];
         memset(&r, 0, sizeof r);
         const uint64_t L = c->h_rd_off[i + 1] - c->h_rd_off[i];
         r.qlen = (int32_t)L;
@@ -1386,6 +1459,9 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
             r.dv = frac >= 1.0f ? 0.0f : 1.0f - powf(frac, 1.0f / fmaxf(avg_k, 1.0f));
         }
     }
+    if (c->multi_last) { if (int e = multi_epilogue(c)) return e; }
+    else c->multi.clear();
+    if (res && n) memcpy(res, c->h_res.data(), (size_t)n * sizeof(mm2g_read_result));
     for (int t = 0; t < 6; ++t) c->counters[t] = cnt[t];
     c->counters[6] = c->h_stat[4];    // anchors left after the sort's singleton filter (the DP input)
     for (int t = 0; t < 6; ++t) c->counters[7 + t] = c->h_stat[8 + t];   // anchors per chain kernel class and pass
@@ -1401,9 +1477,7 @@ static inline char* put_u(char* p, uint64_t v) {
     return p;
 }
 
-int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, const char* const* names, uint32_t n, char* out, int64_t cap) {
-    if (!idx || (n && (!res || !names))) return set_err(MM2G_E_ARG, "null argument");
-    const HostIndex& H = idx->h;
+static int64_t format_paf(const HostIndex& H, const mm2g_read_result* res, const char* const* names, uint32_t n, char* out, int64_t cap) {
     int64_t o = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const mm2g_read_result& r = res[i];
@@ -1433,6 +1507,47 @@ int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, cons
             memcpy(out + o, tname, tn); o += (int64_t)tn;
             memcpy(out + o, line + 256, (size_t)(q - (line + 256))); o += q - (line + 256);
         } else o += len;
+    }
+    return o;
+}
+
+int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, const char* const* names, uint32_t n, char* out, int64_t cap) {
+    if (!idx || (n && (!res || !names))) return set_err(MM2G_E_ARG, "null argument");
+    return format_paf(idx->h, res, names, n, out, cap);
+}
+
+int64_t mm2g_batch_paf(mm2g_ctx* c, const char* const* names, uint32_t n, char* out, int64_t cap) {
+    if (!c || (n && !names)) return set_err(MM2G_E_ARG, "null argument");
+    if (!c->mapped || !c->collected || c->h_res.size() != c->n_reads) return set_err(MM2G_E_STATE, "call mm2g_batch_results first");
+    if (n > c->n_reads) return set_err(MM2G_E_ARG, "n exceeds the batch size");
+    const HostIndex& H = *c->hidx;
+    if (!c->multi_last) return format_paf(H, c->h_res.data(), names, n, out, cap);
+    // several lines per read: write_paf_many_with_scores (paf.rs:238-248) -> write_paf (:224-236)
+    int64_t o = 0;
+    std::string line;
+    for (uint32_t i = 0; i < n; ++i) {
+        const mm2g::MultiRead& M = c->multi[i];
+        if (M.panic) continue;                       // the reference panics before printing (main.rs:218-226)
+        const uint32_t qlen = (uint32_t)c->h_res[i].qlen;
+        for (const mm2g::MultiLine& L : M.lines) {
+            const HostSeq& sq = H.seq[L.rid];
+            const uint32_t qs = (uint32_t)L.qs, qe = (uint32_t)L.qe;
+            const uint32_t pqs = L.rev ? qlen - qe : qs, pqe = L.rev ? qlen - qs : qe;
+            char buf[320];
+            line.assign(names[i]);
+            snprintf(buf, sizeof buf, "\t%u\t%u\t%u\t%c\t", qlen, pqs, pqe, L.rev ? '-' : '+');
+            line += buf;
+            line += sq.has_name ? sq.name.c_str() : "*";
+            snprintf(buf, sizeof buf, "\t%u\t%u\t%u\t%u\t%u\t60\ttp:A:%c\tcm:i:%u\ts1:i:%u\ts2:i:%u\tdv:f:%.4f\trl:i:0\n",
+                     sq.len, (uint32_t)L.ts, (uint32_t)L.te, (uint32_t)std::max(L.qe - L.qs, 0), (uint32_t)std::max(L.te - L.ts, 0),
+                     L.primary ? 'P' : 'S', (uint32_t)L.cm, (uint32_t)std::max(M.s1, 0), (uint32_t)std::max(M.s2, 0), (double)L.dv);
+            line += buf;
+            if (out) {
+                if (o + (int64_t)line.size() > cap) return set_err(MM2G_E_NOMEM, "PAF output buffer too small");
+                memcpy(out + o, line.data(), line.size());
+            }
+            o += (int64_t)line.size();
+        }
     }
     return o;
 }
@@ -1680,7 +1795,7 @@ int64_t mm2g_debug_anchors(mm2g_ctx* c, uint32_t r, uint64_t* xy, int64_t cap) {
     uint64_t off[2];
     HIPCHK(hipMemcpy(off, (uint64_t*)c->a_off.p + r, 16, hipMemcpyDeviceToHost));
     int64_t A = (int64_t)(off[1] - off[0]);
-    if (!c->debug && !c->stop_after_sort) {   // production sort: only the anchors kept by the singleton filter are sorted
+    if (!c->full_last) {   // production sort: only the anchors kept by the singleton filter are sorted
         uint32_t kept = 0;
         HIPCHK(hipMemcpy(&kept, (uint32_t*)c->cnt2.p + r, 4, hipMemcpyDeviceToHost));
         A = kept;

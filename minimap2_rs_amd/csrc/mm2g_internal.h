@@ -57,6 +57,7 @@ struct ChainKParams {
     float rescue_ratio_f;   // (1.0f - rmq_rescue_ratio), computed on the host in f32
     int32_t pass;           // 0 = first DP, 1 = rescue DP (only RF_RESCUED reads)
     int32_t lut_n;          // entries in the pen LUT (bw + 1)
+    int32_t multi;          // -n <= 1, -m <= k: chains[0] is one anchor, the rescue test sees coverage = span
 };
 
 // Device index layout: open-addressed table of distinct minimizer hashes.

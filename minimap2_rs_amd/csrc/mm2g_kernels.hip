@@ -4034,7 +4034,9 @@ __global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
     int32_t fl = RF_MAPPED | (flags0 & RF_RESCUED);
     if (g == 2u * a.kl.n_seq) fl |= RF_PANIC;
     if (P.pass == 0) {
-        int32_t cov = qe - qs; if (cov < 0) cov = 0;
+        // rescue_long_join tests chains[0] (lchain.rs:321-326): the fallback chain, or under P.multi the
+        // best one-anchor backtrack chain, whose coverage is the span
+        int32_t cov = P.multi ? span : qe - qs; if (cov < 0) cov = 0;
         int32_t unc = qlen - cov; if (unc < 0) unc = 0;
         if (unc > P.rescue_size || (float)cov < (float)qlen * P.rescue_ratio_f) fl |= RF_RESCUED;
     }

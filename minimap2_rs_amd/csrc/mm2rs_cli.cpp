@@ -234,6 +234,7 @@ int main(int argc, char** argv) {
         std::string cat;
         std::vector<uint64_t> offs{0};
         std::vector<mm2g_read_result> res;
+        std::vector<char> paf;                // formatted by the worker (mm2g_batch_paf reads its context)
         bool ok = false;
     };
     std::mutex mu;
@@ -257,6 +258,15 @@ int main(int argc, char** argv) {
             B->res.resize(n);
             B->ok = mm2g_batch_set_reads(c, (const uint8_t*)B->cat.data(), B->offs.data(), n) == 0 && mm2g_batch_map(c, &mo) == 0 &&
                     mm2g_batch_results(c, B->res.data(), n) == 0;
+            if (B->ok) {   // write_paf_many_with_scores (paf.rs:238-248): one line per read, or several under -n <= 1 -m <= k
+                std::vector<const char*> nm(n);
+                for (uint32_t i = 0; i < n; ++i) nm[i] = B->names[i].c_str();
+                const int64_t need = mm2g_batch_paf(c, nm.data(), n, nullptr, 0);
+                B->paf.resize((size_t)std::max<int64_t>(need, 0) + 1);
+                const int64_t got = need < 0 ? need : mm2g_batch_paf(c, nm.data(), n, B->paf.data(), (int64_t)B->paf.size());
+                B->ok = got >= 0;
+                if (B->ok) B->paf.resize((size_t)got);
+            }
             if (!B->ok) fprintf(stderr, "Error: %s\n", mm2g_last_error());
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -266,7 +276,6 @@ int main(int argc, char** argv) {
             cv.notify_all();
         }
     };
-    std::vector<char> pafbuf;
     auto writer = [&]() {
         for (size_t next = 0;; ++next) {
             Batch* B;
@@ -278,17 +287,12 @@ int main(int argc, char** argv) {
             }
             if (B->ok) {
                 const uint32_t n = (uint32_t)B->names.size();
-                std::vector<const char*> nm(n);
                 for (uint32_t i = 0; i < n; ++i) {
-                    nm[i] = B->names[i].c_str();
-                    if (B->res[i].flags & MM2G_R_EMPTY) fprintf(stderr, "warning: read %s is empty (the reference asserts on it, src/sketch.rs:30); skipped\n", nm[i]);
-                    if (B->res[i].flags & MM2G_R_PANIC) fprintf(stderr, "warning: read %s: the reference panics here (index out of bounds: rid 2147483647, DESIGN.md Q19); no PAF line\n", nm[i]);
+                    const char* nm = B->names[i].c_str();
+                    if (B->res[i].flags & MM2G_R_EMPTY) fprintf(stderr, "warning: read %s is empty (the reference asserts on it, src/sketch.rs:30); skipped\n", nm);
+                    if (B->res[i].flags & MM2G_R_PANIC) fprintf(stderr, "warning: read %s: the reference panics here (index out of bounds: rid 2147483647 (DESIGN.md Q19), or an empty chain under -n <= 0); no PAF line\n", nm);
                 }
-                const int64_t need = mm2g_format_paf(idx, B->res.data(), nm.data(), n, nullptr, 0);
-                pafbuf.resize((size_t)std::max<int64_t>(need, 0) + 512 * (size_t)n + 1);
-                const int64_t got = mm2g_format_paf(idx, B->res.data(), nm.data(), n, pafbuf.data(), (int64_t)pafbuf.size());
-                if (got < 0) { fprintf(stderr, "Error: %s\n", mm2g_last_error()); std::lock_guard<std::mutex> lk(mu); failed = true; }
-                else fwrite(pafbuf.data(), 1, (size_t)got, fo);
+                fwrite(B->paf.data(), 1, B->paf.size(), fo);
             }
             delete B;
             { std::lock_guard<std::mutex> lk(mu); --inflight; }

@@ -290,7 +290,7 @@ def test_cli_align_min_cnt(small_world, dense_world, tmp_path):
     """`mm2rs align -n 1` / `-n 0` / `-n -1` with -m above k (the default 40,
     and 16): byte-identical to the oracle CLI with the same flags -- the
     backtrack yields one-anchor chains scored <= k, so none passes and the
-    fallback path runs (DESIGN.md "-n <= 1").  `-n 1 -m 15` is refused."""
+    fallback path runs (DESIGN.md "-n <= 1").  -m <= k: test_multi_chain_*."""
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     mm2rs = os.path.join(root, "minimap2_rs_amd", "build", "mm2rs")
@@ -304,8 +304,49 @@ def test_cli_align_min_cnt(small_world, dense_world, tmp_path):
             c = subprocess.run([cpu, "align", ref, reads] + flags, check=True, capture_output=True, text=True).stdout
             c3 = subprocess.run([cpu, "align", ref, reads], check=True, capture_output=True, text=True).stdout
             assert g == c == c3 and g.count("\n") > 10, flags
-        bad = subprocess.run([mm2rs, "align", mmi, reads, "-n", "1", "-m", "15"], capture_output=True, text=True)
-        assert bad.returncode != 0 and "tie order" in bad.stderr
+
+
+def test_cli_multi_chain(small_world, dense_world, tmp_path):
+    """`mm2rs align -n 1 -m 15` (and -n 0 -m 0, -n -1 -m 8): several chains per
+    read reach the output (tp:A:P / tp:A:S, s2) through the backtrack, merge
+    and selection of lchain.rs:92-160,237-314 -- byte-identical to the oracle
+    CLI under the restated rustc 1.81+ sort_unstable (DESIGN.md "-n <= 1")."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mm2rs = os.path.join(root, "minimap2_rs_amd", "build", "mm2rs")
+    cpu = os.path.join(root, "oracle", "build", "mm2rs-cpu")
+    for wi, world in enumerate((small_world, dense_world)):
+        ref, reads, rnames, rseqs = world
+        mmi = str(tmp_path / f"ref{wi}.mmi")
+        subprocess.run([mm2rs, "index", ref, "-d", mmi], check=True, capture_output=True)
+        for flags in (["-n", "1", "-m", "15"], ["-n", "0", "-m", "0"], ["-n", "-1", "-m", "8", "-N", "2"]):
+            g = subprocess.run([mm2rs, "align", mmi, reads] + flags, check=True, capture_output=True, text=True).stdout
+            c = subprocess.run([cpu, "align", ref, reads] + flags, check=True, capture_output=True, text=True).stdout
+            assert g == c, (wi, flags)
+            assert "tp:A:S" in g, (wi, flags)
+
+
+@pytest.mark.parametrize("mc,m", [(1, 15), (0, 0), (-1, 8), (1, 1)])
+def test_multi_chain_vs_oracle(dev, small_world, dense_world, mc, m):
+    """-n <= 1 with -m <= k through the library (api.align -> mm2g_batch_paf):
+    the PAF text, several lines per read, equals the oracle's on the small and
+    dense worlds (mid_occ 20 and 5000)."""
+    for world, mid in ((small_world, None), (dense_world, 5000), (dense_world, 20)):
+        ref, reads, rnames, rseqs = world
+        oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+        idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+        mid = mid if mid is not None else max(idx.calc_mid_occ(2e-4), 10)
+        dev.upload_index(idx, mid)
+        dev.set_debug(False)
+        dev.set_reads(rseqs)
+        dev.map(M.map_opts(min_cnt=mc, min_chain_score=m))
+        got = dev.batch_paf(rnames)
+        want_paf = os.path.join(os.path.dirname(reads), f"want_multi_{mid}_{mc}_{m}.paf")
+        oi.align_fasta(reads, want_paf, mid_occ=mid, min_cnt=mc, min_chain_score=m)
+        want = open(want_paf).read()
+        assert got == want, (mid, mc, m)
+        assert want.count("\n") > len({ln.split("\t")[0] for ln in want.splitlines()})
+    dev.set_debug(True)
 
 
 @pytest.mark.parametrize("seg_small,lds_kb", [(1024, 0), (64, 0), (8, 0), (1, 0), (1024, 76), (8, 76)])

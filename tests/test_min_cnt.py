@@ -13,8 +13,9 @@ it extracts is the single anchor i0, with score f[i0] - f[pprev[i0]] (or f[i0]
     _with_gap's sort_unstable_by_key on qs (lchain.rs:292) meets large tie
     classes (every hit of one minimizer has the same qs), so the PAF depends
     on the tie order, which Rust leaves unspecified and which changed with the
-    rustc sort implementation.  The device path refuses that combination
-    (MM2G_E_UNSUP); this test measures the exposure.
+    rustc sort implementation (both restated in the oracle: ipnsort, the
+    default, and pdqsort); these tests measure the exposure, and the device
+    path's multi-chain output is compared in test_gpu_parity.py.
 """
 import os
 
@@ -57,7 +58,7 @@ def test_min_cnt_le1_equals_default_when_m_above_span(world):
 
 def test_min_cnt_le1_low_m_depends_on_tie_order(world):
     """-n 1 -m <= k: the two extreme tie orders give different PAF for many
-    reads (the reason the device path returns MM2G_E_UNSUP there)."""
+    reads (why Rust's sort_unstable is restated, not replaced)."""
     ref, reads, td = world
     oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
     try:
