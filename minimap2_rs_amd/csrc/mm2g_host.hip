@@ -101,10 +101,11 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SPEC_ROUNDS: return 3;
     case MM2G_KNOB_MED_PAIRS: return 0;
     case MM2G_KNOB_MED_PAIRS_RESCUE: return 0;
-    case MM2G_KNOB_SORT_LB: return 1;
+    case MM2G_KNOB_SORT_LB: return 0;
     case MM2G_KNOB_SKETCH_VIEW: return 2560;
     case MM2G_KNOB_MW_MIN: return 0;
     case MM2G_KNOB_PRUNE_RESCUE: return 1;
+    case MM2G_KNOB_VIEW_READS: return 2048;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -769,7 +770,10 @@ static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf) {
     // query views (odd k only: the fixed warm-up is exact there; a re-run
     // after a slot overflow has them off, so the exact per-read layout needs one pass)
     const uint32_t V = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(c->knob[MM2G_KNOB_SKETCH_VIEW], 1 << 30));
-    if (V >= 64 && (k & 1) && !c->views_off && c->max_read_len > V && !c->knob[MM2G_KNOB_SKETCH_PROF] && !slot) {
+    // ... and only for batches too small to fill the GPU with one wave per read
+    // (C2's 500-read units; C3's 5,000-read units measured 4 % slower with views)
+    const bool few = (int64_t)n < c->knob[MM2G_KNOB_VIEW_READS];
+    if (V >= 64 && (k & 1) && few && !c->views_off && c->max_read_len > V && !c->knob[MM2G_KNOB_SKETCH_PROF] && !slot) {
         const uint32_t W0 = (uint32_t)((2 * (w + k) + 64 + 7) & ~7);
         const uint64_t nvmax = (uint64_t)n + c->total_bases / V + 1;
         uint32_t *v_read, *v_len, *v_pre, *v_from, *v_cnt, *v_need, *nvr; uint64_t *v_off, *v_base, *v_end, *vo, *vx; uint8_t* v_last; uint32_t* vy;

@@ -239,9 +239,9 @@ struct SeqNt4 {
 
 template <bool K32, typename Src, bool HPC = false>
 #ifndef SK_WPE
-#define SK_WPE 4            // waves per SIMD: caps k_sketch at 128 VGPRs
+#define SK_WPE(Src) (std::is_same<Src, SeqNt4>::value ? 5 : 4)   // waves per SIMD: the query sketch (nt4) at 96 VGPRs, 5 waves per SIMD; the index build (ASCII) at 128
 #endif
-__global__ __launch_bounds__(256, SK_WPE) void k_sketch(SketchArgs a) {
+__global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int w = a.w, k = a.k;
     const int wv = wave_id(), lane = lane_id();
@@ -743,7 +743,7 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
         int kn = 1;                        // next seed_write part boundary
         // SC_U chunks of 64 minimizers at a time: their table probes are
         // independent, so SC_U loads per lane are in flight together
-        constexpr int SC_U = 2;
+        constexpr int SC_U = 4;
         for (uint32_t b0 = 0; b0 < m; b0 += 64 * SC_U) {
             uint64_t h[SC_U];
             uint32_t sl[SC_U], n[SC_U], off[SC_U];
@@ -757,31 +757,18 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
                 h[u] = act ? (a.mz_x[mb + i] >> 8) : 0;
                 sl[u] = ix_slot(h[u], a.log2cap); n[u] = 0; off[u] = 0;
             }
-            // linear probing, read a 64-B group of 4 slots at a time (one request,
-            // all four loads in flight): at load <= 0.5 the first group nearly
-            // always ends the probe, where slot-by-slot took ~1.5 dependent loads
-            for (;;) {
-                bool all = true;
+            // linear probing, one slot per step (measured against 64-B groups of
+            // four slots per step: twice the load instructions and 2x slower)
+            while (any(!(done[0] && done[1] && done[2] && done[3]))) {
+                IxEntry e[SC_U];
 #pragma unroll
-                for (int u = 0; u < SC_U; ++u) all = all && done[u];
-                if (!any(!all)) break;
-                IxEntry e[SC_U][4];
-#pragma unroll
-                for (int u = 0; u < SC_U; ++u)
-                    if (!done[u]) {
-#pragma unroll
-                        for (int g = 0; g < 4; ++g) e[u][g] = a.tab[(sl[u] & ~3u) + (uint32_t)g];
-                    }
+                for (int u = 0; u < SC_U; ++u) if (!done[u]) e[u] = a.tab[sl[u]];
 #pragma unroll
                 for (int u = 0; u < SC_U; ++u) {
                     if (done[u]) continue;
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        if (done[u] || g < (int)(sl[u] & 3u)) continue;
-                        if (e[u][g].key == h[u]) { off[u] = e[u][g].off; n[u] = e[u][g].n; done[u] = true; }
-                        else if (e[u][g].key == U64MAX) done[u] = true;
-                    }
-                    sl[u] = ((sl[u] & ~3u) + 4u) & cmask;
+                    if (e[u].key == h[u]) { off[u] = e[u].off; n[u] = e[u].n; done[u] = true; }
+                    else if (e[u].key == U64MAX) done[u] = true;
+                    else sl[u] = (sl[u] + 1) & cmask;
                 }
             }
 #pragma unroll
@@ -898,6 +885,7 @@ template <int NT, typename KP>
 DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint32_t A, unsigned char* lds,
                         uint32_t* w4, uint32_t* s_sc, uint64_t* pq);
 
+template <bool LB>   // LB: the instance with the LB pass (static LDS and registers only there)
 __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) { *a.rcount = 0; if (a.rwork) *a.rwork = 0; }   // k_sort_read's list for k_sort_radix / k_sort_big
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
@@ -934,7 +922,7 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) a.tmp[CK(base + i, a.cap_keys)] = s[i];   // sorted keys live in tmp
     // pass-0 LB and candidate segments from the sorted keys in LDS (as k_sort_read; the unsorted
     // keys in HBM are dead now and receive the candidate list)
-    if (a.lut && a.fmin && a.ncand && a.P.lut_n <= SMALL_LB_LUT) {
+    if constexpr (LB) if (a.lut && a.fmin && a.ncand && a.P.lut_n <= SMALL_LB_LUT) {
         __shared__ __align__(16) unsigned char s_lb[SMALL_LB_LUT * 2 + SORT_SMALL / 8];
         __shared__ uint32_t s_w4[32], s_sc4[16];
         sort_lb_cands<256>(a, r, (const uint64_t*)s, (uint32_t*)(K + base), A, s_lb, s_w4, s_sc4, nullptr);
@@ -1339,23 +1327,25 @@ DEVI void scan_lb(int32_t& a, int32_t& b) {
 // then streams the read: many one-segment items would cost more).  fmin[r] =
 // max LB either way.  LDS: the pen LUT, then ceil(A / 64) u64 bitmap words;
 // w4: 5 NW words of static LDS.
+// LB recurrence state carried into a range of sorted keys: the composition
+// entering it (block-uniform), each thread's best so far, the key before it.
+struct LbState { int32_t carry, best; uint64_t prev; };
+
+// The LB scan over n sorted keys O[0, n) at read position gbase (a multiple of
+// 64): isolated-anchor bits into isob per chunk, the composition carried in st.
+// (Measured: the same scan over each k_sort_read window in LDS costs as much as
+// over O, ~15 us per read at the sort's 4 waves per SIMD)
 template <int NT, typename KP>
-DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint32_t A, unsigned char* lds,
-                        uint32_t* w4, uint32_t* s_sc, uint64_t* pq) {
+DEVI void lb_scan(const SortArgs& a, KP O, uint32_t n, uint32_t gbase, const int16_t* lut, uint64_t* isob, uint32_t* w4, LbState& st) {
     constexpr int NW = NT / 64;
     constexpr int32_t NEG = -(1 << 29);
     constexpr int U = 8;                           // chunks per wave per round, all independent (loads in flight together)
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int lane = lane_id(), wv = wave_id();
     const ChainKParams P = a.P;                   // a copy: a reference into the kernel argument forces it to scratch
-    int16_t* lut = (int16_t*)lds;
-    uint64_t* isob = (uint64_t*)(lds + (((P.lut_n * 2) + 15) & ~15));
-    load_lut(lut, a.lut, P.lut_n);
-    __syncthreads();
-    const uint64_t t_lb0 = pq && tid == 0 ? wall_clock64() : 0;
     const uint32_t qb = a.qb, gsh = a.qb + a.rb;
     const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << a.rb) - 1;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
-    const uint32_t nwd = (A + 63) >> 6;
+    const uint32_t nwd = (n + 63) >> 6;
     int32_t* wca = (int32_t*)w4;                  // [NW] the waves' round compositions (a, b)
     int32_t* wcb = wca + NW;
     // Rounds of NW * U chunks: wave w takes chunks c = c0 + w*U + u.  Each chunk's
@@ -1363,27 +1353,28 @@ DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint3
     // in registers until the LB entering the chunk is known (a scan over the
     // chunks' totals: in the wave, then across the waves through LDS); nothing
     // is carried from chunk to chunk inside a wave.
-    int32_t carry = NEG, best = span;
+    int32_t carry = st.carry, best = st.best;
+    const uint64_t prev = st.prev;
     for (uint32_t c0 = 0; c0 < nwd; c0 += NW * U) {
         int32_t sa[U], sb[U];
         uint64_t kk[U], pv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t cc = c0 + (uint32_t)(wv * U + u), i = cc * 64 + (uint32_t)lane;
-            kk[u] = (cc < nwd && i < A) ? O[i] : 0;
-            pv[u] = (cc < nwd && cc > 0) ? O[cc * 64 - 1] : 0;   // the chunk's predecessor key (same address on every lane)
+            kk[u] = (cc < nwd && i < n) ? O[i] : 0;
+            pv[u] = (cc < nwd && cc > 0) ? O[cc * 64 - 1] : prev;   // the chunk's predecessor key (same address on every lane)
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t cc = c0 + (uint32_t)(wv * U + u), i = cc * 64 + (uint32_t)lane;
-            const bool valid = cc < nwd && i < A;
+            const bool valid = cc < nwd && i < n;
             const uint64_t ak = kk[u];
             const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)(uint32_t)(pv[u] >> 32)) << 32) |
                                 (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)(uint32_t)pv[u]);
             const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
             const int32_t p = (int32_t)((ak >> qb) & rmask), pj = (int32_t)((pk >> qb) & rmask);
             const int32_t q = (int32_t)(ak & qmask), qj = (int32_t)(pk & qmask);
-            const bool iso = valid && (i == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx));
+            const bool iso = valid && (gbase + i == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx));
             int32_t xa = valid ? NEG : 0, xb = valid ? span : NEG;   // invalid lanes: the identity
             if (valid && !iso) {   // comput_sc (lchain.rs:17-34) of (i, i-1); the LUT is (gap*dd + 0.5*log2(dd+1)) as i32
                 const int32_t dq = q - qj, dr = p - pj;
@@ -1419,6 +1410,20 @@ DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint3
         for (int w2 = 0; w2 < NW; ++w2) xc = max(max(xc + wca[w2], NEG), wcb[w2]);
         carry = xc;
     }
+    st.carry = carry; st.best = best;
+    if (n) st.prev = O[n - 1];
+}
+
+// The candidate segments from the isolated-anchor bitmap isob (A bits) and the
+// threads' LB maxima (see sort_lb_cands).
+template <int NT>
+DEVI void lb_finish(const SortArgs& a, uint32_t r, const uint64_t* isob, uint32_t* Kc, uint32_t A, int32_t best,
+                    uint32_t* w4, uint32_t* s_sc, uint64_t* pq, uint64_t t_lb0) {
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int32_t span = a.P.span;
+    const uint32_t nwd = (A + 63) >> 6;
+    int32_t* wca = (int32_t*)w4;
     __syncthreads();                               // bitmap complete
     best = rdl(scan_max(best), 63);
     int32_t* wmx = wca + 2 * NW;
@@ -1487,14 +1492,32 @@ DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint3
     if (pq && tid == 0) { pq[17] += wall_clock64() - t_lb0; pq[18] = tot; }
 }
 
+
+template <int NT, typename KP>
+DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint32_t A, unsigned char* lds,
+                        uint32_t* w4, uint32_t* s_sc, uint64_t* pq) {
+    constexpr int32_t NEG = -(1 << 29);
+    const int tid = threadIdx.x;
+    int16_t* lut = (int16_t*)lds;
+    uint64_t* isob = (uint64_t*)(lds + (((a.P.lut_n * 2) + 15) & ~15));
+    load_lut(lut, a.lut, a.P.lut_n);
+    __syncthreads();
+    const uint64_t t_lb0 = pq && tid == 0 ? wall_clock64() : 0;
+    LbState st{NEG, a.P.span, 0};
+    lb_scan<NT>(a, O, A, 0u, lut, isob, w4, st);
+    lb_finish<NT>(a, r, isob, Kc, A, st.best, w4, s_sc, pq, t_lb0);
+}
+
 // GL: the group offsets stay in HBM (2 n_seq + 2 > GOFF_LDS).  A template
 // parameter rather than a pointer chosen at run time: a pointer that may be
 // LDS or global compiles to flat loads, and every flat load waits for all
 // outstanding global loads and stores (vmcnt(0)), which serialised P1/P2 per key.
-template <bool GL, int NT>
+// LB: the instance with the pass-0 LB pass (MM2G_KNOB_SORT_LB); the other one
+// keeps its registers (89 VGPRs against 120), so other contexts' waves still fit
+// beside a sorting workgroup.
+template <bool GL, int NT, bool LB>
 __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
     constexpr int NW = NT / 64;
-    constexpr int RK_KPT = (SORT_LDS / 8 + NT - 1) / NT < 20 ? (SORT_LDS / 8 + NT - 1) / NT : 20;   // window keys per thread
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t red[32];
     __shared__ uint32_t s_sc[16], s_kept, s_nbig;
@@ -1588,7 +1611,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
         // top 16 bits, which the key layout must leave free.
         const uint32_t cofs = LW >= cw + 2 ? (LW - cw) & ~1u : 0u;
         const uint32_t kbits = gsh + (32u - (uint32_t)__builtin_clz(2u * a.n_seq | 1u));
-        const uint32_t W = min(cofs >> 1, (uint32_t)(RK_KPT * NT));   // keys per window (the rank phase holds RK_KPT per thread)
+        const uint32_t W = cofs >> 1;                        // keys per window
         if (kbits > 48u || qb + CELL_SHIFT > 32u || cofs < 2 * nw || W < SEG_RANK) { defer(); return; }
         {
             constexpr uint64_t kmask = (1ULL << 48) - 1;
@@ -1720,63 +1743,45 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 // B: ranks inside the segments.  Keys of one segment share every bit
                 // above the cell-local lb <= 32 (rank, group, cell), so they compare
                 // by their low dwords.
-                // Each thread keeps its keys and their destinations in registers (a
-                // shift register: constant indices, no scratch); after a barrier they
-                // are permuted in place in S and leave for O in whole lines -- scattered
-                // 8-B stores to O cost one request per key in the TA.
+                // Each key leaves for its place in O directly (measured against a
+                // permutation in LDS with whole-line writes: slower)
                 const uint32_t* S32 = (const uint32_t*)S;
                 uint32_t pc_tiny = 0, pc_long = 0, pc_srch = 0;     // MM2G_KNOB_SORT_PROF segment classes
-                uint64_t xk[RK_KPT];
-                uint32_t pk[RK_KPT];
-                for (int u = 0; u < RK_KPT; ++u) {
-                    const uint32_t i = (uint32_t)tid + (uint32_t)u * NT;
-                    uint64_t xo = 0;
-                    uint32_t po = 0;
-                    if (i < nwin) {
-                        const uint64_t x = S[i];
-                        uint32_t s, e;
-                        seg_of(x, s, e);
-                        const uint32_t L = e - s;
-                        xo = x & kmask;
-                        if (L > a.seg_small) {             // P4b; stays unsorted
-                            po = i;
-                            if (i == s) {
-                                const uint32_t slot = atomicAdd(&s_nbig, 1u);
-                                if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s, oa + e);
-                            }
-                        } else {
-                            const uint32_t xl = (uint32_t)x;
-                            uint32_t rank = 0;
-                            if (pq) {
-                                if (L <= SEG_TINY) ++pc_tiny;
-                                else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
-                            }
-                            if (L <= SEG_TINY) {
-                                for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
-                            } else {
-                                const uint32_t co = i >> 6;
-                                rank = i - max(s, co << 6);
-                                for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
-                                    if (c == co) continue;
-                                    rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
-                                }
-                            }
-                            po = s + rank;
+                for (uint32_t i = tid; i < nwin; i += NT) {
+                    const uint64_t x = S[i];
+                    uint32_t s, e;
+                    seg_of(x, s, e);
+                    const uint32_t L = e - s;
+                    if (L > a.seg_small) {             // P4b; copied unsorted
+                        O[oa + i] = x & kmask;
+                        if (i == s) {
+                            const uint32_t slot = atomicAdd(&s_nbig, 1u);
+                            if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s, oa + e);
+                        }
+                        continue;
+                    }
+                    const uint32_t xl = (uint32_t)x;
+                    uint32_t rank = 0;
+                    if (pq) {
+                        if (L <= SEG_TINY) ++pc_tiny;
+                        else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
+                    }
+                    if (L <= SEG_TINY) {
+                        for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
+                    } else {
+                        const uint32_t co = i >> 6;
+                        rank = i - max(s, co << 6);
+                        for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
+                            if (c == co) continue;
+                            rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
                         }
                     }
-#pragma unroll
-                    for (int v = 0; v + 1 < RK_KPT; ++v) { xk[v] = xk[v + 1]; pk[v] = pk[v + 1]; }
-                    xk[RK_KPT - 1] = xo; pk[RK_KPT - 1] = po;
+                    O[oa + s + rank] = x & kmask;
                 }
                 if (pq) {
                     const uint64_t v14 = wave_sum64(((uint64_t)pc_long << 32) | pc_tiny), v15 = wave_sum64(pc_srch);
                     if (lane == 0) { atomicAdd((unsigned long long*)&pq[14], (unsigned long long)v14); atomicAdd((unsigned long long*)&pq[15], (unsigned long long)v15); }
                 }
-                __syncthreads();                   // every compare has read S
-#pragma unroll
-                for (int u = 0; u < RK_KPT; ++u) if ((uint32_t)tid + (uint32_t)u * NT < nwin) S[pk[u]] = xk[u];
-                __syncthreads();
-                for (uint32_t i = tid; i < nwin; i += NT) O[oa + i] = S[i];
                 __syncthreads();
                 SORT_PH(5);
                 ra = rb;
@@ -1816,7 +1821,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
             }
             SORT_PH(6);
             // pass-0 LB and candidate segments (k_chain_lb / k_chain_seg's scan, fused)
-            if (a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
+            if (LB && a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
                 __syncthreads();                   // O complete (rank phase, P4b) and visible to the block
                 sort_lb_cands<NT>(a, r, (const uint64_t*)O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc, pq);
                 SORT_PH(3);
@@ -4363,7 +4368,11 @@ int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
 int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
     if (a.n == 0) return 0;
     const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4;
-    if (stage == 0) hipLaunchKernelGGL(k_sort_small, dim3(a.n), dim3(256), 0, st, a);
+    const bool lb = a.lut != nullptr;
+    if (stage == 0) {
+        if (lb) hipLaunchKernelGGL(k_sort_small<true>, dim3(a.n), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_sort_small<false>, dim3(a.n), dim3(256), 0, st, a);
+    }
     else if (stage == 1) {
         // the requested LDS (default SORT_LDS: one workgroup per CU), at least the two bitmaps
         size_t lds = std::max<size_t>(a.lds_words ? (size_t)a.lds_words * 4 : (size_t)SORT_LDS, bmb);
@@ -4373,11 +4382,14 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
         // up to SORT_LDS_HALF: 512-thread workgroups, two per CU (one read's
         // barrier and latency phases overlap the other's)
         const bool gl = 2u * b.n_seq + 2u > (uint32_t)GOFF_LDS;
+#define SR_LAUNCH(G, T) do { if (lb) hipLaunchKernelGGL((k_sort_read<G, T, true>), dim3(a.n), dim3(T), lds, st, b); \
+                             else hipLaunchKernelGGL((k_sort_read<G, T, false>), dim3(a.n), dim3(T), lds, st, b); } while (0)
         if (lds <= (size_t)SORT_LDS_HALF) {
-            if (gl) hipLaunchKernelGGL((k_sort_read<true, 512>), dim3(a.n), dim3(512), lds, st, b);
-            else hipLaunchKernelGGL((k_sort_read<false, 512>), dim3(a.n), dim3(512), lds, st, b);
-        } else if (gl) hipLaunchKernelGGL((k_sort_read<true, 1024>), dim3(a.n), dim3(1024), lds, st, b);
-        else hipLaunchKernelGGL((k_sort_read<false, 1024>), dim3(a.n), dim3(1024), lds, st, b);
+            if (gl) SR_LAUNCH(true, 512);
+            else SR_LAUNCH(false, 512);
+        } else if (gl) SR_LAUNCH(true, 1024);
+        else SR_LAUNCH(false, 1024);
+#undef SR_LAUNCH
     } else if (a.cells) {       // the singleton filter is on: every listed read takes the bucket path
         SortArgs b = a;
         b.lds_words = (uint32_t)(SORT_LDS / 4);

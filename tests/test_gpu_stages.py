@@ -86,7 +86,7 @@ def test_workspace_exact_fallback(small_world, dense_world):
         d.close()
 
 
-@pytest.mark.parametrize("kn", [dict(sort_lb=0), dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1),
+@pytest.mark.parametrize("kn", [dict(sort_lb=1), dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1, sort_lb=1),
                                 dict(mw_min=64), dict(sort_small=1, mw_min=128, sketch_view=300)])
 def test_round4_paths_vs_oracle(dev, small_world, dense_world, kn):
     """Every round-4 production path, on and off, against the oracle (PAF and
