@@ -209,6 +209,29 @@ int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, cons
  * Returns bytes written; out = NULL only sizes. */
 int64_t mm2g_batch_paf(mm2g_ctx* ctx, const char* const* names, uint32_t n, char* out, int64_t cap);
 
+/* One line of the multi-chain output (paf_from_chain_with_primary, src/paf.rs:130-222). */
+typedef struct {
+    int32_t qs, qe, ts, te;  /* chain ranges (forward-of-anchor query coordinates)  */
+    int32_t rid, rev, cm;
+    int32_t primary;         /* tp:A:P (1) or S (0)                                 */
+    float dv;
+    int32_t s1, s2;
+} mm2g_chain_line;
+/* The host epilogue of one read under -n <= 1 -m <= k (what mm2g_batch_results
+ * runs per read; DESIGN.md §2 "-n <= 1"), on the caller's sorted anchors
+ * (xy pairs as build_anchors_filtered returns them) and the final chain_dp_all
+ * pass's f / pprev (after rescue_long_join when it re-ran the DP): the
+ * backtrack (src/lchain.rs:92-175; z ordered by rustc 1.81+ sort_unstable),
+ * merge_adjacent_chains_with_gap (:288-314, max_gap = opts->max_gap),
+ * select_and_filter_chains (:237-260) and the PAF records with dv
+ * (paf.rs:155-199; mini_pos = the read's minimizer positions of the index's
+ * (w, k) sketch, avg_k their mean span in f32; tlen[rid] per target).  Host
+ * only.  Returns the number of lines (written up to cap), 0 for none, or
+ * MM2G_E_STATE when the reference panics on the read (*panic = 1). */
+int64_t mm2g_multi_chain_lines(const uint64_t* xy, const int32_t* f, const int32_t* pprev, int64_t n, int32_t qlen,
+                               const int32_t* mini_pos, int64_t n_mini, float avg_k, const uint32_t* tlen, uint32_t n_seq,
+                               const mm2g_map_opts* opts, mm2g_chain_line* out, int64_t cap, int32_t* panic);
+
 /* ---------------------------------------------------------------- stages
  * Stage-level access for parity tests (each replaces one reference fn). */
 /* sketch_sequence(seq, w, k, rid, false, out) (src/sketch.rs:29-100) on the

@@ -55,6 +55,12 @@ class ChainResult(C.Structure):
                 ("qe", C.c_int32), ("ts", C.c_int32), ("te", C.c_int32), ("rid", C.c_int32), ("rev", C.c_int32)]
 
 
+class ChainLine(C.Structure):
+    _fields_ = [("qs", C.c_int32), ("qe", C.c_int32), ("ts", C.c_int32), ("te", C.c_int32), ("rid", C.c_int32),
+                ("rev", C.c_int32), ("cm", C.c_int32), ("primary", C.c_int32), ("dv", C.c_float), ("s1", C.c_int32),
+                ("s2", C.c_int32)]
+
+
 # knobs (include/mm2g.h)
 KNOBS = {"sort_small": 1, "seg_small": 2, "seg_chunk": 3, "giant_min": 4, "giant_min0": 5, "giant_lcap": 6, "giant_gmax": 7,
          "giant_gblocks": 8, "filter": 9, "lazy": 10, "prune": 11, "giant": 12, "sketch_prof": 13, "sort_prof": 14,
@@ -99,6 +105,9 @@ SIGNATURES = {
     "mm2g_batch_results": (C.c_int, [_VP, C.POINTER(ReadResult), C.c_uint32]),
     "mm2g_format_paf": (C.c_int64, [_VP, C.POINTER(ReadResult), C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.c_int64]),
     "mm2g_batch_paf": (C.c_int64, [_VP, C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.c_int64]),
+    "mm2g_multi_chain_lines": (C.c_int64, [_P64, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int64, C.c_int32,
+                                           C.POINTER(C.c_int32), C.c_int64, C.c_float, C.POINTER(C.c_uint32), C.c_uint32,
+                                           C.POINTER(MapOpts), C.POINTER(ChainLine), C.c_int64, C.POINTER(C.c_int32)]),
     "mm2g_batch_sketch": (C.c_int, [_VP, C.c_int, C.c_int, C.c_uint32, _P64, _P64, _P64, C.c_uint64]),
     "mm2g_ctx_set_debug": (C.c_int, [_VP, C.c_int]),
     "mm2g_debug_anchors": (C.c_int64, [_VP, C.c_uint32, _P64, C.c_int64]),

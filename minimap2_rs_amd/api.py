@@ -32,7 +32,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib as L
-from ._lib import ChainParams, ChainResult, MapOpts, Nt4Batch, ReadResult, check, load
+from ._lib import ChainLine, ChainParams, ChainResult, MapOpts, Nt4Batch, ReadResult, check, load
 
 
 @dataclass
@@ -432,3 +432,27 @@ def align(index: Index, names: Sequence[str], seqs: Sequence[bytes], frac: float
     d.set_reads(seqs)
     res = d.map(opts)
     return d.batch_paf(list(names))
+
+
+def multi_chain_lines(xy: np.ndarray, f: np.ndarray, pprev: np.ndarray, qlen: int, mini_pos: np.ndarray, avg_k: float,
+                      tlen: np.ndarray, opts: Optional[MapOpts] = None):
+    """mm2g_multi_chain_lines (host only): the -n <= 1 -m <= k epilogue of one read -> (lines, panic)."""
+    o = opts if opts is not None else map_opts(min_cnt=1, min_chain_score=15)
+    a = np.ascontiguousarray(xy, dtype=np.uint64).reshape(-1)
+    n = len(a) // 2
+    f32 = np.ascontiguousarray(f, dtype=np.int32)
+    p32 = np.ascontiguousarray(pprev, dtype=np.int32)
+    mp = np.ascontiguousarray(mini_pos, dtype=np.int32)
+    tl = np.ascontiguousarray(tlen, dtype=np.uint32)
+    cap = max(n, 1) + 8
+    out = (ChainLine * cap)()
+    pan = C.c_int32(0)
+    I32 = C.POINTER(C.c_int32)
+    m = load().mm2g_multi_chain_lines(a.ctypes.data_as(L._P64), f32.ctypes.data_as(I32), p32.ctypes.data_as(I32), n, int(qlen),
+                                      mp.ctypes.data_as(I32), len(mp), float(avg_k), tl.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                      len(tl), C.byref(o), out, cap, C.byref(pan))
+    if pan.value:
+        return [], True
+    check(m, "multi_chain_lines")
+    return [out[i] for i in range(min(m, cap))], False
+

@@ -1515,6 +1515,23 @@ static int64_t format_paf(const HostIndex& H, const mm2g_read_result* res, const
     return o;
 }
 
+int64_t mm2g_multi_chain_lines(const uint64_t* xy, const int32_t* f, const int32_t* pprev, int64_t n, int32_t qlen,
+                               const int32_t* mini_pos, int64_t n_mini, float avg_k, const uint32_t* tlen, uint32_t n_seq,
+                               const mm2g_map_opts* o, mm2g_chain_line* out, int64_t cap, int32_t* panic) {
+    if (!o || n < 0 || n_mini < 0 || (n && (!xy || !f || !pprev)) || (n_mini && !mini_pos) || (n_seq && !tlen) || (cap && !out))
+        return set_err(MM2G_E_ARG, "null argument");
+    mm2g::MultiParams P{o->min_cnt, o->min_chain_score, 500, o->max_gap, o->mask_level, o->pri_ratio, o->best_n};
+    mm2g::MultiRead M;
+    mm2g::multi_chain_read(xy, f, pprev, n, qlen, mini_pos, n_mini, avg_k, 0, tlen, n_seq, P, M);
+    if (panic) *panic = M.panic ? 1 : 0;
+    if (M.panic) return set_err(MM2G_E_STATE, "the reference panics on this read");
+    for (size_t i = 0; i < M.lines.size() && (int64_t)i < cap; ++i) {
+        const mm2g::MultiLine& L = M.lines[i];
+        out[i] = mm2g_chain_line{L.qs, L.qe, L.ts, L.te, L.rid, L.rev, L.cm, L.primary ? 1 : 0, L.dv, M.s1, M.s2};
+    }
+    return (int64_t)M.lines.size();
+}
+
 int64_t mm2g_format_paf(const mm2g_index* idx, const mm2g_read_result* res, const char* const* names, uint32_t n, char* out, int64_t cap) {
     if (!idx || (n && (!res || !names))) return set_err(MM2G_E_ARG, "null argument");
     return format_paf(idx->h, res, names, n, out, cap);
