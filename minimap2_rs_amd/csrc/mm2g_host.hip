@@ -1017,6 +1017,10 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                 ca.mw_min = 0;
             }
             if (stg == 2) continue;   // launched above
+            // k_chain_seg routes a segment to k_chain_med only when its estimated pairs stay
+            // under est_lane (EST_LANE for pass 0 with full DP arrays): at 0 the queue stays
+            // empty and the launch would only add its latency (C2 is launch-bound)
+            if (stg == 1 && ca.est_lane == 0 && !(pass == 0 && full)) continue;
             ProfScope ps(c, names[pass][stg]);
             LCHK(launch_chain_stage(stg, ca, blocks[stg], c->stream));
         }
