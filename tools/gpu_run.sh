@@ -51,7 +51,7 @@ for S in "${STEPS[@]}"; do
     c2)
       timeout -k 10 400 python -u bench.py --preset ecoli --reads 1000 --steps 10 --warmup 2 --no-cpu $BARGS > "$OUT/c2.json" 2> "$OUT/c2.err"; line "$OUT/c2.json" ;;
     c5)
-      timeout -k 10 600 python -u bench.py --reads 2000 --read-len 100000 --steps 3 --warmup 1 --no-cpu $BARGS > "$OUT/c5.json" 2> "$OUT/c5.err"; line "$OUT/c5.json" ;;
+      timeout -k 10 600 python -u bench.py --reads 2000 --read-len 100000 --steps 12 --warmup 1 --no-cpu $BARGS > "$OUT/c5.json" 2> "$OUT/c5.err"; line "$OUT/c5.json" ;;
     multi)
       rc=0; timeout -k 10 120 python -u bench.py --gpus 2 --steps 2 > "$OUT/multi_nccl2.json" 2> "$OUT/multi_nccl2.err" || rc=$?
       echo "bench.py --gpus 2 on $(python3 -c 'import torch; print(torch.cuda.device_count())') GPU(s): exit $rc" | tee "$OUT/multi_nccl2.rc"
