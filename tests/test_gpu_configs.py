@@ -169,3 +169,45 @@ def test_c5_hg38_100kb(hg38, tmp_path):
     # pass 0's 100 kb chains through k_chain_long_mw (one 8-wave workgroup per segment of >= 4096 anchors)
     with knobs(dev, mw_min=4096):
         _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5mw")
+
+
+@pytest.mark.parametrize("mc,m", [(1, 15), (0, 0)])
+def test_hg38_multi_chain(hg38, tmp_path, mc, m):
+    """`-n <= 1 -m <= k` (several chains per read: tp:A:P/S lines, real s2)
+    at the C3 and C5 shapes, mm2g_batch_paf's text against the oracle's PAF:
+    120 x 10 kb and 12 x 100 kb reads (+ 4 chimeras).  On the full
+    hg38-shaped index nearly every read has some chain on an odd rid (the Q19
+    pseudo-group), so the reference panics on it and both sides print
+    nothing; the same reads against an index of the first contig alone
+    (rid 0: no Q19) give the primary and secondary lines."""
+    names, lens, gbuf, oi, idx, mid, dev = hg38
+    n0 = int(lens[0])
+    oi1 = O.OIndex.build_from_buffer(names[:1], gbuf[:n0], lens[:1], threads=THREADS)
+    idx1 = M.Index.build_from_buffer(names[:1], gbuf[:n0], lens[:1], threads=THREADS, device=0)
+    mid1 = max(idx1.calc_mid_occ(2e-4), 10)
+    dev1 = M.Device(0)
+    dev1.upload_index(idx1, mid1)
+    try:
+        for tag, n, L, seed in (("c3", 120, 10000, 3), ("c5", 12, 100000, 5)):
+            for one, (d, o, mo, g, ln) in enumerate(((dev, oi, mid, gbuf, lens), (dev1, oi1, mid1, gbuf[:n0], lens[:1]))):
+                seqs, rn = _reads(g, ln, n, L, seed)
+                if L == 100000:
+                    for i in range(4):
+                        seqs.append(seqs[i][:50000] + seqs[4 + i][50000:])
+                        rn.append(f"chim{i}")
+                d.set_debug(False)
+                d.set_reads(seqs)
+                d.map(M.map_opts(min_cnt=mc, min_chain_score=m))
+                got = d.batch_paf(rn)
+                fa = str(tmp_path / f"{tag}_{one}_multi.fa")
+                simdata.write_fasta(fa, rn, seqs)
+                want = str(tmp_path / f"{tag}_{one}_multi_{mc}_{m}.paf")
+                o.align_fasta(fa, want, mid_occ=mo, min_cnt=mc, min_chain_score=m)
+                want = open(want).read()
+                assert got == want, (tag, one, mc, m)
+                if one and not (mc <= 0 and L == 100000):   # -n 0 on 100 kb reads: an empty chain always reaches the merge (a panic)
+                    assert "tp:A:S" in want and len({ln.split("\t")[0] for ln in want.splitlines()}) > n // 2, (tag, mc, m)
+    finally:
+        dev1.close()
+        oi1.close()
+        idx1.close()
