@@ -1039,6 +1039,9 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                             "per-anchor path: %llu settled by the simple/shortcut step, %llu exact (%llu 64-lane window steps in all); "
                             "shader cycles per per-anchor-path anchor: st %.0f simple %.0f exact %.0f tail %.0f\n",
                     pass, g[16], g[24], g[25], g[17], g[19], g[18], g[20] / np_, g[21] / np_, g[22] / np_, g[23] / np_);
+            fprintf(stderr, "[long_prof] pass %d heaviest segment: %llu anchors committed speculatively in %llu rounds, %llu by the per-anchor path; "
+                            "shader cycles: speculative %llu, per-anchor path %llu, segment %llu\n",
+                    pass, g[26], g[27], g[28], g[30], g[29], g[31]);
         }
         if (ca.lseg_prof) {   // the slowest long segments of this pass
             uint32_t nl = 0;

@@ -3116,6 +3116,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
         int32_t best_f = INT_MIN, best_i = -1;
         (void)A; (void)n_deep;
         const uint64_t seg_t0 = wall_clock64();
+        uint64_t pc_spec = 0, pc_seg0 = PROF ? clock64() : 0;   // PROF: the heaviest segment's cycles
         // ---- cooperative DP of segment [s, e): anchor s is isolated, every
         // later anchor has a candidate predecessor.  The 64 newest
         // predecessors (rpos, qpos, f, pprev; lane l <-> j = i-1-l) live in
@@ -3160,6 +3161,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
             // loop would run past its 64 predecessors, and every anchor left after
             // a.spec_rounds rounds, takes the per-anchor path below.
             int32_t i_seq = ib;
+            const uint64_t tsp0 = PROF ? clock64() : 0;
             if (a.lazy) {
                 const int32_t k = i0 + lane;
                 const bool kv = k >= ib && k < ie;
@@ -3284,6 +3286,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     st = slo > st ? slo : st;
                 }
             }
+            if (PROF) pc_spec += clock64() - tsp0;
             for (int32_t i = i_seq; i < ie; ++i) {
                 if (PROF) tp = clock64();
                 const uint64_t ki = rdl64(ak, i - i0);
@@ -3523,6 +3526,12 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 atomicAdd(&a.gprof[20], (unsigned long long)pc_st); atomicAdd(&a.gprof[21], (unsigned long long)pc_simple);
                 atomicAdd(&a.gprof[22], (unsigned long long)pc_exact); atomicAdd(&a.gprof[23], (unsigned long long)pc_tail);
                 atomicAdd(&a.gprof[24], (unsigned long long)pn_spec); atomicAdd(&a.gprof[25], (unsigned long long)pn_rounds);
+                if (t == 0) {   // the heaviest segment (lseg_order is longest first)
+                    atomicAdd(&a.gprof[26], (unsigned long long)pn_spec); atomicAdd(&a.gprof[27], (unsigned long long)pn_rounds);
+                    atomicAdd(&a.gprof[28], (unsigned long long)(pn_done + pn_exact));
+                    atomicAdd(&a.gprof[29], (unsigned long long)(pc_st + pc_simple + pc_exact + pc_tail));
+                    atomicAdd(&a.gprof[30], (unsigned long long)pc_spec); atomicAdd(&a.gprof[31], (unsigned long long)(clock64() - pc_seg0));
+                }
             }
         }
     }
