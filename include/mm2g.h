@@ -330,12 +330,10 @@ enum {
     MM2G_KNOB_MED_PAIRS_RESCUE = 24, /* the same for the rescue pass [0]                                          */
     MM2G_KNOB_WS_FAIL = 25,      /* tests: the next this-many up-front anchor-workspace reservations fail as if
                                     HBM were full, forcing the exact-size fallback; 0 = off [0]              */
-    MM2G_KNOB_SORT_LB = 26,      /* the sort computes the pass-0 DP lower bound and candidate segments (k_chain_lb
-                                    skips those reads, k_chain_seg runs only the candidates) [0]             */
+    /* 26: retired (round 5; the sort's fused LB pass, measured slower and removed) */
     MM2G_KNOB_SKETCH_VIEW = 27,  /* odd k: reads longer than this are sketched as views of this many bases,
                                     one wave each; 0 = one wave per read [2560]                             */
-    MM2G_KNOB_MW_MIN = 28,       /* pass-0 segments of at least this many anchors (rounded up to a power of two)
-                                    take an 8-wave workgroup each (k_chain_long_mw); 0 = off [0]             */
+    /* 28: retired (round 5; k_chain_long_mw, measured 2x slower and removed) */
     MM2G_KNOB_PRUNE_RESCUE = 29, /* the rescue pass prunes segments by pass 0's best-f lower bound [1]         */
     MM2G_KNOB_VIEW_READS = 30,   /* sketch views (MM2G_KNOB_SKETCH_VIEW) only for batches of fewer reads [2048]  */
     MM2G_KNOB_COUNT = 31

@@ -101,9 +101,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SPEC_ROUNDS: return 3;
     case MM2G_KNOB_MED_PAIRS: return 0;
     case MM2G_KNOB_MED_PAIRS_RESCUE: return 0;
-    case MM2G_KNOB_SORT_LB: return 0;
     case MM2G_KNOB_SKETCH_VIEW: return 2560;
-    case MM2G_KNOB_MW_MIN: return 0;
     case MM2G_KNOB_PRUNE_RESCUE: return 1;
     case MM2G_KNOB_VIEW_READS: return 2048;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
@@ -137,7 +135,7 @@ struct mm2g_ctx {
     DevBuf tab_off, tab_key, tab_cnt;
     DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
     DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, item_read, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist, ncand;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, item_read, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist;
     DevBuf dstat;                          // batch status block (BS_* word, workspace needs, counters)
     DevBuf chain_rdoff;                    // mm2g_chain_batch: prefix sums of the caller's qlen
     uint64_t cap_tab = 0, cap_A = 0;       // filter-table entries / anchors the workspaces hold
@@ -218,7 +216,6 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
         hipStreamSynchronize(c->stream) != hipSuccess) return;
     (void)hipFree(d);
     double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tot = 0, a0 = 0, a2 = 0, np = 0, nleg = 0, nbigp = 0, ktiny = 0, klong = 0, ksrch = 0;
-    double lb_scan = 0, lb_all = 0, n_lb = 0, n_cand = 0, n_over = 0;
     uint64_t t_lo = ~0ULL, t_hi = 0;
     uint32_t m = 0;
     std::vector<uint32_t> q0, q2, q3;
@@ -236,8 +233,6 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
         t_lo = std::min(t_lo, p[10]); t_hi = std::max(t_hi, p[11]);
         q0.push_back((uint32_t)p[8]); q2.push_back((uint32_t)p[9]);
         ktiny += (double)(uint32_t)p[14]; klong += (double)(p[14] >> 32); ksrch += (double)p[15];
-        lb_scan += (double)p[16]; lb_all += (double)p[17];
-        if (p[17]) { ++n_lb; n_cand += (double)p[18]; if (p[18] > (uint64_t)(p[9] & 0xffffffffu) / 32 + 8) ++n_over; }
     }
     if (!m) return;
     std::sort(q0.begin(), q0.end()); std::sort(q2.begin(), q2.end()); std::sort(q3.begin(), q3.end());
@@ -250,9 +245,6 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
             ph[5] / m / 100, ph[6] / m / 100, tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
     fprintf(stderr, "[sort_prof] keys per read in segments <= %u: %.0f, 17..64: %.0f, > 64: %.0f (%.2f other-chunk searches each)\n",
             16u, ktiny / m, (a2 - ktiny - klong) / m, klong / m, klong > 0 ? ksrch / klong : 0.0);
-    if (n_lb > 0)
-        fprintf(stderr, "[sort_prof] LB pass on %.0f reads: scan %.1f us, with candidates %.1f us per read; candidates per read %.2f, "
-                        "over budget (streamed) %.0f reads\n", n_lb, lb_scan / n_lb / 100, lb_all / n_lb / 100, n_cand / n_lb, n_over);
 }
 
 // MM2G_SKETCH_PROF: phase times of k_sketch summed over each read's tiles
@@ -885,14 +877,13 @@ static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_
 static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const ChainKParams& P0, float gap, int npass, int32_t mdx1,
                      int32_t mdy1, int32_t bw_long, uint64_t A_cap, const uint64_t* a_off, const uint32_t* a_cnt, uint64_t* keys,
                      uint64_t* ktmp, const uint32_t* cnt2, const uint64_t* smax, ReadOut* out, const uint32_t* abort, bool full,
-                     unsigned long long* stat = nullptr, const uint32_t* ncand = nullptr, int32_t* sort_fmin = nullptr,
-                     bool sort_lq = false) {
+                     unsigned long long* stat = nullptr) {
     int32_t *fb, *pb;
     ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
     int16_t* lut; uint32_t* work;
     if (int e = upload_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1, &lut)) return e;
     ENSURE(c->work, uint32_t, 4, work);
-    HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));   // [0..1] k_chain_giant hand-out per pass, [2..3] k_chain_long_mw
+    HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));   // [0..1] k_chain_giant hand-out per pass
     uint32_t* order;
     ENSURE(c->order, uint32_t, n, order);
     int32_t* tmark;
@@ -916,12 +907,8 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                  lazy ? 1u : 0u, nullptr, 0u};
     ca.abort = abort;
     ca.full_dp = full ? 1u : 0u;   // not "no fmin": with pruning off, production still follows the med_pairs knobs
-    ca.ncand = ncand;              // pass 0: the sort's candidate segments / LB (null: every read streams)
     int32_t* fmin_buf = nullptr;
-    if (!full && K[MM2G_KNOB_PRUNE]) {
-        if (sort_fmin) fmin_buf = sort_fmin;   // initialised (and set for its LB reads) by the sort
-        else ENSURE(c->fmin, int32_t, n, fmin_buf);
-    }
+    if (!full && K[MM2G_KNOB_PRUNE]) ENSURE(c->fmin, int32_t, n, fmin_buf);
     uint32_t* item_off;
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
@@ -951,11 +938,8 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         if (mb <= 0) mb = 1024;
         sb = std::max(1, std::min((int)((n * 4 + 3) / 4), sb));   // items: up to ~4 chunks per read
         HIPCHK(hipMemsetAsync(rbest, 0, (size_t)n * 8, c->stream));
-        // long count (pass 0/1 slot), medium count, medium taken; pass 0's long count may hold the
-        // sort's candidate segments already (zeroed before the sort, sort_lb_cands)
-        // (only when the sort ran its LB pass: with sort_lb off a stale count would replay another batch's segments)
-        if (pass == 0 && sort_lq) HIPCHK(hipMemsetAsync(lseg_n + 2, 0, 8, c->stream));
-        else HIPCHK(hipMemsetAsync(lseg_n + pass, 0, 16 - 4 * (size_t)pass, c->stream));
+        // long count (pass 0/1 slot), medium count, medium taken
+        HIPCHK(hipMemsetAsync(lseg_n + pass, 0, 16 - 4 * (size_t)pass, c->stream));
         static const char* names[2][5] = {{"chain_seg", "chain_med", "chain_lorder", "chain_long", "chain_fin"},
                                           {"chain_seg_rescue", "chain_med_rescue", "chain_lorder_rescue", "chain_long_rescue", "chain_fin_rescue"}};
         const int blocks[5] = {sb, mb, 1, lb, 0};
@@ -965,11 +949,15 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         }
         // lower bound of each read's best f: prunes segments (pass 0, not in debug
         // mode; the rescue pass runs on few reads, where it costs more than it saves)
-        // the rescue pass prunes by pass 0's bound: every pass-0 transition is accepted at bw_long
-        // with the same score, so its best f >= LB_1 >= LB_0 = fmin (no k_chain_lb of its own)
-        ca.fmin = (pass == 0 || K[MM2G_KNOB_PRUNE_RESCUE]) ? fmin_buf : nullptr;
+        // the rescue pass prunes by pass 0's bound: when the rescue's comput_sc limits are all at
+        // least pass 0's (bw_long >= bw, max_dist_x/y no smaller), every pass-0 transition is
+        // accepted there with the same score, so its best f >= LB_1 >= LB_0 = fmin (no k_chain_lb
+        // of its own).  The reference accepts -r A,B with B < A (main.rs:205-206): then pass-0
+        // steps with dd in (bw_long, bw] are rejected in the rescue and the bound does not hold.
+        const bool rescue_wider = bw_long >= P0.bw && mdx1 >= P0.max_dist_x && mdy1 >= P0.max_dist_y;
+        ca.fmin = (pass == 0 || (K[MM2G_KNOB_PRUNE_RESCUE] && rescue_wider)) ? fmin_buf : nullptr;
         if (ca.fmin && pass == 0) {
-            if (!sort_fmin) HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
+            HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
             ProfScope ps(c, "chain_lb");
             LCHK(launch_chain_stage(5, ca, 2048, c->stream));
         }
@@ -1004,17 +992,6 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                     ca.giant_gmax = gmax;
                     LCHK(launch_chain_stage(8, ca, gblocks, c->stream));
                 }
-            }
-            // pass 0's longest segments (C5's 100 kb chains): one 8-wave workgroup each
-            if (stg == 2 && pass == 0 && ca.lazy && K[MM2G_KNOB_MW_MIN] > 0) {
-                uint32_t mw = 1;
-                while ((int64_t)mw < K[MM2G_KNOB_MW_MIN] && mw < (1u << 30)) mw <<= 1;   // a power of two (k_chain_long_mw)
-                ca.mw_min = mw;
-                int dev = 0, ncu = 256;
-                if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-                ProfScope ps(c, "chain_long_mw");
-                LCHK(launch_chain_stage(9, ca, std::max(1, ncu) * 4, c->stream));
-                ca.mw_min = 0;
             }
             if (stg == 2) continue;   // launched above
             // k_chain_seg routes a segment to k_chain_med only when its estimated pairs stay
@@ -1248,26 +1225,6 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     const float gap = 0.01f * 0.8f * (float)o->k;
     const int npass = stop_at == 3 ? 1 : 2;
     const bool chain = !stop_after_sort && stop_at != 1 && stop_at != 2;
-    uint32_t* ncand;
-    ENSURE(c->ncand, uint32_t, n, ncand);
-    int32_t* fmin_buf = nullptr;
-    const int16_t* lut_sort = nullptr;
-    if (chain && !full && K[MM2G_KNOB_PRUNE]) {
-        ENSURE(c->fmin, int32_t, n, fmin_buf);
-        if (filt && K[MM2G_KNOB_SORT_LB] && P.lut_n <= SORT_LB_LUT) {
-            int16_t* l;
-            if (int e = upload_lut(c, gap, std::max(o->bw, npass > 1 ? o->bw_long : 0) + 1, &l)) return e;
-            lut_sort = l;
-        }
-    }
-    // the long-segment queue: the sort's LB pass appends pass 0's long candidate segments to it
-    uint4* lseg_q = nullptr; uint32_t* lseg_nq = nullptr;
-    const uint32_t lcap_q = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_TINY + 1) + 64, 0xffffffffu);
-    if (lut_sort) {
-        uint32_t* lo_;
-        ENSURE(c->lseg, uint4, lcap_q, lseg_q); ENSURE(c->lseg_order, uint32_t, lcap_q, lo_); ENSURE(c->lseg_n, uint32_t, 4, lseg_nq);
-        HIPCHK(hipMemsetAsync(lseg_nq, 0, 16, c->stream));
-    }
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
                 filt ? c->dix->cells : 0u, cnt2, smax, (uint32_t)std::min<int64_t>(K[MM2G_KNOB_SORT_SMALL], 4096), nullptr, 0u,
                 (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_SEG_SMALL], SEG_THREAD)), nullptr};
@@ -1276,8 +1233,6 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.rlist = rlist; so.rcount = rlist + n; so.rwork = rlist + n + 1;
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
-    so.ncand = ncand; so.fmin = fmin_buf; so.lut = lut_sort; so.P = P;
-    so.lseg = lseg_q; so.lseg_n = lseg_nq; so.lseg_cap = lcap_q;
     uint64_t* sprof = nullptr;
     if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 192)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 192, c->stream)); so.prof = sprof; }
     if (stop_at != 1) {
@@ -1301,7 +1256,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     if (chain) {
         // 5. chain DP + fallback + rescue
         if (int e = run_chain(c, n, c->d_rd_off, P, gap, npass, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
-                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, full, st, ncand, fmin_buf, lut_sort != nullptr))
+                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, full, st))
             return e;
         // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
         const bool sep = (H.w != o->w || H.k != o->k);
@@ -1317,7 +1272,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         ProfScope ps(c, "dv");
         if (stop_at != 4) LCHK(launch_dv(da, c->stream));
     }
-    LCHK(launch_batch_sums(n, mz_cnt, cnt2, ncand, st, c->stream));
+    LCHK(launch_batch_sums(n, mz_cnt, cnt2, st, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_out, out, (size_t)n * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_stat, st, STAT_WORDS * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipEventRecord(c->ev_done, c->stream));
@@ -1476,8 +1431,8 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     for (int t = 0; t < 6; ++t) c->counters[t] = cnt[t];
     c->counters[6] = c->h_stat[4];    // anchors left after the sort's singleton filter (the DP input)
     for (int t = 0; t < 6; ++t) c->counters[7 + t] = c->h_stat[8 + t];   // anchors per chain kernel class and pass
-    c->counters[13] = c->h_stat[5];   // DP anchors in reads k_chain_seg streams (no candidate list from the sort)
-    c->counters[14] = c->h_stat[6];   // ... in reads k_chain_lb runs on (no LB from the sort)
+    c->counters[13] = c->h_stat[4];   // DP anchors whose keys k_chain_seg streams (pass 0)
+    c->counters[14] = c->h_stat[4];   // ... that k_chain_lb streams (pass 0)
     return 0;
 }
 

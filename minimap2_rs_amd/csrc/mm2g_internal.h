@@ -173,22 +173,7 @@ struct SortArgs {
     uint32_t* rcount = nullptr;
     const uint32_t* order = nullptr;   // k_sort_read: block b sorts read order[b] (heaviest first); null = b
     uint32_t* rwork = nullptr;         // k_sort_big: next list entry to take (zeroed by k_sort_small)
-    // Pass-0 DP lower bound and candidate segments (k_sort_read, DESIGN.md
-    // "Chain DP from the sort"): per read the LB of k_chain_lb over the whole
-    // sorted read (fmin) and the segments that can hold the best f (len * span
-    // >= fmin), written as u16 start | u16 length << 16 over the read's own
-    // (dead) unsorted-key region; ncand: their count, or NC_STREAM / NC_STREAM_LB
-    uint32_t* ncand = nullptr;         // per read (k_sort_small initialises every read to NC_STREAM)
-    int32_t* fmin = nullptr;           // null: no LB / candidates (debug mode, pruning off)
-    const int16_t* lut = nullptr;      // comput_sc pen LUT of pass 0 (lut_n entries)
-    ChainKParams P{};                  // pass-0 chain parameters (max_dist_x/y, bw, span, lut_n)
-    uint4* lseg = nullptr;             // pass 0's long-segment queue (ChainArgs::lseg): candidates of more than
-    uint32_t* lseg_n = nullptr;        //   CHAIN_TINY anchors go there directly, only shorter ones to k_chain_seg
-    uint32_t lseg_cap = 0;
 };
-constexpr uint32_t NC_STREAM = 0xffffffffu;      // no LB from the sort: k_chain_lb + streaming k_chain_seg
-constexpr uint32_t NC_STREAM_LB = 0xfffffffeu;   // fmin from the sort (k_chain_lb skips the read), streaming k_chain_seg
-constexpr int SORT_LB_LUT = 8192;                // the sort's LB pass keeps the pen LUT in LDS up to this many entries
 struct ChainArgs {
     uint32_t n;
     const uint64_t* rd_off;
@@ -230,8 +215,6 @@ struct ChainArgs {
     uint32_t spec_rounds = 3; // k_chain_long: speculative rounds per 64-anchor block (MM2G_KNOB_SPEC_ROUNDS)
     int32_t est_lane = 0;    // k_chain_seg (production): estimated DP pairs up to which a segment takes one lane
     uint32_t full_dp = 0;    // debug mode (exact f/pprev everywhere): pass 0 uses EST_LANE instead of est_lane
-    uint32_t mw_min = 0;     // k_chain_long_mw: segments of >= this many anchors (a power of two; 0 = off)
-    const uint32_t* ncand = nullptr;   // pass 0: per read NC_STREAM, NC_STREAM_LB or the sort's candidate count (SortArgs)
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
     const uint32_t* abort = nullptr;
     unsigned long long* gprof = nullptr;   // MM2G_LSEG_PROF: k_chain_giant phase sums (16 counters)
@@ -271,7 +254,7 @@ int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k, uint64_t cap, uint32_t* status,
                      uint32_t bit, int slot, hipStream_t st);
 // per-batch sums for the counters: status64[3] = sum mz_cnt, status64[4] = sum cnt2
-int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, const uint32_t* ncand, unsigned long long* status64, hipStream_t st);
+int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st);
 // minimizer slots: read r gets [rd_off[r] + 16r, rd_off[r+1] + 16(r+1)), or `slot` entries each when non-zero (tests)
 int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st);
 // query sketch views: per-read view counts; view table from their exclusive scan vo; per-read concatenation

@@ -880,22 +880,12 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
 //   one 1024-thread workgroup per read, stable ranking by wave match.
 // ============================================================================
 constexpr int SORT_SMALL = 4096;
-constexpr int SMALL_LB_LUT = 1024;        // k_sort_small's LB pass: pen LUT entries it keeps in static LDS
-template <int NT, typename KP>
-DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint32_t A, unsigned char* lds,
-                        uint32_t* w4, uint32_t* s_sc, uint64_t* pq);
-
-template <bool LB>   // LB: the instance with the LB pass (static LDS and registers only there)
 __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) { *a.rcount = 0; if (a.rwork) *a.rwork = 0; }   // k_sort_read's list for k_sort_radix / k_sort_big
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint64_t s[SORT_SMALL];
     const uint32_t r = blockIdx.x;
     if (r >= a.n) return;
-    if (threadIdx.x == 0) {   // k_sort_read overwrites both for the reads whose LB pass it runs
-        if (a.ncand) a.ncand[r] = NC_STREAM;
-        if (a.fmin) a.fmin[r] = 0;
-    }
     const uint64_t base = a.a_off[r];
     const uint32_t A = (uint32_t)(a.a_off[r + 1] - base);
     if (A > a.small_max) return;
@@ -920,13 +910,6 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
         }
     }
     for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) a.tmp[CK(base + i, a.cap_keys)] = s[i];   // sorted keys live in tmp
-    // pass-0 LB and candidate segments from the sorted keys in LDS (as k_sort_read; the unsorted
-    // keys in HBM are dead now and receive the candidate list)
-    if constexpr (LB) if (a.lut && a.fmin && a.ncand && a.P.lut_n <= SMALL_LB_LUT) {
-        __shared__ __align__(16) unsigned char s_lb[SMALL_LB_LUT * 2 + SORT_SMALL / 8];
-        __shared__ uint32_t s_w4[32], s_sc4[16];
-        sort_lb_cands<256>(a, r, (const uint64_t*)s, (uint32_t*)(K + base), A, s_lb, s_w4, s_sc4, nullptr);
-    }
 }
 
 // ---- per-read sort of the large reads (A0 > small_max): cell buckets.
@@ -1258,7 +1241,7 @@ DEVI void radix_range(uint64_t* src, uint64_t* dst, uint64_t* out, uint32_t A, u
     __syncthreads();
 }
 
-// ---- DPP helpers (wave scans) of the sort's LB pass and the chain kernels
+// ---- DPP helpers (wave scans) of the chain kernels
 template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
 DEVI int32_t dpp(int32_t old, int32_t src) { return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, BANK_MASK, false); }
 // inclusive max-scan over the wave (row_shr 1/2/4/8, row_bcast 15/31)
@@ -1304,218 +1287,11 @@ DEVI void scan_lb(int32_t& a, int32_t& b) {
 #undef LB_STEP
 }
 
-// ---- Chain DP from the sort: the pass-0 lower bound of the read's best f and
-// the segments that can hold it, from the read's sorted keys O[0, A) (complete).
-//   LB[i] = max(span, LB[i-1] + sc(i, i-1)) (k_chain_lb, lchain.rs:73-90: the
-//   first predecessor visited is i-1 and n_skip needs > max_skip visits), a
-//   composition of x -> max(x + a, b).  Each wave walks a contiguous range of
-//   64-key chunks (DPP scan per chunk, the range's composition carried in
-//   registers, U chunks' loads in flight) and keeps max_i A_i and max_i B_i of
-//   its prefix compositions (A_i, B_i); one exchange of the waves' (A, B, maxA,
-//   maxB) then gives max LB over the whole read = max_w max(x_w + maxA_w, maxB_w)
-//   with x_w the LB entering wave w.  k_chain_lb restarts at every 4096-anchor
-//   work item, so this bound is at least as large.
-//   Segments run from an isolated anchor (lchain.rs:75: i == 0, another group,
-//   or rpos_i > rpos_{i-1} + max_dist_x) to the next; one of len anchors has f
-//   <= len * span, so only those with len * span >= max LB can hold the read's
-//   best f or a tie of it (k_chain_seg's pruning rule, with the same bound).
-// The isolated anchors form a bitmap in LDS; each thread takes a run of its
-// words, finds the next start after its last one by a block suffix-min, and
-// the candidates go out as u32 pairs (start, len) to Kc (the read's own
-// unsorted-key region, dead now: <= A segments, 2 words each) in position order, with their count in
-// ncand[r] -- or NC_STREAM_LB when there are more than `budget` (k_chain_seg
-// then streams the read: many one-segment items would cost more).  fmin[r] =
-// max LB either way.  LDS: the pen LUT, then ceil(A / 64) u64 bitmap words;
-// w4: 5 NW words of static LDS.
-// LB recurrence state carried into a range of sorted keys: the composition
-// entering it (block-uniform), each thread's best so far, the key before it.
-struct LbState { int32_t carry, best; uint64_t prev; };
-
-// The LB scan over n sorted keys O[0, n) at read position gbase (a multiple of
-// 64): isolated-anchor bits into isob per chunk, the composition carried in st.
-// (Measured: the same scan over each k_sort_read window in LDS costs as much as
-// over O, ~15 us per read at the sort's 4 waves per SIMD)
-template <int NT, typename KP>
-DEVI void lb_scan(const SortArgs& a, KP O, uint32_t n, uint32_t gbase, const int16_t* lut, uint64_t* isob, uint32_t* w4, LbState& st) {
-    constexpr int NW = NT / 64;
-    constexpr int32_t NEG = -(1 << 29);
-    constexpr int U = 8;                           // chunks per wave per round, all independent (loads in flight together)
-    const int lane = lane_id(), wv = wave_id();
-    const ChainKParams P = a.P;                   // a copy: a reference into the kernel argument forces it to scratch
-    const uint32_t qb = a.qb, gsh = a.qb + a.rb;
-    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << a.rb) - 1;
-    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
-    const uint32_t nwd = (n + 63) >> 6;
-    int32_t* wca = (int32_t*)w4;                  // [NW] the waves' round compositions (a, b)
-    int32_t* wcb = wca + NW;
-    // Rounds of NW * U chunks: wave w takes chunks c = c0 + w*U + u.  Each chunk's
-    // inclusive composition scan (lane l: the composition of its lanes 0..l) stays
-    // in registers until the LB entering the chunk is known (a scan over the
-    // chunks' totals: in the wave, then across the waves through LDS); nothing
-    // is carried from chunk to chunk inside a wave.
-    int32_t carry = st.carry, best = st.best;
-    const uint64_t prev = st.prev;
-    for (uint32_t c0 = 0; c0 < nwd; c0 += NW * U) {
-        int32_t sa[U], sb[U];
-        uint64_t kk[U], pv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t cc = c0 + (uint32_t)(wv * U + u), i = cc * 64 + (uint32_t)lane;
-            kk[u] = (cc < nwd && i < n) ? O[i] : 0;
-            pv[u] = (cc < nwd && cc > 0) ? O[cc * 64 - 1] : prev;   // the chunk's predecessor key (same address on every lane)
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t cc = c0 + (uint32_t)(wv * U + u), i = cc * 64 + (uint32_t)lane;
-            const bool valid = cc < nwd && i < n;
-            const uint64_t ak = kk[u];
-            const uint64_t pk = ((uint64_t)(uint32_t)shr1_dpp((int32_t)(uint32_t)(ak >> 32), (int32_t)(uint32_t)(pv[u] >> 32)) << 32) |
-                                (uint32_t)shr1_dpp((int32_t)(uint32_t)ak, (int32_t)(uint32_t)pv[u]);
-            const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
-            const int32_t p = (int32_t)((ak >> qb) & rmask), pj = (int32_t)((pk >> qb) & rmask);
-            const int32_t q = (int32_t)(ak & qmask), qj = (int32_t)(pk & qmask);
-            const bool iso = valid && (gbase + i == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx));
-            int32_t xa = valid ? NEG : 0, xb = valid ? span : NEG;   // invalid lanes: the identity
-            if (valid && !iso) {   // comput_sc (lchain.rs:17-34) of (i, i-1); the LUT is (gap*dd + 0.5*log2(dd+1)) as i32
-                const int32_t dq = q - qj, dr = p - pj;
-                const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-                if (dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw) {
-                    const int32_t dg = dr < dq ? dr : dq;
-                    xa = (span < dg ? span : dg) - (int32_t)lut[dd];
-                }
-            }
-            scan_lb(xa, xb);
-            sa[u] = xa; sb[u] = valid ? xb : NEG;      // sb of an invalid lane never counts for the best
-            const uint64_t im = ballot(iso);
-            if (lane == 0 && cc < nwd) isob[cc] = im;
-        }
-        // the wave's composition over its U chunks (lane 63 of each), in chunk order
-        int32_t ra = 0, rb = NEG;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t ca = rdl(sa[u], 63), cb = rdl(sb[u], 63);
-            rb = max(rb + ca, cb); ra = max(ra + ca, NEG);
-        }
-        __syncthreads();                           // the previous round's readers are done with wca / wcb
-        if (lane == 0) { wca[wv] = ra; wcb[wv] = rb; }
-        __syncthreads();
-        int32_t x = carry;
-        for (int w2 = 0; w2 < wv; ++w2) x = max(max(x + wca[w2], NEG), wcb[w2]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            best = max(best, max(x + sa[u], sb[u]));
-            x = max(max(x + rdl(sa[u], 63), NEG), rdl(sb[u], 63));
-        }
-        int32_t xc = carry;
-        for (int w2 = 0; w2 < NW; ++w2) xc = max(max(xc + wca[w2], NEG), wcb[w2]);
-        carry = xc;
-    }
-    st.carry = carry; st.best = best;
-    if (n) st.prev = O[n - 1];
-}
-
-// The candidate segments from the isolated-anchor bitmap isob (A bits) and the
-// threads' LB maxima (see sort_lb_cands).
-template <int NT>
-DEVI void lb_finish(const SortArgs& a, uint32_t r, const uint64_t* isob, uint32_t* Kc, uint32_t A, int32_t best,
-                    uint32_t* w4, uint32_t* s_sc, uint64_t* pq, uint64_t t_lb0) {
-    constexpr int NW = NT / 64;
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const int32_t span = a.P.span;
-    const uint32_t nwd = (A + 63) >> 6;
-    int32_t* wca = (int32_t*)w4;
-    __syncthreads();                               // bitmap complete
-    best = rdl(scan_max(best), 63);
-    int32_t* wmx = wca + 2 * NW;
-    if (lane == 0) wmx[wv] = best;
-    __syncthreads();
-    for (int w2 = 0; w2 < NW; ++w2) best = max(best, wmx[w2]);
-    if (pq && tid == 0) { const uint64_t t_ = wall_clock64(); pq[16] += t_ - t_lb0; }
-    // segment starts: thread t takes bitmap words [t * wpt, t * wpt + wpt)
-    const uint32_t wpt = (nwd + NT - 1) / NT;
-    const uint32_t wa0 = min(nwd, (uint32_t)tid * wpt), wb0 = min(nwd, wa0 + wpt);
-    uint32_t fpos = A;                             // my first start
-    for (uint32_t w = wa0; w < wb0 && fpos == A; ++w) { const uint64_t m = isob[w]; if (m) fpos = w * 64 + (uint32_t)__builtin_ctzll(m); }
-    // next start after my words: exclusive suffix min over the threads
-    uint32_t v = fpos;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) { const uint32_t o = (uint32_t)__shfl_down((int)v, d, 64); if (lane + d < 64) v = min(v, o); }
-    uint32_t* wmin = w4 + 4 * NW;
-    if (lane == 0) wmin[wv] = v;
-    uint32_t after = (uint32_t)__shfl_down((int)v, 1, 64);
-    __syncthreads();
-    if (lane == 63) after = A;
-    for (int t = wv + 1; t < NW; ++t) after = min(after, wmin[t]);
-    const int64_t need = best;
-    // a candidate has >= Lmin anchors; from Lmin >= 64 on only the last start of
-    // a word can begin one (any other start's segment ends inside the word)
-    const bool top_only = (int64_t)63 * span < need;
-    auto visit = [&](auto&& fn) {
-        for (uint32_t w = wa0; w < wb0; ++w) {
-            const uint64_t m0 = isob[w];
-            if (!m0) continue;
-            uint64_t m = top_only ? (1ULL << (63 - __builtin_clzll(m0))) : m0;
-            while (m) {
-                const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1;
-                const uint64_t rest = b == 63 ? 0ULL : (m0 >> (b + 1)) << (b + 1);
-                uint32_t e = after;
-                if (rest) e = w * 64 + (uint32_t)__builtin_ctzll(rest);
-                else for (uint32_t w2 = w + 1; w2 < wb0; ++w2) { const uint64_t m2 = isob[w2]; if (m2) { e = w2 * 64 + (uint32_t)__builtin_ctzll(m2); break; } }
-                const uint32_t sk = w * 64 + b;
-                if ((int64_t)(e - sk) * span >= need) fn(sk, e);
-            }
-        }
-    };
-    uint32_t mine = 0;
-    visit([&](uint32_t, uint32_t) { ++mine; });
-    uint32_t tot;
-    (void)block_excl_sum<NW>(mine, tot, s_sc);
-    const uint32_t budget = A / 32u + 8u;
-    // long candidates (the usual one or two per read) go straight to pass 0's long-segment queue
-    // (k_chain_long, as k_chain_seg's route() would send them: production sends every segment over
-    // CHAIN_TINY anchors to a wave); k_chain_seg gets only the tiny ones as work items
-    uint32_t ntiny = 0;
-    if (tot <= budget) {                           // block-uniform: block_excl_sum holds barriers
-        uint32_t nt = 0;
-        if (mine) visit([&](uint32_t sk, uint32_t e) { if (e - sk <= (uint32_t)CHAIN_TINY || !a.lseg) ++nt; });
-        uint32_t ot = block_excl_sum<NW>(nt, ntiny, s_sc);
-        if (mine) visit([&](uint32_t sk, uint32_t e) {
-            if (e - sk <= (uint32_t)CHAIN_TINY || !a.lseg) { Kc[2 * ot] = sk; Kc[2 * ot + 1] = e - sk; ++ot; }
-            else {
-                const uint32_t qq = atomicAdd(a.lseg_n, 1u);
-                if (qq < a.lseg_cap) a.lseg[qq] = make_uint4(r, sk, e, 0u);
-            }
-        });
-    }
-    if (tid == 0) { a.fmin[r] = best; a.ncand[r] = tot <= budget ? ntiny : NC_STREAM_LB; }
-    if (pq && tid == 0) { pq[17] += wall_clock64() - t_lb0; pq[18] = tot; }
-}
-
-
-template <int NT, typename KP>
-DEVI void sort_lb_cands(const SortArgs& a, uint32_t r, KP O, uint32_t* Kc, uint32_t A, unsigned char* lds,
-                        uint32_t* w4, uint32_t* s_sc, uint64_t* pq) {
-    constexpr int32_t NEG = -(1 << 29);
-    const int tid = threadIdx.x;
-    int16_t* lut = (int16_t*)lds;
-    uint64_t* isob = (uint64_t*)(lds + (((a.P.lut_n * 2) + 15) & ~15));
-    load_lut(lut, a.lut, a.P.lut_n);
-    __syncthreads();
-    const uint64_t t_lb0 = pq && tid == 0 ? wall_clock64() : 0;
-    LbState st{NEG, a.P.span, 0};
-    lb_scan<NT>(a, O, A, 0u, lut, isob, w4, st);
-    lb_finish<NT>(a, r, isob, Kc, A, st.best, w4, s_sc, pq, t_lb0);
-}
-
 // GL: the group offsets stay in HBM (2 n_seq + 2 > GOFF_LDS).  A template
 // parameter rather than a pointer chosen at run time: a pointer that may be
 // LDS or global compiles to flat loads, and every flat load waits for all
 // outstanding global loads and stores (vmcnt(0)), which serialised P1/P2 per key.
-// LB: the instance with the pass-0 LB pass (MM2G_KNOB_SORT_LB); the other one
-// keeps its registers (89 VGPRs against 120), so other contexts' waves still fit
-// beside a sorting workgroup.
-template <bool GL, int NT, bool LB>
+template <bool GL, int NT>
 __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
     constexpr int NW = NT / 64;
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
@@ -1820,12 +1596,6 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 }
             }
             SORT_PH(6);
-            // pass-0 LB and candidate segments (k_chain_lb / k_chain_seg's scan, fused)
-            if (LB && a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
-                __syncthreads();                   // O complete (rank phase, P4b) and visible to the block
-                sort_lb_cands<NT>(a, r, (const uint64_t*)O, (uint32_t*)K, A, (unsigned char*)dyn64, s_goff, s_sc, pq);
-                SORT_PH(3);
-            }
             SORT_END(nbig, A);
             return;
         }
@@ -1971,7 +1741,6 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
     __shared__ uint32_t s_sc[16], s_read, s_nbig;
     __shared__ uint2 s_big[BIG_MAX];
     __shared__ uint32_t s_goff[GOFF_LDS];
-    __shared__ uint32_t s_w4[5 * 16];              // sort_lb_cands' wave words (s_goff stays live across reads)
     extern __shared__ uint64_t dyn64[];
     uint32_t* dyn = (uint32_t*)dyn64;
     const int tid = threadIdx.x, lane = lane_id();
@@ -2219,11 +1988,6 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
             BIG_PH(6);
             ba = bb;
         }
-        // pass-0 LB and candidate segments, as k_sort_read (K, radix_big's scratch, is dead now)
-        if (a.lut && a.fmin && a.ncand && ((((uint32_t)a.P.lut_n * 2u + 15u) & ~15u) + 8u * ((A + 63u) >> 6)) <= LW * 4u) {
-            __syncthreads();
-            sort_lb_cands<1024>(a, r, (const uint64_t*)O, (uint32_t*)K, A, (unsigned char*)dyn64, s_w4, s_sc, pq);
-        }
         if (pq && tid == 0) { pq[8] = A0; pq[9] = (0xfffeULL << 32) | A; pq[11] = wall_clock64(); }
 #undef BIG_PH
     }
@@ -2259,7 +2023,8 @@ constexpr int RING_WORDS = 256;   // 8192-bit mark ring (max_iter <= 8000)
 constexpr int RK = 256;           // anchor ring entries per wave (power of two, >= 256)
 static_assert((RK & (RK - 1)) == 0 && RK >= 256, "anchor ring size");
 
-constexpr uint32_t LSEG_DONE = 0xffffffffu;   // lseg[].w: handled by k_chain_giant
+constexpr uint32_t LSEG_DONE = 0x80000000u;   // lseg[].w bit: handled by k_chain_giant (low 31 bits: its wall-clock
+                                              // ticks under MM2G_LSEG_PROF; k_chain_long's own ticks otherwise)
 constexpr int TINY = CHAIN_TINY;  // segments up to this many anchors: one lane, registers
 constexpr int MED = CHAIN_MED;    // up to this many: one lane, state machine over HBM; longer: whole wave
 
@@ -2356,9 +2121,7 @@ __global__ __launch_bounds__(1024) void k_seg_items(ChainArgs a) {
         if (t < a.n) {
             const uint32_t r = a.order[t];
             const bool on = a.P.pass == 0 || (a.out[r].flags & RF_RESCUED);
-            const uint32_t nc = (a.P.pass == 0 && a.ncand) ? a.ncand[r] : NC_STREAM;
-            // the sort's candidate segments (one item each), else 4096-anchor chunks
-            c = !on ? 0u : nc < NC_STREAM_LB ? nc : (a.cnt2[r] + a.seg_chunk - 1) / a.seg_chunk;
+            c = !on ? 0u : (a.cnt2[r] + a.seg_chunk - 1) / a.seg_chunk;   // seg_chunk-anchor chunks
         }
         uint32_t wt;
         const uint32_t ex = wave_excl_sum(c, wt);
@@ -2429,19 +2192,9 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
         if (t < (uint32_t)a.n_prio) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
         const uint64_t base = uni64(a.a_off[r]);
-        const uint32_t nc = (a.ncand && P.pass == 0) ? (uint32_t)uni((int32_t)a.ncand[r]) : NC_STREAM;
-        int32_t c0, c1, A;
-        if (nc < NC_STREAM_LB) {
-            // one candidate segment [s, s + len) of the sort (sort_lb_cands), in the
-            // read's dead unsorted-key region (now a.chain's): streamed as if it
-            // were the whole read, so exactly it is routed
-            c0 = uni((int32_t)a.chain[2 * base + 2 * j]);
-            A = c0 + uni((int32_t)a.chain[2 * base + 2 * j + 1]); c1 = A;
-        } else {
-            c0 = (int32_t)j * (int32_t)a.seg_chunk;
-            A = (int32_t)uni((int32_t)a.cnt2[r]);      // anchors kept by the singleton filter
-            c1 = min(A, c0 + (int32_t)a.seg_chunk);
-        }
+        const int32_t c0 = (int32_t)j * (int32_t)a.seg_chunk;
+        const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);      // anchors kept by the singleton filter
+        const int32_t c1 = min(A, c0 + (int32_t)a.seg_chunk);
         if (c0 >= A) continue;
 #ifdef MM2G_CHECKED
         if (base + (uint64_t)A > a.cap_keys) { if (lane == 0) CK(base + A, a.cap_keys); continue; }
@@ -2632,7 +2385,6 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + wave_id(); it < n_items; it += nwaves) {
         const uint32_t t = (uint32_t)uni((int32_t)((a.item_read && it < a.item_cap) ? a.item_read[it] : item_owner(a.item_off, a.n, it)));
         const uint32_t r = (uint32_t)uni((int32_t)a.order[t]);
-        if (a.ncand && (uint32_t)uni((int32_t)a.ncand[r]) != NC_STREAM) continue;   // the sort set fmin[r] (a larger bound)
         const int32_t c0 = (int32_t)(it - (uint32_t)uni((int32_t)a.item_off[t])) * (int32_t)a.seg_chunk;
         const uint64_t base = uni64(a.a_off[r]);
         const int32_t A = min((int32_t)uni((int32_t)a.cnt2[r]), c0 + (int32_t)a.seg_chunk);
@@ -2835,239 +2587,6 @@ __global__ __launch_bounds__(1024) void k_lseg_order(ChainArgs a) {
     }
 }
 
-// ---- 5b'. the longest pass-0 segments, one 8-wave workgroup each (C5's
-// ~28 k-anchor chains): k_chain_long's speculative 64-anchor block pass spread
-// over a window of MW_NW blocks.  Per window [W0, W0 + 512): every anchor gets
-// the k_chain_lb guess (a composition scan across the window, seeded with the
-// exact f of W0 - 1); then in each round every lane runs the reference loop
-// (lchain.rs:76-89) of its anchor over its 64 nearest predecessors on the
-// current guesses (Jacobi), and everything before the window's first anchor
-// whose result differs from its guess -- and that anchor, unless its loop
-// reaches past 64 predecessors ("deep") -- is exact and committed (the same
-// induction as k_chain_long's, over the whole window).  A deep anchor at the
-// front of the window gets the reference loop from one thread (marks in an LDS
-// bitmap, predecessors exact).  Segments handled here are marked LSEG_DONE for
-// k_chain_long.  Segments are taken longest first; the list's log2-length
-// buckets make "shorter than mw_min (a power of two)" the end of the work.
-constexpr int MW_NW = 8;                  // waves per workgroup: blocks per window
-constexpr int MW_WIN = MW_NW * 64;
-constexpr int MW_RK = 1024;               // anchor ring (keys, f/pprev): >= window + 64 predecessors + the previous window
-constexpr int MW_MKW = 160;               // mark bitmap words of the one-thread path (max_iter <= 5120)
-static_assert(MW_RK >= 2 * MW_WIN, "ring holds the window and the window before it");
-__global__ __launch_bounds__(MW_NW * 64) void k_chain_long_mw(ChainArgs a) {
-    if (a.abort && (*a.abort & BS_ANCHORS)) return;
-    extern __shared__ __align__(16) unsigned char smem[];
-    __shared__ int32_t s_ca[MW_NW], s_cb[MW_NW];
-    __shared__ uint32_t s_bad[MW_NW], s_q;
-    __shared__ uint32_t s_mk[MW_MKW];
-    __shared__ unsigned long long s_best;
-    const ChainKParams P = a.P;
-    int16_t* lut = (int16_t*)smem;
-    const int lut_bytes = ((P.lut_n * 2) + 15) & ~15;
-    uint64_t* rkey = (uint64_t*)(smem + lut_bytes);
-    int2* rfp = (int2*)(rkey + MW_RK);
-    const uint32_t nl = min(*a.lseg_n, a.lseg_cap);
-    if (nl == 0 || a.mw_min == 0) return;
-    {   // the longest segment is first: nothing to do below mw_min
-        const uint4 L0 = a.lseg[a.lseg_order[0]];
-        if (L0.z - L0.y < a.mw_min) return;
-    }
-    load_lut(lut, a.lut, P.lut_n);
-    __syncthreads();
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const uint32_t qb = a.kl.qb, rb = a.kl.rb;
-    const uint64_t qmask = (1ULL << qb) - 1, rmask = (1ULL << rb) - 1;
-    const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
-    constexpr int32_t NEG = -(1 << 29);
-    constexpr uint32_t RM = MW_RK - 1;
-    auto sc_of = [&](uint64_t ki, uint64_t kj, bool& ok) -> int32_t {   // comput_sc (lchain.rs:17-34), LUT penalty
-        const int32_t dq = (int32_t)(ki & qmask) - (int32_t)(kj & qmask), dr = (int32_t)((ki >> qb) & rmask) - (int32_t)((kj >> qb) & rmask);
-        const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-        ok = dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
-        const int32_t dg = dr < dq ? dr : dq;
-        return (span < dg ? span : dg) - (int32_t)lut[ok ? dd : 0];
-    };
-    for (;;) {
-        __syncthreads();
-        if (tid == 0) s_q = atomicAdd(&a.work[2 + (P.pass & 1)], 1u);
-        __syncthreads();
-        const uint32_t t = s_q;
-        if (t >= nl) break;
-        const uint32_t q = a.lseg_order[t];
-        const uint4 L = a.lseg[q];
-        if (L.z - L.y < a.mw_min) break;            // every later one is shorter
-        if (L.w == LSEG_DONE) continue;
-        const uint32_t r = L.x;
-        const int32_t s = (int32_t)L.y, e = (int32_t)L.z;
-        const uint64_t base = a.a_off[r];
-        const uint64_t* K = a.keys + base;
-        int32_t* F = a.f + base; int32_t* PP = a.pp + base;
-        int32_t bf = INT_MIN, bi = -1;
-        uint64_t pairs = 0;
-        if (tid == 0) {                             // anchor s: isolated
-            rkey[s & RM] = K[s]; rfp[s & RM] = make_int2(span, -1);
-            F[s] = span; PP[s] = -1;
-            best_merge(bf, bi, span, s);
-            s_best = 0;
-        }
-        int32_t committed = s + 1;
-        while (committed < e) {
-            const int32_t W0 = committed, W1 = min(e, W0 + MW_WIN);
-            const int32_t k = W0 + tid;
-            const bool kv = k < W1;
-            const uint64_t ak = kv ? K[k] : 0;
-            if (kv) rkey[k & RM] = ak;
-            __syncthreads();
-            // predecessors within reach: j in [max(st_k, k - max_iter), k-1]; 65 = more than 64
-            int32_t dlim = 0;
-            const int32_t pk = (int32_t)((ak >> qb) & rmask);
-            if (kv) {
-                const int32_t b0 = max(s, k - 64);
-                const int32_t pb = (int32_t)((rkey[b0 & RM] >> qb) & rmask);
-                int32_t stk = b0;
-                if (pk > (int32_t)((uint32_t)pb + (uint32_t)maxdx)) {
-                    int32_t pos = b0;
-#pragma unroll
-                    for (int stp = 32; stp >= 1; stp >>= 1) {
-                        const int32_t m = pos + stp;
-                        const int32_t pm = (int32_t)((rkey[(m < k ? m : k) & RM] >> qb) & rmask);
-                        if (m < k && pk > (int32_t)((uint32_t)pm + (uint32_t)maxdx)) pos = m;
-                    }
-                    stk = pos + 1;
-                }
-                int32_t nc = (stk == b0 && b0 > s) ? 65 : k - stk;
-                dlim = nc < P.max_iter ? nc : P.max_iter;
-            }
-            // first guess: the chain through k-1, a composition scan over the window
-            {
-                bool okp = false;
-                int32_t scp = 0;
-                if (kv && dlim >= 1) scp = sc_of(ak, rkey[(k - 1) & RM], okp);
-                int32_t ga = kv ? (okp ? scp : NEG) : 0, gb = kv ? (okp ? NEG : span) : NEG;
-                scan_lb(ga, gb);
-                if (lane == 63) { s_ca[wv] = ga; s_cb[wv] = gb; }
-                __syncthreads();
-                int32_t x = rfp[(W0 - 1) & RM].x;
-                for (int w2 = 0; w2 < wv; ++w2) x = max(max(x + s_ca[w2], NEG), s_cb[w2]);
-                if (kv) rfp[k & RM] = make_int2(max(x + ga, gb), okp ? k - 1 : -1);
-            }
-            __syncthreads();
-            int32_t comm = W0;
-            bool stuck = false;                     // the window's first unsettled anchor is deep
-            for (int rnd = 0; rnd < 8; ++rnd) {
-                const bool act0 = kv && k >= comm;
-                int32_t mf = span, mj = -1, ns = 0, vis = 0;
-                uint64_t mkm = 0;
-                bool brk = false;
-                for (int d0 = 1; d0 <= 64; d0 += 4) {
-                    if (!any(act0 && !brk && d0 <= dlim)) break;
-                    int32_t sv4[4], pp4[4];
-                    bool ok4[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int d = d0 + u;
-                        const bool inr = act0 && d <= dlim;
-                        const int32_t j = k - d;
-                        uint64_t kj = 0;
-                        int2 fpj = make_int2(0, -1);
-                        if (inr) { kj = rkey[j & RM]; fpj = rfp[j & RM]; }
-                        bool ok;
-                        const int32_t sc = sc_of(ak, kj, ok);
-                        ok4[u] = inr && ok;
-                        sv4[u] = sc + fpj.x;
-                        pp4[u] = fpj.y;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int d = d0 + u;
-                        const bool act = act0 && !brk && d <= dlim;
-                        vis += act ? 1 : 0;
-                        if (act && ok4[u]) {
-                            if (sv4[u] > mf) { mf = sv4[u]; mj = k - d; if (ns > 0) --ns; }
-                            else if ((mkm >> (d - 1)) & 1ULL) { ++ns; if (ns > P.max_skip) brk = true; }
-                            if (!brk && pp4[u] >= 0) { const int32_t tt = k - pp4[u]; if (tt <= 64) mkm |= 1ULL << ((tt - 1) & 63); }
-                        }
-                    }
-                }
-                const bool deep = act0 && !brk && dlim > 64;
-                const int2 gv = act0 ? rfp[k & RM] : make_int2(0, 0);
-                const bool bad = act0 && (deep || mf != gv.x || mj != gv.y);
-                const uint64_t badM = ballot(bad), deepM = ballot(deep);
-                if (lane == 0) s_bad[wv] = badM ? ((uint32_t)(wv * 64 + ctz64(badM)) | (((deepM >> ctz64(badM)) & 1ULL) ? 0x80000000u : 0u)) : 0x7fffffffu;
-                __syncthreads();                    // every lane has read rfp; the first bad anchors are known
-                uint32_t fbw = 0x7fffffffu;
-                for (int w2 = 0; w2 < MW_NW; ++w2) { const uint32_t v = s_bad[w2]; if ((v & 0x7fffffffu) < (fbw & 0x7fffffffu)) fbw = v; }
-                const bool fb_deep = fbw != 0x7fffffffu && (fbw & 0x80000000u);
-                const int32_t fb = fbw == 0x7fffffffu ? W1 : W0 + (int32_t)(fbw & 0x7fffffffu);
-                const int32_t cend = fb_deep ? fb : (fb < W1 ? fb + 1 : W1);
-                pairs += (act0 && k < cend) ? (uint64_t)vis : 0ull;
-                if (act0 && k >= fb && !deep) rfp[k & RM] = make_int2(mf, mj);   // fb exact, later lanes the next guess
-                __syncthreads();
-                comm = cend;
-                if (comm >= W1) break;
-                if (fb_deep) { stuck = true; break; }
-            }
-            // commit [W0, comm)
-            if (kv && k < comm) {
-                const int2 v = rfp[k & RM];
-                F[k] = v.x; PP[k] = v.y;
-                best_merge(bf, bi, v.x, k);
-            }
-            if (stuck) {
-                // the reference loop for anchor c = comm, one thread; every predecessor is exact
-                __syncthreads();                    // F/PP of this window's committed anchors written
-                if (tid == 0) {
-                    const int32_t c = comm;
-                    const uint64_t kc = rkey[c & RM];
-                    const int32_t pc = (int32_t)((kc >> qb) & rmask);
-                    int32_t lo = s, hi = c;         // st_c: the first j >= s with pc <= p_j + maxdx (keys sorted by p)
-                    while (lo < hi) {
-                        const int32_t m = (lo + hi) >> 1;
-                        const uint64_t km = m >= W0 - MW_WIN ? rkey[m & RM] : K[m];
-                        if (pc > (int32_t)((uint32_t)(int32_t)((km >> qb) & rmask) + (uint32_t)maxdx)) lo = m + 1; else hi = m;
-                    }
-                    const int32_t jlo = max(lo, c - P.max_iter);
-                    const int32_t nwd = (c - jlo + 31) >> 5;
-                    for (int32_t w2 = 0; w2 < nwd && w2 < MW_MKW; ++w2) s_mk[w2] = 0;
-                    int32_t mf = span, mj = -1, ns = 0;
-                    for (int32_t j = c - 1; j >= jlo; --j) {
-                        const bool in_ring = j >= W0 - MW_WIN;
-                        const uint64_t kj = in_ring ? rkey[j & RM] : K[j];
-                        const int2 fpj = in_ring ? rfp[j & RM] : make_int2(F[j], PP[j]);
-                        bool ok;
-                        const int32_t sv = sc_of(kc, kj, ok) + fpj.x;
-                        ++pairs;
-                        if (!ok) continue;
-                        if (sv > mf) { mf = sv; mj = j; if (ns > 0) --ns; }
-                        else if ((s_mk[(j - jlo) >> 5] >> ((j - jlo) & 31)) & 1u) { if (++ns > P.max_skip) break; }
-                        if (fpj.y >= jlo) s_mk[(fpj.y - jlo) >> 5] |= 1u << ((fpj.y - jlo) & 31);
-                    }
-                    rfp[c & RM] = make_int2(mf, mj);
-                    F[c] = mf; PP[c] = mj;
-                    best_merge(bf, bi, mf, c);
-                }
-                comm += 1;
-            }
-            __syncthreads();
-            committed = comm;
-        }
-        // the segment's last argmax f (packed key) and DP pair count
-        uint64_t bk = bi >= 0 ? best_key(bf, bi) : 0ull;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) { const uint64_t o = __shfl_xor(bk, d, 64); bk = o > bk ? o : bk; }
-        pairs = wave_sum64(pairs);
-        if (lane == 0) {
-            if (bk) atomicMax(&s_best, bk);
-            if (pairs) atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)pairs);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            atomicMax(a.rbest + r, s_best);
-            a.lseg[q].w = LSEG_DONE;
-        }
-    }
-}
-
 // ---- 5b. one long segment per wave, wave-cooperative (heaviest first)
 // PROF (MM2G_KNOB_LSEG_PROF): shader-clock cycles of each phase of the
 // per-anchor step, summed over the pass's long segments into a.gprof[16..31]:
@@ -3102,7 +2621,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
     for (uint32_t t = blockIdx.x * DP_NW + wv; t < nl; t += nwaves) {
         const uint32_t q = (uint32_t)uni((int32_t)a.lseg_order[t]);
         const uint4 L = a.lseg[q];
-        if (uni((int32_t)L.w) == (int32_t)LSEG_DONE) continue;   // k_chain_giant did it
+        if ((uint32_t)uni((int32_t)L.w) & LSEG_DONE) continue;   // k_chain_giant did it
         const uint32_t r = (uint32_t)uni((int32_t)L.x);
         const int32_t s = uni((int32_t)L.y), e = uni((int32_t)L.z);
         if (t < 256) __builtin_amdgcn_s_setprio(2);
@@ -3515,7 +3034,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
             best_merge(best_f, best_i, bm, i0 + 63 - clz64(ballot(valid && fv == bm)));
         }
         if (lane == 0) {
-            if (a.lseg_prof) a.lseg[q].w = (uint32_t)min<uint64_t>(wall_clock64() - seg_t0, 0xffffffffull);   // MM2G_LSEG_PROF
+            if (a.lseg_prof) a.lseg[q].w = (uint32_t)min<uint64_t>(wall_clock64() - seg_t0, 0x7fffffffull);   // MM2G_LSEG_PROF
             atomicMax(a.rbest + r, best_key(best_f, best_i));
             atomicAdd((unsigned long long*)&a.out[r].dp_pairs, (unsigned long long)cpairs);
             atomicAdd(&a.out[r].n_noniso, (uint32_t)(e - s - 1));
@@ -3949,7 +3468,7 @@ __global__ __launch_bounds__(1024) void k_chain_giant(ChainArgs a) {
         __syncthreads();
         if (tid == 0) {
             atomicMax(a.rbest + r, s_best);
-            a.lseg[q].w = LSEG_DONE;
+            a.lseg[q].w = LSEG_DONE | (a.lseg_prof ? (uint32_t)min<uint64_t>(wall_clock64() - g_t0, 0x7fffffffull) : 0u);
         }
         // LDS-only barrier: the next segment may reuse the LDS arrays, but the
         // global stores above need not have landed (a full __syncthreads would
@@ -4204,20 +3723,15 @@ __global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t
 }
 
 // per-batch sums for mm2g_batch_counters (st[3] = minimizers, st[4] = anchors in the DP)
-__global__ __launch_bounds__(1024) void k_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, const uint32_t* ncand,
-                                                    unsigned long long* st) {
-    // st[3] minimizers, st[4] anchors in the DP, st[5] of them in reads k_chain_seg streams
-    // (no candidate list), st[6] in reads k_chain_lb runs on (no LB from the sort)
-    __shared__ unsigned long long ws[4][16];
-    unsigned long long v[4] = {0, 0, 0, 0};
-    for (uint32_t i = threadIdx.x; i < n; i += 1024) {
-        const uint32_t c2 = cnt2 ? cnt2[i] : 0u, nc = ncand ? ncand[i] : NC_STREAM;
-        v[0] += mz_cnt[i]; v[1] += c2; v[2] += nc >= NC_STREAM_LB ? c2 : 0u; v[3] += nc == NC_STREAM ? c2 : 0u;
-    }
+__global__ __launch_bounds__(1024) void k_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* st) {
+    // st[3] minimizers, st[4] anchors in the DP
+    __shared__ unsigned long long ws[2][16];
+    unsigned long long v[2] = {0, 0};
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) { v[0] += mz_cnt[i]; v[1] += cnt2 ? cnt2[i] : 0u; }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { v[k] = wave_sum64(v[k]); if (lane_id() == 0) ws[k][threadIdx.x >> 6] = v[k]; }
+    for (int k = 0; k < 2; ++k) { v[k] = wave_sum64(v[k]); if (lane_id() == 0) ws[k][threadIdx.x >> 6] = v[k]; }
     __syncthreads();
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < 2) {
         unsigned long long x = 0;
         for (int t = 0; t < 16; ++t) x += ws[threadIdx.x][t];
         st[3 + threadIdx.x] = x;
@@ -4377,11 +3891,7 @@ int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
 int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
     if (a.n == 0) return 0;
     const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4;
-    const bool lb = a.lut != nullptr;
-    if (stage == 0) {
-        if (lb) hipLaunchKernelGGL(k_sort_small<true>, dim3(a.n), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL(k_sort_small<false>, dim3(a.n), dim3(256), 0, st, a);
-    }
+    if (stage == 0) hipLaunchKernelGGL(k_sort_small, dim3(a.n), dim3(256), 0, st, a);
     else if (stage == 1) {
         // the requested LDS (default SORT_LDS: one workgroup per CU), at least the two bitmaps
         size_t lds = std::max<size_t>(a.lds_words ? (size_t)a.lds_words * 4 : (size_t)SORT_LDS, bmb);
@@ -4391,8 +3901,7 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
         // up to SORT_LDS_HALF: 512-thread workgroups, two per CU (one read's
         // barrier and latency phases overlap the other's)
         const bool gl = 2u * b.n_seq + 2u > (uint32_t)GOFF_LDS;
-#define SR_LAUNCH(G, T) do { if (lb) hipLaunchKernelGGL((k_sort_read<G, T, true>), dim3(a.n), dim3(T), lds, st, b); \
-                             else hipLaunchKernelGGL((k_sort_read<G, T, false>), dim3(a.n), dim3(T), lds, st, b); } while (0)
+#define SR_LAUNCH(G, T) hipLaunchKernelGGL((k_sort_read<G, T>), dim3(a.n), dim3(T), lds, st, b)
         if (lds <= (size_t)SORT_LDS_HALF) {
             if (gl) SR_LAUNCH(true, 512);
             else SR_LAUNCH(false, 512);
@@ -4455,7 +3964,6 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
     case 7: hipLaunchKernelGGL(k_chain_giant<false>, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
     case 8: hipLaunchKernelGGL(k_chain_giant<true>, dim3(blocks), dim3(1024), lut_lds(a.P.lut_n), st, a); break;
-    case 9: hipLaunchKernelGGL(k_chain_long_mw, dim3(blocks), dim3(MW_NW * 64), lut_lds(a.P.lut_n) + (size_t)MW_RK * 16, st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 3) / 4), dim3(256), 0, st, a); break;
     }
     LAUNCH_CHECK();
@@ -4473,8 +3981,8 @@ int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, in
     LAUNCH_CHECK();
     return 0;
 }
-int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, const uint32_t* ncand, unsigned long long* status64, hipStream_t st) {
-    hipLaunchKernelGGL(k_batch_sums, dim3(1), dim3(1024), 0, st, n, mz_cnt, cnt2, ncand, status64);
+int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st) {
+    hipLaunchKernelGGL(k_batch_sums, dim3(1), dim3(1024), 0, st, n, mz_cnt, cnt2, status64);
     LAUNCH_CHECK();
     return 0;
 }

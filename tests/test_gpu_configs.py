@@ -166,9 +166,9 @@ def test_c5_hg38_100kb(hg38, tmp_path):
                 assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
     # production defaults (the rescue pass pruned by pass 0's bound): PAF and per-read outcome
     _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5prune")
-    # pass 0's 100 kb chains through k_chain_long_mw (one 8-wave workgroup per segment of >= 4096 anchors)
-    with knobs(dev, mw_min=4096):
-        _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5mw")
+    # pass 0's 100 kb chains with more speculative rounds per block
+    with knobs(dev, spec_rounds=8):
+        _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5sr8")
 
 
 @pytest.mark.parametrize("mc,m", [(1, 15), (0, 0)])

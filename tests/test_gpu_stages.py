@@ -86,15 +86,13 @@ def test_workspace_exact_fallback(small_world, dense_world):
         d.close()
 
 
-@pytest.mark.parametrize("kn", [dict(sort_lb=1), dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1, sort_lb=1),
-                                dict(mw_min=64), dict(sort_small=1, mw_min=128, sketch_view=300)])
+@pytest.mark.parametrize("kn", [dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1),
+                                dict(spec_rounds=1), dict(sort_small=1, spec_rounds=16, sketch_view=300)])
 def test_round4_paths_vs_oracle(dev, small_world, dense_world, kn):
-    """Every round-4 production path, on and off, against the oracle (PAF and
-    per-read outcome, small and dense worlds at mid_occ 20 and 5000): the sort's
-    LB pass and candidate segments (sort_lb; sort_small=1 sends every read
-    through k_sort_read's, else most of these reads take k_sort_small's),
-    the rescue pass's pruning by pass 0's bound, query sketch views, and
-    k_chain_long_mw for pass 0's long segments."""
+    """Production paths, on and off, against the oracle (PAF and per-read
+    outcome, small and dense worlds at mid_occ 20 and 5000): the rescue pass's
+    pruning by pass 0's bound, query sketch views, every read through
+    k_sort_read (sort_small=1), and k_chain_long's speculative rounds."""
     with knobs(dev, **kn):
         _production_vs_oracle(dev, small_world, dense_world, tag=str(kn))
 
@@ -108,6 +106,18 @@ def test_wide_gaps_vs_oracle(dev, small_world, dense_world, max_gap, bw_long):
     with knobs(dev, sort_small=1):
         _production_vs_oracle(dev, small_world, dense_world, opts=M.map_opts(max_gap=max_gap, bw_long=bw_long),
                               tag=f"-g {max_gap} -r 500,{bw_long}")
+
+
+@pytest.mark.parametrize("max_gap,bw,bw_long", [(5000, 500, 200), (300, 500, 400), (300, 2000, 20000)])
+def test_narrow_rescue_vs_oracle(dev, small_world, dense_world, max_gap, bw, bw_long):
+    """A rescue pass narrower than pass 0 in some comput_sc limit (-r 500,200:
+    bw_long < bw, main.rs:205-206 accepts it; -g below bw: max_dist_x of the
+    rescue is max(max_gap, bw_long) < pass 0's max(max_gap, bw)).  Pass 0's best-f
+    bound no longer bounds the rescue's DP there, so the rescue pass must not be
+    pruned by it; the last case keeps every limit wider and prunes."""
+    with knobs(dev, prune_rescue=1):
+        _production_vs_oracle(dev, small_world, dense_world, opts=M.map_opts(max_gap=max_gap, bw=bw, bw_long=bw_long),
+                              tag=f"-g {max_gap} -r {bw},{bw_long}")
 
 
 def test_seed_batch_vs_oracle(dev, small_world, dense_world):
