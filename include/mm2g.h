@@ -336,7 +336,10 @@ enum {
     /* 28: retired (round 5; k_chain_long_mw, measured 2x slower and removed) */
     MM2G_KNOB_PRUNE_RESCUE = 29, /* the rescue pass prunes segments by pass 0's best-f lower bound [1]         */
     MM2G_KNOB_VIEW_READS = 30,   /* sketch views (MM2G_KNOB_SKETCH_VIEW) only for batches of fewer reads [2048]  */
-    MM2G_KNOB_COUNT = 31
+    MM2G_KNOB_SEG_SPARSE = 31,   /* pass 0: work items whose reads' best-f bound rules out every segment of <= 8
+                                    anchors find their candidate segments from k_chain_lb's segment-start bits
+                                    instead of streaming their keys [1]                                       */
+    MM2G_KNOB_COUNT = 32
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);
@@ -362,8 +365,8 @@ int mm2g_prof_reset(mm2g_ctx* ctx);
  * [6]=anchors entering the DP (after the sort's singleton filter); anchors in
  * the DP's long segments below the giant-kernel size [7] / from it on [8] and
  * in its medium segments [9] of pass 0, and [10], [11], [12] of the rescue pass;
- * DP anchors in reads that k_chain_seg streams (no candidate list from the
- * sort) [13] and that k_chain_lb runs on (no lower bound from the sort) [14].
+ * DP anchors whose keys k_chain_seg streams in pass 0 (the rest take its sparse
+ * items) [13] and that k_chain_lb streams [14].
  * Copies min(n, MM2G_N_COUNTERS) values; returns how many. */
 #define MM2G_N_COUNTERS 15
 int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out, int n);

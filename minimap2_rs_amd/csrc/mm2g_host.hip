@@ -104,6 +104,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SKETCH_VIEW: return 2560;
     case MM2G_KNOB_PRUNE_RESCUE: return 1;
     case MM2G_KNOB_VIEW_READS: return 2048;
+    case MM2G_KNOB_SEG_SPARSE: return 1;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -135,7 +136,7 @@ struct mm2g_ctx {
     DevBuf tab_off, tab_key, tab_cnt;
     DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
     DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, item_read, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, item_read, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist, isob;
     DevBuf dstat;                          // batch status block (BS_* word, workspace needs, counters)
     DevBuf chain_rdoff;                    // mm2g_chain_batch: prefix sums of the caller's qlen
     uint64_t cap_tab = 0, cap_A = 0;       // filter-table entries / anchors the workspaces hold
@@ -909,6 +910,10 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     ca.full_dp = full ? 1u : 0u;   // not "no fmin": with pruning off, production still follows the med_pairs knobs
     int32_t* fmin_buf = nullptr;
     if (!full && K[MM2G_KNOB_PRUNE]) ENSURE(c->fmin, int32_t, n, fmin_buf);
+    // pass 0's segment-start words (k_chain_lb -> k_chain_seg's sparse items): read r at (a_off[r] >> 6) + r
+    uint64_t* isob = nullptr;
+    if (fmin_buf && K[MM2G_KNOB_SEG_SPARSE] && K[MM2G_KNOB_MED_PAIRS] == 0) ENSURE(c->isob, uint64_t, A_cap / 64 + n + 2, isob);
+    ca.seg_streamed = stat ? stat + 5 : nullptr;
     uint32_t* item_off;
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
@@ -956,6 +961,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         // steps with dd in (bw_long, bw] are rejected in the rescue and the bound does not hold.
         const bool rescue_wider = bw_long >= P0.bw && mdx1 >= P0.max_dist_x && mdy1 >= P0.max_dist_y;
         ca.fmin = (pass == 0 || (K[MM2G_KNOB_PRUNE_RESCUE] && rescue_wider)) ? fmin_buf : nullptr;
+        ca.isob = pass == 0 ? isob : nullptr;
         if (ca.fmin && pass == 0) {
             HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
             ProfScope ps(c, "chain_lb");
@@ -1027,14 +1033,18 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
             nl = std::min(nl, lcap);
             std::vector<uint4> ls(nl);
             if (nl) HIPCHK(hipMemcpy(ls.data(), lseg, (size_t)nl * 16, hipMemcpyDeviceToHost));
-            std::sort(ls.begin(), ls.end(), [](const uint4& x, const uint4& y) { return x.w > y.w; });
-            double tot = 0; for (auto& v : ls) tot += v.w;
-            fprintf(stderr, "[lseg_prof] pass %d: %u long segments, sum %.0f us; slowest:", pass, nl, tot / 100);
+            // lseg[].w: wall-clock ticks (100 MHz) of the kernel that ran the segment; bit 31 = k_chain_giant's
+            const uint32_t GBIT = 0x80000000u;
+            std::sort(ls.begin(), ls.end(), [&](const uint4& x, const uint4& y) { return (x.w & ~GBIT) > (y.w & ~GBIT); });
+            double tot = 0, tot_g = 0; uint32_t ng = 0;
+            for (auto& v : ls) { tot += v.w & ~GBIT; if (v.w & GBIT) { tot_g += v.w & ~GBIT; ++ng; } }
+            fprintf(stderr, "[lseg_prof] pass %d: %u long segments (%u by k_chain_giant), sum %.0f us (giant %.0f us); slowest:", pass, nl, ng,
+                    tot / 100, tot_g / 100);
             for (size_t i = 0; i < ls.size() && i < 8; ++i) {
                 ReadOut ro;
                 HIPCHK(hipMemcpy(&ro, out + ls[i].x, sizeof ro, hipMemcpyDeviceToHost));
-                fprintf(stderr, " (read %u len %u %.0f us, read j-steps %u pairs %llu)", ls[i].x, ls[i].z - ls[i].y, ls[i].w / 100.0,
-                        ro.n_steps, (unsigned long long)ro.dp_pairs);
+                fprintf(stderr, " (read %u len %u %s %.0f us, read j-steps %u pairs %llu)", ls[i].x, ls[i].z - ls[i].y,
+                        (ls[i].w & GBIT) ? "giant" : "long", (ls[i].w & ~GBIT) / 100.0, ro.n_steps, (unsigned long long)ro.dp_pairs);
             }
             fprintf(stderr, "\n");
         }
@@ -1431,7 +1441,7 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     for (int t = 0; t < 6; ++t) c->counters[t] = cnt[t];
     c->counters[6] = c->h_stat[4];    // anchors left after the sort's singleton filter (the DP input)
     for (int t = 0; t < 6; ++t) c->counters[7 + t] = c->h_stat[8 + t];   // anchors per chain kernel class and pass
-    c->counters[13] = c->h_stat[4];   // DP anchors whose keys k_chain_seg streams (pass 0)
+    c->counters[13] = c->h_stat[5];   // DP anchors whose keys k_chain_seg streams (pass 0; the rest: sparse items)
     c->counters[14] = c->h_stat[4];   // ... that k_chain_lb streams (pass 0)
     return 0;
 }

@@ -219,6 +219,11 @@ struct ChainArgs {
     const uint32_t* abort = nullptr;
     unsigned long long* gprof = nullptr;   // MM2G_LSEG_PROF: k_chain_giant phase sums (16 counters)
     unsigned long long* seg_stat = nullptr;   // k_lseg_order: anchors in long (< / >= giant_min) and medium segments
+    // Pass 0 (production, pruning on): segment starts of the sorted kept anchors, one bit per
+    // anchor (k_chain_lb writes them, k_chain_seg's sparse items read them); read r's words
+    // start at (a_off[r] >> 6) + r.  Null: every item streams its keys.
+    uint64_t* isob = nullptr;
+    unsigned long long* seg_streamed = nullptr;   // pass 0: anchors of the items k_chain_seg streamed (counter)
 };
 struct DvArgs {
     uint32_t n;

@@ -2205,6 +2205,67 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
         uint32_t n_big = 0;
         int32_t max_seg = 0;
         const int32_t fm = a.fmin ? uni(a.fmin[r]) : 0;   // segments with len * span < fm are skipped
+        if (a.isob && P.pass == 0 && fm > CHAIN_TINY * span) {
+            // Sparse item (production pass 0, DESIGN.md "Candidate segments"): every segment that
+            // can hold the read's best f has len >= Lmin > CHAIN_TINY anchors, so it goes to the
+            // long-segment queue whole; the segment starts come from k_chain_lb's isolated-anchor
+            // words (1 bit per anchor) and no key is read here.  Lane l takes word c0/64 + l.
+            const int32_t Lmin = (fm + span - 1) / span;
+            const uint64_t* isw = a.isob + (base >> 6) + r;
+            const int32_t w0 = c0 >> 6, w1 = (c1 + 63) >> 6;            // the item's words (<= 64)
+            const int32_t wl = w0 + lane;
+            const uint64_t m = wl < w1 ? isw[wl] : 0ULL;
+            // the first start after the item (closes its last open segment): scan on, 64 words at a time
+            int32_t beyond = A;
+            for (int32_t wb0 = w1; wb0 * 64 < A; wb0 += 64) {
+                const int32_t wq = wb0 + lane;
+                const uint64_t mq = wq * 64 < A ? isw[wq] : 0ULL;
+                const uint64_t nz = ballot(mq != 0ULL);
+                if (nz) { const int l0 = ctz64(nz); beyond = wb0 * 64 + l0 * 64 + ctz64(rdl64(mq, l0)); break; }
+            }
+            // first start in a later word of the item: exclusive suffix minimum over the lanes
+            int32_t fs = m ? wl * 64 + ctz64(m) : INT_MAX;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) { const int32_t o = __shfl_down(fs, d, 64); if (lane + d < 64) fs = min(fs, o); }
+            int32_t after = __shfl_down(fs, 1, 64);
+            after = lane == 63 ? beyond : min(after, beyond);
+            uint64_t mm = m;
+            if (Lmin >= 64) mm = m ? (1ULL << (63 - clz64(m))) : 0ULL;   // only a word's last start can begin one
+            uint32_t n_c = 0;
+            int32_t mx = 0;
+            while (any(mm != 0ULL)) {
+                bool cand = false;
+                int32_t sl = 0, el = 0;
+                if (mm) {
+                    const int b = ctz64(mm);
+                    mm &= mm - 1;
+                    const uint64_t rest = b == 63 ? 0ULL : (m >> (b + 1)) << (b + 1);
+                    sl = wl * 64 + b;
+                    el = rest ? wl * 64 + ctz64(rest) : after;
+                    cand = el - sl >= Lmin;
+                }
+                const uint64_t cm = ballot(cand);
+                if (cm) {
+                    uint32_t q0 = 0;
+                    if (lane == 0) q0 = atomicAdd(a.lseg_n, (uint32_t)__popcll(cm));
+                    q0 = (uint32_t)uni((int32_t)q0);
+                    if (cand) {
+                        const uint32_t q = q0 + (uint32_t)__popcll(cm & lanemask_lt());
+                        if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
+                        mx = max(mx, el - sl);
+                    }
+                    n_c += (uint32_t)__popcll(cm);
+                }
+            }
+            const int32_t ml = rdl(scan_max(mx), 63);
+            if (lane == 0) {
+                ReadOut* O = a.out + r;
+                O->t_pass[P.pass] = (uint32_t)(wall_clock64() - t_start);
+                O->pad2 = (uint32_t)(ml > 65535 ? 65535 : ml) | ((n_c > 65535 ? 65535u : n_c) << 16);
+            }
+            continue;
+        }
+        if (lane == 0 && a.seg_streamed && P.pass == 0) atomicAdd(a.seg_streamed, (unsigned long long)(c1 - c0));
         int32_t bf = INT_MIN, bi = -1;      // per-lane best (singletons and tiny segments)
         int32_t pend = -1;                  // start of the open segment
         int32_t th0 = 0, th1 = 0, th2 = 0, tt0 = 0, tt1 = 0, tt2 = 0;   // tiny class queue heads / tails
@@ -2389,6 +2450,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
         const uint64_t base = uni64(a.a_off[r]);
         const int32_t A = min((int32_t)uni((int32_t)a.cnt2[r]), c0 + (int32_t)a.seg_chunk);
         const uint64_t* K = a.keys + base;
+        uint64_t* isw = a.isob ? a.isob + (base >> 6) + r : nullptr;   // this read's segment-start words (ChainArgs::isob)
         int32_t carry = NEG, best = span;      // LB restarts at span at a chunk start: still a lower bound
         uint64_t k0 = c0 > 0 ? K[c0 - 1] : 0;
         uint32_t prev_lo = (uint32_t)uni((int32_t)(uint32_t)k0), prev_hi = (uint32_t)uni((int32_t)(uint32_t)(k0 >> 32));
@@ -2406,7 +2468,12 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
                 const uint32_t g = (uint32_t)(ak >> gsh), gp = (uint32_t)(pk >> gsh);
                 const int32_t p = (int32_t)((ak >> qb) & rmask), pj = (int32_t)((pk >> qb) & rmask);
                 const int32_t q = (int32_t)(ak & qmask), qj = (int32_t)(pk & qmask);
-                const bool iso = il == 0 || il == c0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx);
+                const bool tiso = il == 0 || g != gp || p > (int32_t)((uint32_t)pj + (uint32_t)maxdx);   // starts a segment
+                const bool iso = tiso || il == c0;
+                if (isw) {
+                    const uint64_t im = ballot(valid && tiso);
+                    if (lane == 0 && i00 + u * 64 < A) isw[(i00 + u * 64) >> 6] = im;
+                }
                 int32_t sa = NEG;
                 if (valid && !iso) {
                     const int32_t dq = q - qj, dr = p - pj;

@@ -86,15 +86,30 @@ def test_workspace_exact_fallback(small_world, dense_world):
         d.close()
 
 
-@pytest.mark.parametrize("kn", [dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1),
-                                dict(spec_rounds=1), dict(sort_small=1, spec_rounds=16, sketch_view=300)])
+@pytest.mark.parametrize("kn", [dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1), dict(seg_sparse=0),
+                                dict(spec_rounds=1), dict(sort_small=1, spec_rounds=16, sketch_view=300, seg_chunk=128)])
 def test_round4_paths_vs_oracle(dev, small_world, dense_world, kn):
     """Production paths, on and off, against the oracle (PAF and per-read
     outcome, small and dense worlds at mid_occ 20 and 5000): the rescue pass's
     pruning by pass 0's bound, query sketch views, every read through
-    k_sort_read (sort_small=1), and k_chain_long's speculative rounds."""
+    k_sort_read (sort_small=1), k_chain_seg's sparse items off (seg_sparse=0) and
+    over 128-anchor items (their segment-start words cut mid-segment), and
+    k_chain_long's speculative rounds."""
     with knobs(dev, **kn):
         _production_vs_oracle(dev, small_world, dense_world, tag=str(kn))
+
+
+def test_sparse_items_taken(dev, small_world, dense_world):
+    """Production pass 0 finds most candidate segments from k_chain_lb's
+    segment-start bits (k_chain_seg's sparse items read no keys): fewer
+    anchors are streamed than enter the DP, and the results equal the oracle's."""
+    _production_vs_oracle(dev, small_world, dense_world, tag="sparse")
+    c = dev.counters()
+    assert c["dp_anchors"] > 0 and c["seg_stream_anchors"] < c["dp_anchors"], c
+    with knobs(dev, seg_sparse=0):
+        _production_vs_oracle(dev, small_world, dense_world, tag="streamed")
+        c = dev.counters()
+        assert c["seg_stream_anchors"] == c["dp_anchors"], c
 
 
 @pytest.mark.parametrize("max_gap,bw_long", [(5000, 40000), (40000, 20000)])
