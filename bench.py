@@ -354,7 +354,8 @@ KERNEL_SYMBOLS = {
     "filter": ("k_filter", ""), "seed_count": ("k_seed_count", ""), "seed_write": ("k_seed_write", ""),
     "sort_small": ("k_sort_small", ""), "sort_large": ("k_sort_read", ""), "sort_radix": ("k_sort_radix", ""),
     "sort_big": ("k_sort_big", ""),
-    "chain_items": ("k_seg_items", ""), "chain_lb": ("k_chain_lb", ""), "chain_seg": ("k_chain_seg", ""),
+    "chain_items": ("k_seg_items", ""), "chain_lb": ("k_chain_lb", ""), "chain_cands": ("k_seg_cands", ""),
+    "chain_seg": ("k_chain_seg", ""),
     "chain_med": ("k_chain_med", ""), "chain_lorder": ("k_lseg_order", ""), "chain_long": ("k_chain_long", ""),
     "chain_giant": ("k_chain_giant", ""), "chain_fin": ("k_chain_fin", ""),
     "chain_items_rescue": ("k_seg_items", ""), "chain_seg_rescue": ("k_chain_seg", ""), "chain_med_rescue": ("k_chain_med", ""),
@@ -378,8 +379,6 @@ def alg_bytes(cnt: dict, res) -> dict:
     mapped = (res["flags"] & 1) != 0
     cm = int(res["cm"][mapped].astype(np.int64).sum())
     mdv = int(res["m_dv"][mapped].astype(np.int64).sum())
-    # kept anchors of the reads whose LB pass ran in k_sort_read (k_sort_small's reads it from LDS)
-    lb_sorted = max(0, Adp - cnt.get("lb_stream_anchors", Adp) - int(na[(na > 1) & (na <= SORT_SMALL)].sum()))
     return {
         "mz_base": 24 * n,
         "sketch": (L + 3) // 4 + 12 * m,                 # nt4 codes in; (x 8 B, y 4 B) per minimizer out
@@ -388,13 +387,13 @@ def alg_bytes(cnt: dict, res) -> dict:
         "seed_count": 9 * m + 16 * mk + 8 * m,            # keep+x in, 16 B table entry per kept, (n, poff) out
         "seed_write": 12 * m + 16 * A,                    # (n, poff, y) in; 8 B position in + 8 B key out per anchor
         "sort_small": 16 * int(na[(na > 1) & (na <= SORT_SMALL)].sum()),
-        # + the pass-0 LB pass over the kept keys of the reads it runs on (8 B each, read back from HBM)
-        "sort_large": 16 * int(na[(na > SORT_SMALL) & (na <= SORT_CELL_MAX)].sum()) + 8 * lb_sorted,
+        "sort_large": 16 * int(na[(na > SORT_SMALL) & (na <= SORT_CELL_MAX)].sum()),
         "sort_radix": 16 * int(na[na > SORT_CELL_MAX].sum()),
         "sort_big": 16 * int(na[na > SORT_CELL_MAX].sum()),
         "chain_items": 8 * n,
-        "chain_lb": 8 * cnt.get("lb_stream_anchors", Adp),      # reads without the sort's LB
-        "chain_seg": 8 * cnt.get("seg_stream_anchors", Adp),    # streamed reads (candidate items are tiny)
+        "chain_lb": 8 * cnt.get("lb_stream_anchors", Adp) + Adp // 8,   # keys in, segment-start bits out
+        "chain_cands": Adp // 8 + 12 * n,                        # segment-start bits in (per read: a_off, cnt2, fmin)
+        "chain_seg": 8 * cnt.get("seg_stream_anchors", Adp),    # the items left to streaming
         "chain_med": 16 * cnt.get("med_anchors", 0),
         "chain_lorder": 0,
         "chain_long": 16 * cnt.get("long_anchors", 0),

@@ -136,7 +136,7 @@ struct mm2g_ctx {
     DevBuf tab_off, tab_key, tab_cnt;
     DevBuf a_part;                         // seed_write part starts (SEED_PARTS - 1 per read)
     DevBuf giant_scr;                      // k_chain_giant<true> scratch (allocated on first use)
-    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, item_read, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist, isob;
+    DevBuf a_cnt, a_off, keys, keys_tmp, fbuf, ppbuf, fmin, item_off, item_read, outb, lut, work, order, tmark, lseg, lseg_order, lseg_n, rbest, mseg, cnt2, smax, rlist, isob, sq, sq_n;
     DevBuf dstat;                          // batch status block (BS_* word, workspace needs, counters)
     DevBuf chain_rdoff;                    // mm2g_chain_batch: prefix sums of the caller's qlen
     uint64_t cap_tab = 0, cap_A = 0;       // filter-table entries / anchors the workspaces hold
@@ -912,7 +912,14 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     if (!full && K[MM2G_KNOB_PRUNE]) ENSURE(c->fmin, int32_t, n, fmin_buf);
     // pass 0's segment-start words (k_chain_lb -> k_chain_seg's sparse items): read r at (a_off[r] >> 6) + r
     uint64_t* isob = nullptr;
-    if (fmin_buf && K[MM2G_KNOB_SEG_SPARSE] && K[MM2G_KNOB_MED_PAIRS] == 0) ENSURE(c->isob, uint64_t, A_cap / 64 + n + 2, isob);
+    uint2* sq = nullptr;
+    uint32_t* sq_n = nullptr;
+    const uint32_t sq_cap = (uint32_t)std::min<uint64_t>(A_cap / 64 + n + 16, 0xffffffffu);
+    if (fmin_buf && K[MM2G_KNOB_SEG_SPARSE] && K[MM2G_KNOB_MED_PAIRS] == 0) {
+        ENSURE(c->isob, uint64_t, A_cap / 64 + n + 2, isob);
+        ENSURE(c->sq, uint2, sq_cap, sq);
+        ENSURE(c->sq_n, uint32_t, 1, sq_n);
+    }
     ca.seg_streamed = stat ? stat + 5 : nullptr;
     uint32_t* item_off;
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
@@ -962,10 +969,19 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         const bool rescue_wider = bw_long >= P0.bw && mdx1 >= P0.max_dist_x && mdy1 >= P0.max_dist_y;
         ca.fmin = (pass == 0 || (K[MM2G_KNOB_PRUNE_RESCUE] && rescue_wider)) ? fmin_buf : nullptr;
         ca.isob = pass == 0 ? isob : nullptr;
+        ca.sq = nullptr; ca.sq_n = nullptr; ca.sq_cap = 0;
         if (ca.fmin && pass == 0) {
             HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
-            ProfScope ps(c, "chain_lb");
-            LCHK(launch_chain_stage(5, ca, 2048, c->stream));
+            {
+                ProfScope ps(c, "chain_lb");
+                LCHK(launch_chain_stage(5, ca, 2048, c->stream));
+            }
+            if (ca.isob) {   // candidate segments per read; k_chain_seg streams only the reads left over
+                HIPCHK(hipMemsetAsync(sq_n, 0, 4, c->stream));
+                ca.sq = sq; ca.sq_n = sq_n; ca.sq_cap = sq_cap;
+                ProfScope ps(c, "chain_cands");
+                LCHK(launch_chain_stage(10, ca, (int)std::min<uint32_t>((n + 3) / 4, 2048), c->stream));
+            }
         }
         ca.lseg_prof = K[MM2G_KNOB_LSEG_PROF] ? 1u : 0u;
         unsigned long long* gprof = nullptr;

@@ -224,6 +224,10 @@ struct ChainArgs {
     // start at (a_off[r] >> 6) + r.  Null: every item streams its keys.
     uint64_t* isob = nullptr;
     unsigned long long* seg_streamed = nullptr;   // pass 0: anchors of the items k_chain_seg streamed (counter)
+    // k_seg_cands -> k_chain_seg (pass 0 with isob): the (read, chunk) items left to streaming
+    uint2* sq = nullptr;
+    uint32_t* sq_n = nullptr;
+    uint32_t sq_cap = 0;
 };
 struct DvArgs {
     uint32_t n;

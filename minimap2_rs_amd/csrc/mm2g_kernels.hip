@@ -628,55 +628,114 @@ DEVI uint32_t fslot(uint64_t h, uint32_t tmask) { return (uint32_t)((h * 0x9E377
 constexpr int FT_MAX = 4096;
 DEVI bool filter_lds_ok(uint32_t ts, int k) { return ts > 0 && ts <= (uint32_t)FT_MAX && k <= 16; }
 
+// Reads whose count table does not fit k_filter_lds (large m, or k > 16):
+// persistent 1024-thread blocks, one read at a time.  Reads with m <= 65535
+// (C5's 100 kb reads: m ~ 18.6 k) count in LDS: est[] holds, per slot of
+// fslot(h), the number of minimizers hashed there -- at least the count of
+// every hash in the slot -- so a minimizer with est <= T = max(q_occ_max,
+// cutoff) keeps (the reference drops it iff cnt > q_occ_max && cnt > cutoff);
+// only hashes over T get exact counts, in a small LDS table (all occurrences
+// of a hash share its slot, so they all enter).  The global open-addressed
+// table (the former path, ~1.6 GB of zeroing per C5 step) remains for larger
+// reads and for a candidate-table overflow.
+constexpr int FB_EST = 32768;          // estimate counters (u32)
+constexpr int FB_XT = 1024;            // exact slots for the hashes over T (u64 key + u32 count)
+constexpr size_t FB_LDS = (size_t)FB_EST * 4 + (size_t)FB_XT * 12;
 __global__ __launch_bounds__(1024) void k_filter(FilterArgs a, int a_k) {
-    // one 1024-thread block per read whose table does not fit k_filter_lds (large m)
-    const uint32_t r = blockIdx.x;
-    if (r >= a.n) return;
+    extern __shared__ __align__(16) unsigned char fsm[];
+    uint32_t* est = (uint32_t*)fsm;
+    unsigned long long* xk = (unsigned long long*)(fsm + (size_t)FB_EST * 4);
+    uint32_t* xc = (uint32_t*)(xk + FB_XT);
+    __shared__ uint32_t s_ovf;
     const int tid = threadIdx.x;
-    const uint64_t mb = a.mz_base[r];
-    const uint32_t m = a.mz_cnt[r];
-    uint8_t* keep = a.keep + mb;
-    const uint32_t ts = tab_size_for(m, a.q_occ_max);
-    if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) return;   // seeds.rs:14-15: k_filter_lds
-    if (filter_lds_ok(ts, a_k)) return;                        // done by k_filter_lds
-    const uint64_t tb = a.tab_off[r];                          // prefix of the global tables only
-    if (tb + ts > a.cap_tab) return;                           // workspace too small: batch flagged BS_TAB by the scan
-    uint64_t* tk = a.tab_key + tb; uint32_t* tc = a.tab_cnt + tb;
-    for (uint32_t i = tid; i < ts; i += 1024) { tk[i] = U64MAX; tc[i] = 0; }
-    __threadfence_block();
-    __syncthreads();
-    const uint32_t tmask = ts - 1;
-    for (uint32_t b0 = 0; b0 < m; b0 += 1024) {
-        const uint32_t i = b0 + tid;
-        bool done = i >= m;
-        const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
-        uint32_t sl = fslot(h, tmask);
-        while (any(!done)) {
-            if (!done) {
-                const unsigned long long prev = atomicCAS((unsigned long long*)&tk[sl], (unsigned long long)U64MAX, (unsigned long long)h);
-                if (prev == U64MAX || prev == h) { atomicAdd(&tc[sl], 1u); done = true; }
-                else sl = (sl + 1) & tmask;
+    for (uint32_t r = blockIdx.x; r < a.n; r += gridDim.x) {
+        const uint64_t mb = a.mz_base[r];
+        const uint32_t m = a.mz_cnt[r];
+        uint8_t* keep = a.keep + mb;
+        const uint32_t ts = tab_size_for(m, a.q_occ_max);
+        if (a.q_occ_frac <= 0.0f || a.q_occ_max <= 0 || ts == 0) continue;   // seeds.rs:14-15: k_filter_lds
+        if (filter_lds_ok(ts, a_k)) continue;                      // done by k_filter_lds
+        const float prod = (float)m * a.q_occ_frac;                // (m as f32 * q_occ_frac) as usize
+        const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
+        const uint64_t T = cutoff > (uint64_t)a.q_occ_max ? cutoff : (uint64_t)a.q_occ_max;
+        if (m <= 65535u) {
+            for (int i = tid; i < FB_EST; i += 1024) est[i] = 0;
+            for (int i = tid; i < FB_XT; i += 1024) { xk[i] = U64MAX; xc[i] = 0; }
+            if (tid == 0) s_ovf = 0;
+            __syncthreads();
+            for (uint32_t i = tid; i < m; i += 1024) atomicAdd(&est[fslot(a.mz_x[mb + i] >> 8, FB_EST - 1)], 1u);
+            __syncthreads();
+            for (uint32_t i = tid; i < m; i += 1024) {
+                const uint64_t h = a.mz_x[mb + i] >> 8;
+                if ((uint64_t)est[fslot(h, FB_EST - 1)] <= T) continue;
+                uint32_t sl = fslot(h, FB_XT - 1);
+                for (int pr = 0;; ++pr) {
+                    if (pr == FB_XT) { s_ovf = 1; break; }
+                    const unsigned long long prev = atomicCAS(&xk[sl], (unsigned long long)U64MAX, (unsigned long long)h);
+                    if (prev == U64MAX || prev == h) { atomicAdd(&xc[sl], 1u); break; }
+                    sl = (sl + 1) & (FB_XT - 1);
+                }
+            }
+            __syncthreads();
+            const bool ovf = s_ovf != 0;
+            if (!ovf) {
+                for (uint32_t i = tid; i < m; i += 1024) {
+                    const uint64_t h = a.mz_x[mb + i] >> 8;
+                    uint8_t kp = 1;
+                    if ((uint64_t)est[fslot(h, FB_EST - 1)] > T) {
+                        uint32_t sl = fslot(h, FB_XT - 1), c = 0;
+                        for (int pr = 0; pr < FB_XT; ++pr) {
+                            const unsigned long long e = xk[sl];
+                            if (e == h) { c = xc[sl]; break; }
+                            if (e == U64MAX) break;
+                            sl = (sl + 1) & (FB_XT - 1);
+                        }
+                        kp = (uint64_t)c > T ? 0 : 1;
+                    }
+                    keep[i] = kp;
+                }
+            }
+            __syncthreads();                                   // the LDS tables are reused by the next read
+            if (!ovf) continue;
+        }
+        const uint64_t tb = a.tab_off[r];                          // prefix of the global tables only
+        if (tb + ts > a.cap_tab) continue;                         // workspace too small: batch flagged BS_TAB by the scan
+        uint64_t* tk = a.tab_key + tb; uint32_t* tc = a.tab_cnt + tb;
+        for (uint32_t i = tid; i < ts; i += 1024) { tk[i] = U64MAX; tc[i] = 0; }
+        __threadfence_block();
+        __syncthreads();
+        const uint32_t tmask = ts - 1;
+        for (uint32_t b0 = 0; b0 < m; b0 += 1024) {
+            const uint32_t i = b0 + tid;
+            bool done = i >= m;
+            const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
+            uint32_t sl = fslot(h, tmask);
+            while (any(!done)) {
+                if (!done) {
+                    const unsigned long long prev = atomicCAS((unsigned long long*)&tk[sl], (unsigned long long)U64MAX, (unsigned long long)h);
+                    if (prev == U64MAX || prev == h) { atomicAdd(&tc[sl], 1u); done = true; }
+                    else sl = (sl + 1) & tmask;
+                }
             }
         }
-    }
-    __threadfence_block();
-    __syncthreads();
-    const float prod = (float)m * a.q_occ_frac;
-    const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
-    for (uint32_t b0 = 0; b0 < m; b0 += 1024) {
-        const uint32_t i = b0 + tid;
-        bool done = i >= m;
-        const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
-        uint32_t sl = fslot(h, tmask), c = 0;
-        while (any(!done)) {
-            if (!done) {
-                const uint64_t kk = __hip_atomic_load(&tk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (kk == h) { c = __hip_atomic_load(&tc[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); done = true; }
-                else if (kk == U64MAX) done = true;
-                else sl = (sl + 1) & tmask;
+        __threadfence_block();
+        __syncthreads();
+        for (uint32_t b0 = 0; b0 < m; b0 += 1024) {
+            const uint32_t i = b0 + tid;
+            bool done = i >= m;
+            const uint64_t h = done ? 0 : (a.mz_x[mb + i] >> 8);
+            uint32_t sl = fslot(h, tmask), c = 0;
+            while (any(!done)) {
+                if (!done) {
+                    const uint64_t kk = __hip_atomic_load(&tk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (kk == h) { c = __hip_atomic_load(&tc[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); done = true; }
+                    else if (kk == U64MAX) done = true;
+                    else sl = (sl + 1) & tmask;
+                }
             }
+            if (i < m) keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
         }
-        if (i < m) keep[i] = ((int64_t)c > (int64_t)a.q_occ_max && (uint64_t)c > cutoff) ? 0 : 1;
+        __syncthreads();                                       // before the next read reuses s_ovf / LDS
     }
 }
 
@@ -2167,7 +2226,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     int32_t* tqs = (int32_t*)(krings + DP_NW * KRING);          // 3 classes x TQ segment starts
     uint8_t* tls = (uint8_t*)(tqs + DP_NW * 3 * TQ);            // their lengths
     int2* medbs = (int2*)(tls + DP_NW * 3 * TQ);
-    if (blockIdx.x * DP_NW >= (uint32_t)a.item_off[a.n]) return;   // no work item for this workgroup: skip the LUT load
+    if (blockIdx.x * DP_NW >= (a.sq ? min(*a.sq_n, a.sq_cap) : (uint32_t)a.item_off[a.n])) return;   // no work item for this workgroup: skip the LUT load
     load_lut(lut, a.lut, P.lut_n);
     __syncthreads();
     const int lane = lane_id(), wv = wave_id();
@@ -2183,11 +2242,17 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
     // of the reads in `order` (heaviest first).  A wave starts its chunk at the
     // first isolated anchor at or after c0 and finishes the segment open at c1.
     const uint32_t nwaves = gridDim.x * DP_NW;
-    const uint32_t n_items = (uint32_t)uni((int32_t)a.item_off[a.n]);
+    const uint32_t n_items = a.sq ? min((uint32_t)uni((int32_t)*a.sq_n), a.sq_cap) : (uint32_t)uni((int32_t)a.item_off[a.n]);
     for (uint32_t it = blockIdx.x * DP_NW + wv; it < n_items; it += nwaves) {
-        const uint32_t t = (uint32_t)uni((int32_t)((a.item_read && it < a.item_cap) ? a.item_read[it] : item_owner(a.item_off, a.n, it)));
-        const uint32_t r = (uint32_t)uni((int32_t)a.order[t]);
-        const uint32_t j = it - (uint32_t)uni((int32_t)a.item_off[t]);
+        uint32_t r, j, t = 0xffffffffu;
+        if (a.sq) {   // pass 0 with k_seg_cands: only the reads it left to streaming, (read, chunk) per item
+            const uint2 q = a.sq[it];
+            r = (uint32_t)uni((int32_t)q.x); j = (uint32_t)uni((int32_t)q.y);
+        } else {
+            t = (uint32_t)uni((int32_t)((a.item_read && it < a.item_cap) ? a.item_read[it] : item_owner(a.item_off, a.n, it)));
+            r = (uint32_t)uni((int32_t)a.order[t]);
+            j = it - (uint32_t)uni((int32_t)a.item_off[t]);
+        }
         const uint64_t t_start = wall_clock64();
         if (t < (uint32_t)a.n_prio) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
@@ -2205,66 +2270,6 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
         uint32_t n_big = 0;
         int32_t max_seg = 0;
         const int32_t fm = a.fmin ? uni(a.fmin[r]) : 0;   // segments with len * span < fm are skipped
-        if (a.isob && P.pass == 0 && fm > CHAIN_TINY * span) {
-            // Sparse item (production pass 0, DESIGN.md "Candidate segments"): every segment that
-            // can hold the read's best f has len >= Lmin > CHAIN_TINY anchors, so it goes to the
-            // long-segment queue whole; the segment starts come from k_chain_lb's isolated-anchor
-            // words (1 bit per anchor) and no key is read here.  Lane l takes word c0/64 + l.
-            const int32_t Lmin = (fm + span - 1) / span;
-            const uint64_t* isw = a.isob + (base >> 6) + r;
-            const int32_t w0 = c0 >> 6, w1 = (c1 + 63) >> 6;            // the item's words (<= 64)
-            const int32_t wl = w0 + lane;
-            const uint64_t m = wl < w1 ? isw[wl] : 0ULL;
-            // the first start after the item (closes its last open segment): scan on, 64 words at a time
-            int32_t beyond = A;
-            for (int32_t wb0 = w1; wb0 * 64 < A; wb0 += 64) {
-                const int32_t wq = wb0 + lane;
-                const uint64_t mq = wq * 64 < A ? isw[wq] : 0ULL;
-                const uint64_t nz = ballot(mq != 0ULL);
-                if (nz) { const int l0 = ctz64(nz); beyond = wb0 * 64 + l0 * 64 + ctz64(rdl64(mq, l0)); break; }
-            }
-            // first start in a later word of the item: exclusive suffix minimum over the lanes
-            int32_t fs = m ? wl * 64 + ctz64(m) : INT_MAX;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) { const int32_t o = __shfl_down(fs, d, 64); if (lane + d < 64) fs = min(fs, o); }
-            int32_t after = __shfl_down(fs, 1, 64);
-            after = lane == 63 ? beyond : min(after, beyond);
-            uint64_t mm = m;
-            if (Lmin >= 64) mm = m ? (1ULL << (63 - clz64(m))) : 0ULL;   // only a word's last start can begin one
-            uint32_t n_c = 0;
-            int32_t mx = 0;
-            while (any(mm != 0ULL)) {
-                bool cand = false;
-                int32_t sl = 0, el = 0;
-                if (mm) {
-                    const int b = ctz64(mm);
-                    mm &= mm - 1;
-                    const uint64_t rest = b == 63 ? 0ULL : (m >> (b + 1)) << (b + 1);
-                    sl = wl * 64 + b;
-                    el = rest ? wl * 64 + ctz64(rest) : after;
-                    cand = el - sl >= Lmin;
-                }
-                const uint64_t cm = ballot(cand);
-                if (cm) {
-                    uint32_t q0 = 0;
-                    if (lane == 0) q0 = atomicAdd(a.lseg_n, (uint32_t)__popcll(cm));
-                    q0 = (uint32_t)uni((int32_t)q0);
-                    if (cand) {
-                        const uint32_t q = q0 + (uint32_t)__popcll(cm & lanemask_lt());
-                        if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
-                        mx = max(mx, el - sl);
-                    }
-                    n_c += (uint32_t)__popcll(cm);
-                }
-            }
-            const int32_t ml = rdl(scan_max(mx), 63);
-            if (lane == 0) {
-                ReadOut* O = a.out + r;
-                O->t_pass[P.pass] = (uint32_t)(wall_clock64() - t_start);
-                O->pad2 = (uint32_t)(ml > 65535 ? 65535 : ml) | ((n_c > 65535 ? 65535u : n_c) << 16);
-            }
-            continue;
-        }
         if (lane == 0 && a.seg_streamed && P.pass == 0) atomicAdd(a.seg_streamed, (unsigned long long)(c1 - c0));
         int32_t bf = INT_MIN, bi = -1;      // per-lane best (singletons and tiny segments)
         int32_t pend = -1;                  // start of the open segment
@@ -2493,6 +2498,89 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
         }
         const int32_t m = rdl(scan_max(best), 63);
         if (lane == 0) atomicMax(a.fmin + r, m);
+    }
+}
+
+// ---- 5a''. pass 0 (production, after k_chain_lb): per read, the segments that
+// can hold its best f.  With fm = k_chain_lb's bound, a segment of len anchors
+// has f <= len * span, so only len >= Lmin = ceil(fm / span) can (k_chain_seg's
+// pruning rule).  When Lmin > CHAIN_TINY every candidate goes to the
+// long-segment queue whole (k_chain_long / k_chain_giant), and the candidates
+// come from k_chain_lb's segment-start bits (1 bit per anchor, isob) without
+// reading a key.  Reads with a weaker bound (no real chain) are queued for
+// k_chain_seg's streaming pass, one (read, chunk) item per seg_chunk anchors.
+// One wave per read; its words are walked from the last 64-word chunk to the
+// first, carrying the first segment start of the later chunks.
+__global__ __launch_bounds__(256) void k_seg_cands(ChainArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
+    const int lane = lane_id();
+    const int32_t span = a.P.span;
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
+        const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);
+        if (A <= 0) continue;
+        const int32_t fm = uni(a.fmin[r]);
+        const uint64_t base = uni64(a.a_off[r]);
+        const uint64_t t0 = wall_clock64();
+        if (fm <= CHAIN_TINY * span) {
+            const uint32_t nit = (uint32_t)((A + (int32_t)a.seg_chunk - 1) / (int32_t)a.seg_chunk);
+            uint32_t q0 = 0;
+            if (lane == 0) q0 = atomicAdd(a.sq_n, nit);
+            q0 = (uint32_t)uni((int32_t)q0);
+            for (uint32_t jj = (uint32_t)lane; jj < nit; jj += 64)
+                if (q0 + jj < a.sq_cap) a.sq[q0 + jj] = make_uint2(r, jj);
+            continue;
+        }
+        const int32_t Lmin = (fm + span - 1) / span;
+        const uint64_t* isw = a.isob + (base >> 6) + r;
+        const int32_t nwd = (A + 63) >> 6;
+        int32_t carry = A;                                   // first segment start after the current chunk
+        uint32_t n_c = 0;
+        int32_t mx = 0;
+        for (int32_t cw = ((nwd - 1) >> 6) << 6; cw >= 0; cw -= 64) {
+            const int32_t wl = cw + lane;
+            const uint64_t m = wl < nwd ? isw[wl] : 0ULL;
+            int32_t fs = m ? wl * 64 + ctz64(m) : INT_MAX;
+            int32_t sfx = fs;                                 // inclusive suffix minimum over the lanes
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) { const int32_t o = __shfl_down(sfx, d, 64); if (lane + d < 64) sfx = min(sfx, o); }
+            int32_t after = __shfl_down(sfx, 1, 64);
+            after = lane == 63 ? carry : min(after, carry);
+            const int32_t cfirst = __shfl(sfx, 0, 64);
+            uint64_t mm = m;
+            if (Lmin >= 64) mm = m ? (1ULL << (63 - clz64(m))) : 0ULL;   // only a word's last start can begin one
+            while (any(mm != 0ULL)) {
+                bool cand = false;
+                int32_t sl = 0, el = 0;
+                if (mm) {
+                    const int b = ctz64(mm);
+                    mm &= mm - 1;
+                    const uint64_t rest = b == 63 ? 0ULL : (m >> (b + 1)) << (b + 1);
+                    sl = wl * 64 + b;
+                    el = rest ? wl * 64 + ctz64(rest) : after;
+                    cand = el - sl >= Lmin;
+                }
+                const uint64_t cm = ballot(cand);
+                if (cm) {
+                    uint32_t q0 = 0;
+                    if (lane == 0) q0 = atomicAdd(a.lseg_n, (uint32_t)__popcll(cm));
+                    q0 = (uint32_t)uni((int32_t)q0);
+                    if (cand) {
+                        const uint32_t q = q0 + (uint32_t)__popcll(cm & lanemask_lt());
+                        if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
+                        mx = max(mx, el - sl);
+                    }
+                    n_c += (uint32_t)__popcll(cm);
+                }
+            }
+            carry = min(carry, cfirst);
+        }
+        const int32_t ml = rdl(scan_max(mx), 63);
+        if (lane == 0) {
+            ReadOut* O = a.out + r;
+            O->t_pass[0] = (uint32_t)(wall_clock64() - t0);
+            O->pad2 = (uint32_t)(ml > 65535 ? 65535 : ml) | ((n_c > 65535 ? 65535u : n_c) << 16);
+        }
     }
 }
 
@@ -3938,7 +4026,11 @@ int launch_filter(const FilterArgs& a, int k, int n_blocks, hipStream_t st) {
     hipLaunchKernelGGL(k_filter_lds, dim3(a.n), dim3(256), 0, st, a, k);
     LAUNCH_CHECK();
     (void)n_blocks;
-    hipLaunchKernelGGL(k_filter, dim3(a.n), dim3(1024), 0, st, a, k);
+    // persistent: one workgroup per CU (its LDS), reads taken by grid stride; most reads of
+    // 10 kb batches are k_filter_lds's and are skipped after one load of their count
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    hipLaunchKernelGGL(k_filter, dim3(std::min<uint32_t>(a.n, (uint32_t)std::max(ncu, 1))), dim3(1024), FB_LDS, st, a, k);
     LAUNCH_CHECK();
     return 0;
 }
@@ -4029,6 +4121,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
         break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
+    case 10: hipLaunchKernelGGL(k_seg_cands, dim3(blocks), dim3(256), 0, st, a); break;
     case 7: hipLaunchKernelGGL(k_chain_giant<false>, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
     case 8: hipLaunchKernelGGL(k_chain_giant<true>, dim3(blocks), dim3(1024), lut_lds(a.P.lut_n), st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 3) / 4), dim3(256), 0, st, a); break;
