@@ -358,7 +358,8 @@ KERNEL_SYMBOLS = {
     "chain_seg": ("k_chain_seg", ""),
     "chain_med": ("k_chain_med", ""), "chain_lorder": ("k_lseg_order", ""), "chain_long": ("k_chain_long", ""),
     "chain_giant": ("k_chain_giant", ""), "chain_fin": ("k_chain_fin", ""),
-    "chain_items_rescue": ("k_seg_items", ""), "chain_seg_rescue": ("k_chain_seg", ""), "chain_med_rescue": ("k_chain_med", ""),
+    "chain_items_rescue": ("k_seg_items", ""), "chain_lb_rescue": ("k_chain_lb", ""), "chain_cands_rescue": ("k_seg_cands", ""),
+    "chain_seg_rescue": ("k_chain_seg", ""), "chain_med_rescue": ("k_chain_med", ""),
     "chain_lorder_rescue": ("k_lseg_order", ""), "chain_giant_rescue": ("k_chain_giant", ""),
     "chain_long_rescue": ("k_chain_long", ""), "chain_fin_rescue": ("k_chain_fin", ""), "dv": ("k_dv", ""),
 }
@@ -400,7 +401,9 @@ def alg_bytes(cnt: dict, res) -> dict:
         "chain_giant": 16 * cnt.get("giant_anchors", 0),
         "chain_fin": 96 * n + 8 * cm,
         "chain_items_rescue": 8 * n,
-        "chain_seg_rescue": 8 * cnt["rescued_anchors"],
+        "chain_lb_rescue": 8 * cnt["rescued_anchors"] + cnt["rescued_anchors"] // 8,
+        "chain_cands_rescue": cnt["rescued_anchors"] // 8 + 12 * n,
+        "chain_seg_rescue": 8 * cnt.get("seg_stream_rescue", cnt["rescued_anchors"]),
         "chain_med_rescue": 16 * cnt.get("med_anchors_rescue", 0),
         "chain_lorder_rescue": 0,
         "chain_giant_rescue": 16 * cnt.get("giant_anchors_rescue", 0),

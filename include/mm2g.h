@@ -365,10 +365,11 @@ int mm2g_prof_reset(mm2g_ctx* ctx);
  * [6]=anchors entering the DP (after the sort's singleton filter); anchors in
  * the DP's long segments below the giant-kernel size [7] / from it on [8] and
  * in its medium segments [9] of pass 0, and [10], [11], [12] of the rescue pass;
- * DP anchors whose keys k_chain_seg streams in pass 0 (the rest take its sparse
- * items) [13] and that k_chain_lb streams [14].
+ * DP anchors whose keys k_chain_seg streams in pass 0 (k_seg_cands finds the
+ * other reads' candidate segments without reading keys) [13], that k_chain_lb
+ * streams [14], and rescued anchors k_chain_seg streams in the rescue pass [15].
  * Copies min(n, MM2G_N_COUNTERS) values; returns how many. */
-#define MM2G_N_COUNTERS 15
+#define MM2G_N_COUNTERS 16
 int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus

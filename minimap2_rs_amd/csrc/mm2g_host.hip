@@ -920,7 +920,6 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         ENSURE(c->sq, uint2, sq_cap, sq);
         ENSURE(c->sq_n, uint32_t, 1, sq_n);
     }
-    ca.seg_streamed = stat ? stat + 5 : nullptr;
     uint32_t* item_off;
     ENSURE(c->item_off, uint32_t, n + 1, item_off);
     ca.item_off = item_off;
@@ -959,28 +958,29 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
             ProfScope ps(c, pass ? "chain_items_rescue" : "chain_items");
             LCHK(launch_chain_stage(6, ca, 1, c->stream));
         }
-        // lower bound of each read's best f: prunes segments (pass 0, not in debug
-        // mode; the rescue pass runs on few reads, where it costs more than it saves)
-        // the rescue pass prunes by pass 0's bound: when the rescue's comput_sc limits are all at
-        // least pass 0's (bw_long >= bw, max_dist_x/y no smaller), every pass-0 transition is
-        // accepted there with the same score, so its best f >= LB_1 >= LB_0 = fmin (no k_chain_lb
-        // of its own).  The reference accepts -r A,B with B < A (main.rs:205-206): then pass-0
-        // steps with dd in (bw_long, bw] are rejected in the rescue and the bound does not hold.
+        // Lower bound of each read's best f (k_chain_lb, this pass's parameters): prunes
+        // segments (not in debug mode).  In the rescue pass (rescued reads only) the bound
+        // is LB_1, raised by pass 0's LB_0 when the rescue's comput_sc limits are all at
+        // least pass 0's (bw_long >= bw, max_dist_x/y no smaller): every pass-0 transition
+        // is then accepted there with the same score, so its best f >= LB_0.  The reference
+        // accepts -r A,B with B < A (main.rs:205-206): then pass-0 steps with dd in
+        // (bw_long, bw] are rejected in the rescue and LB_0 does not bound it.
         const bool rescue_wider = bw_long >= P0.bw && mdx1 >= P0.max_dist_x && mdy1 >= P0.max_dist_y;
-        ca.fmin = (pass == 0 || (K[MM2G_KNOB_PRUNE_RESCUE] && rescue_wider)) ? fmin_buf : nullptr;
-        ca.isob = pass == 0 ? isob : nullptr;
+        ca.fmin = (pass == 0 || K[MM2G_KNOB_PRUNE_RESCUE]) ? fmin_buf : nullptr;
+        ca.isob = isob;
+        ca.seg_streamed = stat ? stat + 5 + pass : nullptr;   // status words 5 / 6
         ca.sq = nullptr; ca.sq_n = nullptr; ca.sq_cap = 0;
-        if (ca.fmin && pass == 0) {
-            HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
+        if (ca.fmin) {
+            if (pass == 0 || !rescue_wider) HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
             {
-                ProfScope ps(c, "chain_lb");
+                ProfScope ps(c, pass ? "chain_lb_rescue" : "chain_lb");
                 LCHK(launch_chain_stage(5, ca, 2048, c->stream));
             }
             if (ca.isob) {   // candidate segments per read; k_chain_seg streams only the reads left over
                 HIPCHK(hipMemsetAsync(sq_n, 0, 4, c->stream));
                 ca.sq = sq; ca.sq_n = sq_n; ca.sq_cap = sq_cap;
-                ProfScope ps(c, "chain_cands");
-                LCHK(launch_chain_stage(10, ca, (int)std::min<uint32_t>((n + 3) / 4, 2048), c->stream));
+                ProfScope ps(c, pass ? "chain_cands_rescue" : "chain_cands");
+                LCHK(launch_chain_stage(10, ca, (int)std::min<uint32_t>((n + 15) / 16, 1024), c->stream));
             }
         }
         ca.lseg_prof = K[MM2G_KNOB_LSEG_PROF] ? 1u : 0u;
@@ -1459,6 +1459,7 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     for (int t = 0; t < 6; ++t) c->counters[7 + t] = c->h_stat[8 + t];   // anchors per chain kernel class and pass
     c->counters[13] = c->h_stat[5];   // DP anchors whose keys k_chain_seg streams (pass 0; the rest: sparse items)
     c->counters[14] = c->h_stat[4];   // ... that k_chain_lb streams (pass 0)
+    c->counters[15] = c->h_stat[6];   // rescued anchors whose keys k_chain_seg streams (pass 1)
     return 0;
 }
 

@@ -223,7 +223,7 @@ struct ChainArgs {
     // anchor (k_chain_lb writes them, k_chain_seg's sparse items read them); read r's words
     // start at (a_off[r] >> 6) + r.  Null: every item streams its keys.
     uint64_t* isob = nullptr;
-    unsigned long long* seg_streamed = nullptr;   // pass 0: anchors of the items k_chain_seg streamed (counter)
+    unsigned long long* seg_streamed = nullptr;   // anchors of the items k_chain_seg streamed in this pass (counter)
     // k_seg_cands -> k_chain_seg (pass 0 with isob): the (read, chunk) items left to streaming
     uint2* sq = nullptr;
     uint32_t* sq_n = nullptr;

@@ -2270,7 +2270,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_seg(ChainArgs a) {
         uint32_t n_big = 0;
         int32_t max_seg = 0;
         const int32_t fm = a.fmin ? uni(a.fmin[r]) : 0;   // segments with len * span < fm are skipped
-        if (lane == 0 && a.seg_streamed && P.pass == 0) atomicAdd(a.seg_streamed, (unsigned long long)(c1 - c0));
+        if (lane == 0 && a.seg_streamed) atomicAdd(a.seg_streamed, (unsigned long long)(c1 - c0));
         int32_t bf = INT_MIN, bi = -1;      // per-lane best (singletons and tiny segments)
         int32_t pend = -1;                  // start of the open segment
         int32_t th0 = 0, th1 = 0, th2 = 0, tt0 = 0, tt1 = 0, tt2 = 0;   // tiny class queue heads / tails
@@ -2445,7 +2445,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     const uint32_t gsh = rb + qb;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
     constexpr int32_t NEG = -(1 << 29);
-    constexpr int U = 4;                      // blocks of 64 keys loaded together
+    constexpr int U = 8;                      // blocks of 64 keys loaded together
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
     const uint32_t n_items = (uint32_t)uni((int32_t)a.item_off[a.n]);
     for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + wave_id(); it < n_items; it += nwaves) {
@@ -2501,7 +2501,8 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     }
 }
 
-// ---- 5a''. pass 0 (production, after k_chain_lb): per read, the segments that
+// ---- 5a''. production, after k_chain_lb (both passes; the rescue pass on its
+// rescued reads): per read, the segments that
 // can hold its best f.  With fm = k_chain_lb's bound, a segment of len anchors
 // has f <= len * span, so only len >= Lmin = ceil(fm / span) can (k_chain_seg's
 // pruning rule).  When Lmin > CHAIN_TINY every candidate goes to the
@@ -2511,76 +2512,106 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
 // k_chain_seg's streaming pass, one (read, chunk) item per seg_chunk anchors.
 // One wave per read; its words are walked from the last 64-word chunk to the
 // first, carrying the first segment start of the later chunks.
-__global__ __launch_bounds__(256) void k_seg_cands(ChainArgs a) {
+// Candidates go to the queues in per-workgroup batches (one global atomic per
+// workgroup and queue: a burst of per-read atomics on one counter serialises).
+constexpr int SC_NW = 16;                 // waves (reads in flight) per workgroup
+constexpr int SC_BUF = 128;               // candidate entries buffered per wave
+__global__ __launch_bounds__(SC_NW * 64) void k_seg_cands(ChainArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
-    const int lane = lane_id();
+    __shared__ uint2 s_buf[SC_NW][SC_BUF];            // (start, end) of this wave's read's candidates
+    __shared__ uint32_t s_cnt[SC_NW], s_rd[SC_NW], s_nit[SC_NW], s_base[2];
+    const int lane = lane_id(), wv = wave_id();
     const int32_t span = a.P.span;
-    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
-        const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);
-        if (A <= 0) continue;
-        const int32_t fm = uni(a.fmin[r]);
-        const uint64_t base = uni64(a.a_off[r]);
-        const uint64_t t0 = wall_clock64();
-        if (fm <= CHAIN_TINY * span) {
-            const uint32_t nit = (uint32_t)((A + (int32_t)a.seg_chunk - 1) / (int32_t)a.seg_chunk);
-            uint32_t q0 = 0;
-            if (lane == 0) q0 = atomicAdd(a.sq_n, nit);
-            q0 = (uint32_t)uni((int32_t)q0);
-            for (uint32_t jj = (uint32_t)lane; jj < nit; jj += 64)
-                if (q0 + jj < a.sq_cap) a.sq[q0 + jj] = make_uint2(r, jj);
-            continue;
-        }
-        const int32_t Lmin = (fm + span - 1) / span;
-        const uint64_t* isw = a.isob + (base >> 6) + r;
-        const int32_t nwd = (A + 63) >> 6;
-        int32_t carry = A;                                   // first segment start after the current chunk
-        uint32_t n_c = 0;
-        int32_t mx = 0;
-        for (int32_t cw = ((nwd - 1) >> 6) << 6; cw >= 0; cw -= 64) {
-            const int32_t wl = cw + lane;
-            const uint64_t m = wl < nwd ? isw[wl] : 0ULL;
-            int32_t fs = m ? wl * 64 + ctz64(m) : INT_MAX;
-            int32_t sfx = fs;                                 // inclusive suffix minimum over the lanes
+    const uint32_t rounds = (a.n + SC_NW - 1) / SC_NW;
+    for (uint32_t g = blockIdx.x; g < rounds; g += gridDim.x) {
+        const uint32_t r = g * SC_NW + (uint32_t)wv;
+        // one read per wave: its candidates to s_buf (or the queue directly past SC_BUF), or its
+        // streaming items' count to s_nit
+        uint32_t nc = 0, nit = 0;
+        if (r < a.n) {
+            const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);
+            const int32_t fm = uni(a.fmin[r]);
+            const uint64_t base = uni64(a.a_off[r]);
+            const bool on = a.P.pass == 0 || (uni(a.out[r].flags) & RF_RESCUED);   // the rescue pass maps rescued reads only
+            const uint64_t t0 = wall_clock64();
+            if (A > 0 && on && fm <= CHAIN_TINY * span) {
+                nit = (uint32_t)((A + (int32_t)a.seg_chunk - 1) / (int32_t)a.seg_chunk);
+            } else if (A > 0 && on) {
+                const int32_t Lmin = (fm + span - 1) / span;
+                const uint64_t* isw = a.isob + (base >> 6) + r;
+                const int32_t nwd = (A + 63) >> 6;
+                int32_t carry = A;                               // first segment start after the current chunk
+                int32_t mx = 0;
+                int32_t cw = ((nwd - 1) >> 6) << 6;
+                uint64_t mnext = cw + lane < nwd ? isw[cw + lane] : 0ULL;
+                for (; cw >= 0; cw -= 64) {                      // last chunk first, the next one's words in flight
+                    const int32_t wl = cw + lane;
+                    const uint64_t m = mnext;
+                    mnext = (cw >= 64) ? isw[cw - 64 + lane] : 0ULL;
+                    const int32_t fs = m ? wl * 64 + ctz64(m) : INT_MAX;
+                    int32_t sfx = fs;                            // inclusive suffix minimum over the lanes
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) { const int32_t o = __shfl_down(sfx, d, 64); if (lane + d < 64) sfx = min(sfx, o); }
-            int32_t after = __shfl_down(sfx, 1, 64);
-            after = lane == 63 ? carry : min(after, carry);
-            const int32_t cfirst = __shfl(sfx, 0, 64);
-            uint64_t mm = m;
-            if (Lmin >= 64) mm = m ? (1ULL << (63 - clz64(m))) : 0ULL;   // only a word's last start can begin one
-            while (any(mm != 0ULL)) {
-                bool cand = false;
-                int32_t sl = 0, el = 0;
-                if (mm) {
-                    const int b = ctz64(mm);
-                    mm &= mm - 1;
-                    const uint64_t rest = b == 63 ? 0ULL : (m >> (b + 1)) << (b + 1);
-                    sl = wl * 64 + b;
-                    el = rest ? wl * 64 + ctz64(rest) : after;
-                    cand = el - sl >= Lmin;
-                }
-                const uint64_t cm = ballot(cand);
-                if (cm) {
-                    uint32_t q0 = 0;
-                    if (lane == 0) q0 = atomicAdd(a.lseg_n, (uint32_t)__popcll(cm));
-                    q0 = (uint32_t)uni((int32_t)q0);
-                    if (cand) {
-                        const uint32_t q = q0 + (uint32_t)__popcll(cm & lanemask_lt());
-                        if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
-                        mx = max(mx, el - sl);
+                    for (int d = 1; d < 64; d <<= 1) { const int32_t o = __shfl_down(sfx, d, 64); if (lane + d < 64) sfx = min(sfx, o); }
+                    int32_t after = __shfl_down(sfx, 1, 64);
+                    after = lane == 63 ? carry : min(after, carry);
+                    const int32_t cfirst = __shfl(sfx, 0, 64);
+                    uint64_t mm = m;
+                    if (Lmin >= 64) mm = m ? (1ULL << (63 - clz64(m))) : 0ULL;   // only a word's last start can begin one
+                    while (any(mm != 0ULL)) {
+                        bool cand = false;
+                        int32_t sl = 0, el = 0;
+                        if (mm) {
+                            const int b = ctz64(mm);
+                            mm &= mm - 1;
+                            const uint64_t rest = b == 63 ? 0ULL : (m >> (b + 1)) << (b + 1);
+                            sl = wl * 64 + b;
+                            el = rest ? wl * 64 + ctz64(rest) : after;
+                            cand = el - sl >= Lmin;
+                        }
+                        const uint64_t cm = ballot(cand);
+                        if (cm) {
+                            const uint32_t k = nc + (uint32_t)__popcll(cm & lanemask_lt());
+                            if (cand) {
+                                if (k < (uint32_t)SC_BUF) s_buf[wv][k] = make_uint2((uint32_t)sl, (uint32_t)el);
+                                else {                           // rare: a read with more than SC_BUF candidates
+                                    const uint32_t q = atomicAdd(a.lseg_n, 1u);
+                                    if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
+                                }
+                                mx = max(mx, el - sl);
+                            }
+                            nc += (uint32_t)__popcll(cm);
+                        }
                     }
-                    n_c += (uint32_t)__popcll(cm);
+                    carry = min(carry, cfirst);
+                }
+                const int32_t ml = rdl(scan_max(mx), 63);
+                if (lane == 0) {
+                    ReadOut* O = a.out + r;
+                    O->t_pass[a.P.pass] = (uint32_t)(wall_clock64() - t0);
+                    const uint32_t st6 = (uint32_t)(ml > 65535 ? 65535 : ml) | ((nc > 65535 ? 65535u : nc) << 16);
+                    if (a.P.pass == 0) O->pad2 = st6; else O->n_deep = st6;
                 }
             }
-            carry = min(carry, cfirst);
         }
-        const int32_t ml = rdl(scan_max(mx), 63);
-        if (lane == 0) {
-            ReadOut* O = a.out + r;
-            O->t_pass[0] = (uint32_t)(wall_clock64() - t0);
-            O->pad2 = (uint32_t)(ml > 65535 ? 65535 : ml) | ((n_c > 65535 ? 65535u : n_c) << 16);
+        if (lane == 0) { s_cnt[wv] = min(nc, (uint32_t)SC_BUF); s_nit[wv] = nit; s_rd[wv] = r; }
+        __syncthreads();
+        if (threadIdx.x == 0) {                              // one atomic per queue for the workgroup
+            uint32_t tc = 0, ti = 0;
+            for (int w = 0; w < SC_NW; ++w) { tc += s_cnt[w]; ti += s_nit[w]; }
+            s_base[0] = tc ? atomicAdd(a.lseg_n, tc) : 0u;
+            s_base[1] = ti ? atomicAdd(a.sq_n, ti) : 0u;
         }
+        __syncthreads();
+        uint32_t oc = s_base[0], oi = s_base[1];
+        for (int w = 0; w < wv; ++w) { oc += s_cnt[w]; oi += s_nit[w]; }
+        const uint32_t myc = s_cnt[wv], myi = s_nit[wv], rr = s_rd[wv];
+        for (uint32_t k = (uint32_t)lane; k < myc; k += 64) {
+            const uint2 e = s_buf[wv][k];
+            if (oc + k < a.lseg_cap) a.lseg[oc + k] = make_uint4(rr, e.x, e.y, 0u);
+        }
+        for (uint32_t k = (uint32_t)lane; k < myi; k += 64)
+            if (oi + k < a.sq_cap) a.sq[oi + k] = make_uint2(rr, k);
+        __syncthreads();                                     // s_buf / s_cnt are reused by the next round
     }
 }
 
@@ -4121,7 +4152,7 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
         break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
-    case 10: hipLaunchKernelGGL(k_seg_cands, dim3(blocks), dim3(256), 0, st, a); break;
+    case 10: hipLaunchKernelGGL(k_seg_cands, dim3(blocks), dim3(SC_NW * 64), 0, st, a); break;
     case 7: hipLaunchKernelGGL(k_chain_giant<false>, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
     case 8: hipLaunchKernelGGL(k_chain_giant<true>, dim3(blocks), dim3(1024), lut_lds(a.P.lut_n), st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 3) / 4), dim3(256), 0, st, a); break;

@@ -14,6 +14,7 @@
 #   prof1   the same with one context (--streams 1): every launch alone on the GPU, the
 #           conditions of the bench line's quiet-GPU roofline figure
 #   c5s1    C5 with one context and one unit per batch, with the long-segment profile
+#   c3p     C3 phase profiles (one context, one unit): sketch, sort, long segments
 #   pmc     FETCH_SIZE and WRITE_SIZE passes (separate runs) -> pmc_traffic.json
 #   sq      one SQ counter pass (stall shares, LDS bank conflicts), 1 stream
 #   ab      alternate bench runs of knob sets: AB="sort_lds_kb=157|sort_lds_kb=128" N=3
@@ -74,6 +75,9 @@ for S in "${STEPS[@]}"; do
     c5s1)
       timeout -k 10 600 python -u bench.py $QUIET --reads 2000 --read-len 100000 --steps 3 --warmup 1 --streams 1 --shares 1 --knob lseg_prof=1 $BARGS \
         > "$OUT/c5s1.json" 2> "$OUT/c5s1.err"; line "$OUT/c5s1.json"; grep -E "_prof\]" "$OUT/c5s1.err" | cut -c1-600 > "$OUT/c5s1_prof.txt" || true ;;
+    c3p)
+      timeout -k 10 300 python -u bench.py $QUIET --steps 1 --warmup 1 --streams 1 --shares 1 --knob lseg_prof=1 --knob sketch_prof=1 --knob sort_prof=1 $BARGS \
+        > "$OUT/c3p.json" 2> "$OUT/c3p.err"; grep -E "_prof\]" "$OUT/c3p.err" | cut -c1-900 > "$OUT/c3p_prof.txt" || true ;;
     pmc)
       timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmcF" -o run -- python3 bench.py $QUIET --steps 6 --warmup 1 $BARGS > "$OUT/pmcF.json" 2> "$OUT/pmcF.err"
       timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmcW" -o run -- python3 bench.py $QUIET --steps 6 --warmup 1 $BARGS > "$OUT/pmcW.json" 2> "$OUT/pmcW.err"
