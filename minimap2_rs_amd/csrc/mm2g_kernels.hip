@@ -2445,7 +2445,7 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
     const uint32_t gsh = rb + qb;
     const int32_t maxdx = P.max_dist_x, maxdy = P.max_dist_y, bw = P.bw, span = P.span;
     constexpr int32_t NEG = -(1 << 29);
-    constexpr int U = 8;                      // blocks of 64 keys loaded together
+    constexpr int U = 4;                      // blocks of 64 keys loaded together
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
     const uint32_t n_items = (uint32_t)uni((int32_t)a.item_off[a.n]);
     for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + wave_id(); it < n_items; it += nwaves) {
@@ -2514,8 +2514,12 @@ __global__ __launch_bounds__(256) void k_chain_lb(ChainArgs a) {
 // first, carrying the first segment start of the later chunks.
 // Candidates go to the queues in per-workgroup batches (one global atomic per
 // workgroup and queue: a burst of per-read atomics on one counter serialises).
+// A read's segment-start words are split lane-major (lane l takes K = nwd/64
+// consecutive words), so all of a read's loads are in flight together; the
+// first start after a lane's words is a suffix minimum over the lanes.
 constexpr int SC_NW = 16;                 // waves (reads in flight) per workgroup
 constexpr int SC_BUF = 128;               // candidate entries buffered per wave
+constexpr int SC_KW = 8;                  // words per lane per load group
 __global__ __launch_bounds__(SC_NW * 64) void k_seg_cands(ChainArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint2 s_buf[SC_NW][SC_BUF];            // (start, end) of this wave's read's candidates
@@ -2525,9 +2529,9 @@ __global__ __launch_bounds__(SC_NW * 64) void k_seg_cands(ChainArgs a) {
     const uint32_t rounds = (a.n + SC_NW - 1) / SC_NW;
     for (uint32_t g = blockIdx.x; g < rounds; g += gridDim.x) {
         const uint32_t r = g * SC_NW + (uint32_t)wv;
-        // one read per wave: its candidates to s_buf (or the queue directly past SC_BUF), or its
-        // streaming items' count to s_nit
-        uint32_t nc = 0, nit = 0;
+        if (lane == 0) s_cnt[wv] = 0;
+        wave_lds_sync();
+        uint32_t nit = 0;
         if (r < a.n) {
             const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);
             const int32_t fm = uni(a.fmin[r]);
@@ -2540,60 +2544,80 @@ __global__ __launch_bounds__(SC_NW * 64) void k_seg_cands(ChainArgs a) {
                 const int32_t Lmin = (fm + span - 1) / span;
                 const uint64_t* isw = a.isob + (base >> 6) + r;
                 const int32_t nwd = (A + 63) >> 6;
-                int32_t carry = A;                               // first segment start after the current chunk
-                int32_t mx = 0;
-                int32_t cw = ((nwd - 1) >> 6) << 6;
-                uint64_t mnext = cw + lane < nwd ? isw[cw + lane] : 0ULL;
-                for (; cw >= 0; cw -= 64) {                      // last chunk first, the next one's words in flight
-                    const int32_t wl = cw + lane;
-                    const uint64_t m = mnext;
-                    mnext = (cw >= 64) ? isw[cw - 64 + lane] : 0ULL;
-                    const int32_t fs = m ? wl * 64 + ctz64(m) : INT_MAX;
-                    int32_t sfx = fs;                            // inclusive suffix minimum over the lanes
+                const int32_t K = (nwd + 63) >> 6;
+                const int32_t w0 = min(nwd, lane * K), w1 = min(nwd, w0 + K);
+                const int32_t ng = (K + SC_KW - 1) / SC_KW;       // load groups per lane (wave-uniform)
+                uint64_t wd[SC_KW];
+                // pass A: this lane's first segment start (its earliest nonzero word)
+                int32_t first = INT_MAX;
+                for (int32_t gq = 0; gq < ng; ++gq) {
+                    if (ballot(first == INT_MAX) == 0ULL) break;
+                    const int32_t gb = w0 + gq * SC_KW;
 #pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) { const int32_t o = __shfl_down(sfx, d, 64); if (lane + d < 64) sfx = min(sfx, o); }
-                    int32_t after = __shfl_down(sfx, 1, 64);
-                    after = lane == 63 ? carry : min(after, carry);
-                    const int32_t cfirst = __shfl(sfx, 0, 64);
-                    uint64_t mm = m;
-                    if (Lmin >= 64) mm = m ? (1ULL << (63 - clz64(m))) : 0ULL;   // only a word's last start can begin one
-                    while (any(mm != 0ULL)) {
-                        bool cand = false;
-                        int32_t sl = 0, el = 0;
-                        if (mm) {
-                            const int b = ctz64(mm);
-                            mm &= mm - 1;
-                            const uint64_t rest = b == 63 ? 0ULL : (m >> (b + 1)) << (b + 1);
-                            sl = wl * 64 + b;
-                            el = rest ? wl * 64 + ctz64(rest) : after;
-                            cand = el - sl >= Lmin;
-                        }
-                        const uint64_t cm = ballot(cand);
-                        if (cm) {
-                            const uint32_t k = nc + (uint32_t)__popcll(cm & lanemask_lt());
-                            if (cand) {
-                                if (k < (uint32_t)SC_BUF) s_buf[wv][k] = make_uint2((uint32_t)sl, (uint32_t)el);
-                                else {                           // rare: a read with more than SC_BUF candidates
-                                    const uint32_t q = atomicAdd(a.lseg_n, 1u);
-                                    if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
-                                }
-                                mx = max(mx, el - sl);
-                            }
-                            nc += (uint32_t)__popcll(cm);
-                        }
+                    for (int u = 0; u < SC_KW; ++u) wd[u] = gb + u < w1 ? isw[gb + u] : 0ULL;
+                    if (first == INT_MAX) {
+#pragma unroll
+                        for (int u = SC_KW - 1; u >= 0; --u) if (wd[u]) first = (gb + u) * 64 + ctz64(wd[u]);
                     }
-                    carry = min(carry, cfirst);
+                }
+                int32_t sfx = first;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) { const int32_t o = __shfl_down(sfx, d, 64); if (lane + d < 64) sfx = min(sfx, o); }
+                int32_t after = __shfl_down(sfx, 1, 64);
+                after = lane == 63 ? A : min(after, A);
+                // pass B: each lane walks its words from the last to the first (lane-divergent, no
+                // cross-lane work inside); candidates to the wave's LDS buffer
+                int32_t mx = 0;
+                auto push = [&](int32_t sl, int32_t el) {
+                    const uint32_t k = atomicAdd(&s_cnt[wv], 1u);
+                    if (k < (uint32_t)SC_BUF) s_buf[wv][k] = make_uint2((uint32_t)sl, (uint32_t)el);
+                    else {                                     // rare: more than SC_BUF candidates in one read
+                        const uint32_t q = atomicAdd(a.lseg_n, 1u);
+                        if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
+                    }
+                    mx = max(mx, el - sl);
+                };
+                for (int32_t gq = ng - 1; gq >= 0; --gq) {
+                    const int32_t gb = w0 + gq * SC_KW;
+                    if (ng > 1) {                               // one group: its words are still in wd
+#pragma unroll
+                        for (int u = 0; u < SC_KW; ++u) wd[u] = gb + u < w1 ? isw[gb + u] : 0ULL;
+                    }
+#pragma unroll
+                    for (int u = SC_KW - 1; u >= 0; --u) {
+                        const uint64_t m = wd[u];
+                        if (!m) continue;
+                        const int32_t w = gb + u;
+                        if (Lmin >= 64) {                         // only a word's last start can begin one
+                            const int32_t sl = w * 64 + 63 - clz64(m);
+                            if (after - sl >= Lmin) push(sl, after);
+                        } else {
+                            uint64_t mm = m;
+                            int32_t e = after;
+                            while (mm) {                          // starts from the highest down
+                                const int b = 63 - clz64(mm);
+                                mm &= ~(1ULL << b);
+                                const int32_t sl = w * 64 + b;
+                                if (e - sl >= Lmin) push(sl, e);
+                                e = sl;
+                            }
+                        }
+                        after = w * 64 + ctz64(m);
+                    }
                 }
                 const int32_t ml = rdl(scan_max(mx), 63);
+                wave_lds_sync();
                 if (lane == 0) {
                     ReadOut* O = a.out + r;
                     O->t_pass[a.P.pass] = (uint32_t)(wall_clock64() - t0);
-                    const uint32_t st6 = (uint32_t)(ml > 65535 ? 65535 : ml) | ((nc > 65535 ? 65535u : nc) << 16);
+                    const uint32_t ncs = s_cnt[wv];
+                    const uint32_t st6 = (uint32_t)(ml > 65535 ? 65535 : ml) | ((ncs > 65535 ? 65535u : ncs) << 16);
                     if (a.P.pass == 0) O->pad2 = st6; else O->n_deep = st6;
                 }
             }
         }
-        if (lane == 0) { s_cnt[wv] = min(nc, (uint32_t)SC_BUF); s_nit[wv] = nit; s_rd[wv] = r; }
+        wave_lds_sync();
+        if (lane == 0) { s_cnt[wv] = min(s_cnt[wv], (uint32_t)SC_BUF); s_nit[wv] = nit; s_rd[wv] = r; }
         __syncthreads();
         if (threadIdx.x == 0) {                              // one atomic per queue for the workgroup
             uint32_t tc = 0, ti = 0;
