@@ -339,7 +339,8 @@ enum {
     MM2G_KNOB_SEG_SPARSE = 31,   /* pass 0: work items whose reads' best-f bound rules out every segment of <= 8
                                     anchors find their candidate segments from k_chain_lb's segment-start bits
                                     instead of streaming their keys [1]                                       */
-    MM2G_KNOB_COUNT = 32
+    MM2G_KNOB_SPEC_BATCH = 32,   /* predecessors per step of k_chain_long's speculative rounds: 4 or 8 [4]     */
+    MM2G_KNOB_COUNT = 33
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

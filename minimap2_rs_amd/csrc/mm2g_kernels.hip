@@ -2805,7 +2805,9 @@ __global__ __launch_bounds__(1024) void k_lseg_order(ChainArgs a) {
 // step, [19] taken through the exact loop; [18] 64-predecessor window steps;
 // cycles of the per-anchor path's [20] st window, [21] simple / shortcut
 // attempt, [22] exact loop, [23] register shift + ring store.
-template <bool PROF>
+// SB: predecessors per step of the speculative rounds (their LDS loads and
+// comput_sc issued together; MM2G_KNOB_SPEC_BATCH)
+template <bool PROF, int SB>
 __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     extern __shared__ __align__(16) unsigned char smem[];
@@ -2941,12 +2943,12 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     // four predecessors per step: their loads and comput_sc are
                     // independent (issued together), only the running maximum /
                     // n_skip / marks update is sequential
-                    for (int d0 = 1; d0 <= 64; d0 += 4) {
+                    for (int d0 = 1; d0 <= 64; d0 += SB) {
                         if (!any(act0 && !brk && d0 <= dlim)) break;
-                        int32_t sv4[4], pp4[4];
-                        bool ok4[4];
+                        int32_t sv4[SB], pp4[SB];
+                        bool ok4[SB];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
+                        for (int u = 0; u < SB; ++u) {
                             const int d = d0 + u;
                             const bool inr = act0 && d <= dlim;
                             const int32_t j = k - d;
@@ -2961,7 +2963,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                             pp4[u] = fpj.y;
                         }
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
+                        for (int u = 0; u < SB; ++u) {
                             const int d = d0 + u;
                             const bool act = act0 && !brk && d <= dlim;
                             vis += act ? 1 : 0;
@@ -4153,7 +4155,7 @@ int chain_max_blocks(int lut_n, int which) {
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     hipError_t e = which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_seg, DP_NW * 64, seg_lds(lut_n))
-                   : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_long<false>, DP_NW * 64, chain_lds(lut_n))
+                   : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_long<false, 4>, DP_NW * 64, chain_lds(lut_n))
                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_chain_med, 256, lut_lds(lut_n));
     if (e != hipSuccess) return 0;
     return ncu * (per > 0 ? per : 1);
@@ -4171,8 +4173,11 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 1: hipLaunchKernelGGL(k_chain_med, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 2: hipLaunchKernelGGL(k_lseg_order, dim3(1), dim3(1024), 0, st, a); break;
     case 3:
-        if (a.lseg_prof) hipLaunchKernelGGL(k_chain_long<true>, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
-        else hipLaunchKernelGGL(k_chain_long<false>, dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
+        if (a.lseg_prof) {
+            if (a.spec_batch == 8) hipLaunchKernelGGL((k_chain_long<true, 8>), dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
+            else hipLaunchKernelGGL((k_chain_long<true, 4>), dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
+        } else if (a.spec_batch == 8) hipLaunchKernelGGL((k_chain_long<false, 8>), dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
+        else hipLaunchKernelGGL((k_chain_long<false, 4>), dim3(blocks), dim3(DP_NW * 64), chain_lds(a.P.lut_n), st, a);
         break;
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
