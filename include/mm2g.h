@@ -340,7 +340,9 @@ enum {
                                     anchors find their candidate segments from k_chain_lb's segment-start bits
                                     instead of streaming their keys [1]                                       */
     MM2G_KNOB_SPEC_BATCH = 32,   /* predecessors per step of k_chain_long's speculative rounds: 4 or 8 [4]     */
-    MM2G_KNOB_COUNT = 33
+    MM2G_KNOB_DV_PAR = 33,       /* odd index k: k_dv matches the chain against the minimizer positions by one
+                                    parallel search per chain anchor instead of the sequential walk [1]     */
+    MM2G_KNOB_COUNT = 34
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

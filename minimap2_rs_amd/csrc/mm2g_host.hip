@@ -106,6 +106,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_VIEW_READS: return 2048;
     case MM2G_KNOB_SEG_SPARSE: return 1;
     case MM2G_KNOB_SPEC_BATCH: return 4;
+    case MM2G_KNOB_DV_PAR: return 1;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -747,7 +748,7 @@ int mm2g_batch_set_reads_nt4(mm2g_ctx* c, const mm2g_nt4_batch* b) {
 // Sketch the resident batch into sk's slots (one slot of L+16 per read, or the
 // exact layout a previous overflow recorded).  A read whose minimizers do not
 // fit is clamped and flagged in *ovf; mm2g_batch_results re-runs the batch.
-static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf) {
+static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf, ReadOut* zout = nullptr, unsigned long long* zst = nullptr) {
     const uint32_t n = c->n_reads;
     uint64_t *base, *end, *x; uint32_t *y, *cnt, *need;
     ENSURE(B.base, uint64_t, n + 1, base); ENSURE(B.end, uint64_t, n + 1, end);
@@ -755,9 +756,12 @@ static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf) {
     const uint32_t slot = c->redo ? 0u : (uint32_t)std::max<int64_t>(0, std::min<int64_t>(c->knob[MM2G_KNOB_WS_MIN], 1 << 30));
     if (!B.exact) B.cap = slot ? (uint64_t)slot * n + 16 : c->total_bases + 16ull * n + 16;
     ENSURE(B.x, uint64_t, B.cap, x); ENSURE(B.y, uint32_t, B.cap, y);
-    if (!B.exact) {
+    if (!B.exact) {   // (zout / zst: the batch's outputs and status block are cleared here too)
         ProfScope ps(c, "mz_base");
-        LCHK(launch_mz_base(n, c->d_rd_off, base, end, slot, c->stream));
+        LCHK(launch_mz_base(n, c->d_rd_off, base, end, slot, c->stream, zout, zst, STAT_WORDS));
+    } else {
+        if (zout) HIPCHK(hipMemsetAsync(zout, 0, sizeof(ReadOut) * ((size_t)n + 1), c->stream));
+        if (zst) HIPCHK(hipMemsetAsync(zst, 0, STAT_WORDS * 8, c->stream));
     }
     SketchArgs a{nullptr, c->d_rd_off, n, w, k, base, end, x, y, cnt, ovf};
     a.pk_words = c->d_words; a.pk_off = c->d_pk_off; a.amb_off = c->d_amb_off; a.mz_need = need;
@@ -879,13 +883,13 @@ static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_
 static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const ChainKParams& P0, float gap, int npass, int32_t mdx1,
                      int32_t mdy1, int32_t bw_long, uint64_t A_cap, const uint64_t* a_off, const uint32_t* a_cnt, uint64_t* keys,
                      uint64_t* ktmp, const uint32_t* cnt2, const uint64_t* smax, ReadOut* out, const uint32_t* abort, bool full,
-                     unsigned long long* stat = nullptr) {
+                     unsigned long long* stat = nullptr, bool order_ready = false) {
     int32_t *fb, *pb;
     ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
     int16_t* lut; uint32_t* work;
     if (int e = upload_lut(c, gap, std::max(P0.bw, npass > 1 ? bw_long : 0) + 1, &lut)) return e;
     ENSURE(c->work, uint32_t, 4, work);
-    HIPCHK(hipMemsetAsync(work, 0, 16, c->stream));   // [0..1] k_chain_giant hand-out per pass
+    // work: [0..1] k_chain_giant hand-out per pass (k_seg_items of pass 0 clears it)
     uint32_t* order;
     ENSURE(c->order, uint32_t, n, order);
     int32_t* tmark;
@@ -900,7 +904,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     const uint32_t mcap2 = (uint32_t)std::min<uint64_t>(A_cap / (CHAIN_TINY + 1) + 64, 0xffffffffu);
     uint4* mseg;
     ENSURE(c->mseg, uint4, mcap2, mseg);
-    LCHK(launch_read_order(n, a_cnt, order, c->stream));
+    if (!order_ready) LCHK(launch_read_order(n, a_cnt, order, c->stream));   // map_enqueue made the same order
     const int64_t* K = c->knob;
     const bool lazy = (!full && K[MM2G_KNOB_LAZY]) || K[MM2G_KNOB_LAZY] == 2;   // 2: also with full DP arrays (tests)
     ChainArgs ca{n, rd_off, a_off, keys, fb, pb, (uint32_t*)ktmp, lut, P0, c->kl, out, work,
@@ -950,16 +954,9 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         if (lb <= 0) lb = 1024;
         if (mb <= 0) mb = 1024;
         sb = std::max(1, std::min((int)((n * 4 + 3) / 4), sb));   // items: up to ~4 chunks per read
-        HIPCHK(hipMemsetAsync(rbest, 0, (size_t)n * 8, c->stream));
-        // long count (pass 0/1 slot), medium count, medium taken
-        HIPCHK(hipMemsetAsync(lseg_n + pass, 0, 16 - 4 * (size_t)pass, c->stream));
         static const char* names[2][5] = {{"chain_seg", "chain_med", "chain_lorder", "chain_long", "chain_fin"},
                                           {"chain_seg_rescue", "chain_med_rescue", "chain_lorder_rescue", "chain_long_rescue", "chain_fin_rescue"}};
         const int blocks[5] = {sb, mb, 1, lb, 0};
-        {
-            ProfScope ps(c, pass ? "chain_items_rescue" : "chain_items");
-            LCHK(launch_chain_stage(6, ca, 1, c->stream));
-        }
         // Lower bound of each read's best f (k_chain_lb, this pass's parameters): prunes
         // segments (not in debug mode).  In the rescue pass (rescued reads only) the bound
         // is LB_1, raised by pass 0's LB_0 when the rescue's comput_sc limits are all at
@@ -971,16 +968,20 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         ca.fmin = (pass == 0 || K[MM2G_KNOB_PRUNE_RESCUE]) ? fmin_buf : nullptr;
         ca.isob = isob;
         ca.seg_streamed = stat ? stat + 5 + pass : nullptr;   // status words 5 / 6
-        ca.sq = nullptr; ca.sq_n = nullptr; ca.sq_cap = 0;
+        ca.zero_fmin = ca.fmin && (pass == 0 || !rescue_wider) ? 1u : 0u;   // cleared by k_seg_items
+        ca.sq = nullptr; ca.sq_cap = 0;
+        ca.sq_n = (ca.fmin && isob) ? sq_n : nullptr;                      // ... as is the item counter
+        {
+            ProfScope ps(c, pass ? "chain_items_rescue" : "chain_items");
+            LCHK(launch_chain_stage(6, ca, 1, c->stream));
+        }
         if (ca.fmin) {
-            if (pass == 0 || !rescue_wider) HIPCHK(hipMemsetAsync(ca.fmin, 0, (size_t)n * 4, c->stream));
             {
                 ProfScope ps(c, pass ? "chain_lb_rescue" : "chain_lb");
                 LCHK(launch_chain_stage(5, ca, 2048, c->stream));
             }
             if (ca.isob) {   // candidate segments per read; k_chain_seg streams only the reads left over
-                HIPCHK(hipMemsetAsync(sq_n, 0, 4, c->stream));
-                ca.sq = sq; ca.sq_n = sq_n; ca.sq_cap = sq_cap;
+                ca.sq = sq; ca.sq_cap = sq_cap;
                 ProfScope ps(c, pass ? "chain_cands_rescue" : "chain_cands");
                 LCHK(launch_chain_stage(10, ca, (int)std::min<uint32_t>((n + 15) / 16, 1024), c->stream));
             }
@@ -1151,8 +1152,10 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     unsigned long long* st;
     ENSURE(c->dstat, unsigned long long, STAT_WORDS, st);
     uint32_t* st32 = (uint32_t*)st;
-    HIPCHK(hipMemsetAsync(out, 0, sizeof(ReadOut) * (n + 1), c->stream));
-    HIPCHK(hipMemsetAsync(st, 0, STAT_WORDS * 8, c->stream));
+    if (n == 0) {
+        HIPCHK(hipMemsetAsync(out, 0, sizeof(ReadOut), c->stream));
+        HIPCHK(hipMemsetAsync(st, 0, STAT_WORDS * 8, c->stream));
+    }
     if (c->h_out_cap < (size_t)n + 1) {
         HIPCHK(hipStreamSynchronize(c->stream));   // a previous batch's copy may still target it
         if (c->h_out) (void)hipHostFree(c->h_out);
@@ -1167,7 +1170,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         return 0;
     }
     // 1. sketch (CLI w/k, rid 0: seeds.rs:7-11)
-    if (int e = run_sketch(c, o->w, o->k, c->sk1, (int32_t*)st32)) return e;
+    if (int e = run_sketch(c, o->w, o->k, c->sk1, (int32_t*)st32, out, st)) return e;   // clears out[] and st[] first
     const uint64_t mcap = c->sk1.cap;
     uint64_t* mz_base = (uint64_t*)c->sk1.base.p; uint32_t* mz_cnt = (uint32_t*)c->sk1.cnt.p;
     // 2. query filter (seeds.rs:13-36; (10, 0.01) hard-wired at main.rs:195).  Only
@@ -1284,7 +1287,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     if (chain) {
         // 5. chain DP + fallback + rescue
         if (int e = run_chain(c, n, c->d_rd_off, P, gap, npass, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
-                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, full, st))
+                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, full, st, true))
             return e;
         // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
         const bool sep = (H.w != o->w || H.k != o->k);
@@ -1297,6 +1300,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         DvArgs da{n, a_off, keys, (const uint32_t*)ktmp, (const uint64_t*)D.base.p, (const uint32_t*)D.cnt.p, (const uint32_t*)D.y.p, kl, o->k,
                   out, c->keys.cap / 8, D.y.cap / 4};
         da.abort = st32;
+        da.strict = (H.k & 1) && c->knob[MM2G_KNOB_DV_PAR] ? 1u : 0u;   // odd k: positions strictly increase
         ProfScope ps(c, "dv");
         if (stop_at != 4) LCHK(launch_dv(da, c->stream));
     }

@@ -229,6 +229,7 @@ struct ChainArgs {
     uint2* sq = nullptr;
     uint32_t* sq_n = nullptr;
     uint32_t sq_cap = 0;
+    uint32_t zero_fmin = 0;   // k_seg_items clears fmin[0, n) (the pass's LB starts from 0)
 };
 struct DvArgs {
     uint32_t n;
@@ -238,6 +239,7 @@ struct DvArgs {
     ReadOut* out;
     uint64_t cap_keys, cap_mz;
     const uint32_t* abort = nullptr;
+    uint32_t strict = 0;      // the dv sketch's k is odd: its minimizer positions strictly increase (parallel match)
 };
 
 }  // namespace mm2g
@@ -266,7 +268,9 @@ int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, in
 // per-batch sums for the counters: status64[3] = sum mz_cnt, status64[4] = sum cnt2
 int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st);
 // minimizer slots: read r gets [rd_off[r] + 16r, rd_off[r+1] + 16(r+1)), or `slot` entries each when non-zero (tests)
-int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st);
+// (zout / zst: also zero out[0, n] and zst[0, zst_words) -- the map's first kernel)
+int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st,
+                   mm2g::ReadOut* zout = nullptr, unsigned long long* zst = nullptr, int zst_words = 0);
 // query sketch views: per-read view counts; view table from their exclusive scan vo; per-read concatenation
 int launch_view_count(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t* nv, hipStream_t st);
 int launch_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, const uint64_t* vo, uint32_t* v_read, uint64_t* v_off,

@@ -955,9 +955,15 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     uint64_t* K = a.keys;
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < A ? K[CK(base + i, a.cap_keys)] : U64MAX;
     __syncthreads();
+    // Thread t (256 threads) exchanges pairs (i, i ^ j) with i = t + 256 u, i < i ^ j.  For
+    // j < 64 both elements stay with the same wave from stage to stage, for j >= 256 with the
+    // same thread: only the stages j = 64 and 128 move elements between waves and need the
+    // workgroup barrier (7 of the 55 stages of a 1024-key sort; the others a wave-level one).
     for (uint32_t kk = 2; kk <= np; kk <<= 1) {
         for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+            const bool xw = j >= 64 && j < 256;
+            if (xw) __syncthreads();
+            for (uint32_t i = threadIdx.x; i < np; i += 256) {
                 const uint32_t ixj = i ^ j;
                 if (ixj > i) {
                     const uint64_t x = s[i], y = s[ixj];
@@ -965,7 +971,8 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
                     if ((x > y) == up) { s[i] = y; s[ixj] = x; }
                 }
             }
-            __syncthreads();
+            if (xw) __syncthreads();
+            else wave_lds_sync();
         }
     }
     for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) a.tmp[CK(base + i, a.cap_keys)] = s[i];   // sorted keys live in tmp
@@ -2169,10 +2176,23 @@ DEVI unsigned long long best_key(int32_t f, int32_t i) {
 // first) cut into chunks of SEG_CHUNK anchors, so that several waves share a
 // heavy read (k_chain_lb, k_chain_seg).  In the rescue pass only rescued reads
 // have items.  item_off[t] = first item of order[t]; item_off[n] = total.
+// The first kernel of each chain pass also clears the pass's state (no
+// separate memset launches): the per-read best keys, its long/medium segment
+// queue counters, the k_seg_cands item counter, the LB buffer when asked
+// (zero_fmin), and in pass 0 the k_chain_giant hand-out counters.
 __global__ __launch_bounds__(1024) void k_seg_items(ChainArgs a) {
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    if (tid == 0) {
+        *a.lseg_n = 0; *a.mseg_n = 0; *a.mseg_take = 0;
+        if (a.sq_n) *a.sq_n = 0;
+        if (a.P.pass == 0 && a.work) { a.work[0] = 0; a.work[1] = 0; a.work[2] = 0; a.work[3] = 0; }
+    }
+    for (uint32_t t = (uint32_t)tid; t < a.n; t += 1024) {
+        a.rbest[t] = 0ULL;
+        if (a.zero_fmin) a.fmin[t] = 0;
+    }
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
     __shared__ uint32_t sc[16];
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     uint32_t carry = 0;
     for (uint32_t t0 = 0; t0 < a.n; t0 += 1024) {
         const uint32_t t = t0 + (uint32_t)tid;
@@ -3863,12 +3883,34 @@ __global__ __launch_bounds__(64) void k_dv(DvArgs a) {
     }
     uint32_t st = b;
     while (st > 0 && uni(mpos(st - 1)) == first) --st;
+    uint32_t j = st, en = st;
+    int32_t n_match = 1;
+    if (a.strict) {
+        // Strictly increasing P (odd index k) and chain positions (dq > 0 along a
+        // chain): the greedy walk (paf.rs:179-186) matches C[kk] exactly where P holds it, and
+        // stops matching at the first C[kk] that P lacks.  So each lane finds its C[kk] by a
+        // lower-bound search (64 chain anchors at a time, the same halving steps for every lane),
+        // and the first lane that misses ends the matches.
+        for (int32_t kb = 1; kb < cm; kb += 64) {
+            const int32_t t = kb + lane;
+            const bool tv = t < cm;
+            const int32_t v = tv ? fwdq(t) : INT_MAX;
+            uint32_t b0 = 0, sz = m;
+            while (sz > 1) { const uint32_t half = sz / 2; if (mpos(b0 + half) < v) b0 += half; sz -= half; }
+            const uint32_t ix = b0 + (mpos(b0) < v ? 1u : 0u);
+            const bool hit = tv && ix < m && mpos(ix < m ? ix : 0) == v;
+            const uint64_t miss = ballot(tv && !hit);
+            const int32_t nv = min(64, cm - kb);
+            const int32_t lim = miss ? ctz64(miss) : nv;
+            if (lim > 0) { n_match += lim; en = (uint32_t)rdl((int32_t)ix, lim - 1); }
+            if (miss) break;
+        }
+    } else {
     // greedy match (paf.rs:179-186): the next j with P[j] == C[kk].  A window of
     // 64 positions after j sits in registers; successive targets are matched in
     // it by ballot (each after the previous match) until one is not there, and
     // then the window moves past its end.
-    uint32_t j = st, en = st;
-    int32_t kk = 1, n_match = 1, kb = 1;
+    int32_t kk = 1, kb = 1;
     int32_t cv = (kb + lane < cm) ? fwdq(kb + lane) : 0;
     while (kk < cm && j + 1 < m) {
         const uint32_t c0 = j + 1;
@@ -3885,6 +3927,7 @@ __global__ __launch_bounds__(64) void k_dv(DvArgs a) {
             avail &= L == 63 ? 0ULL : ~((2ULL << L) - 1ULL);
         }
         if (kk < cm) j = (c0 + 63 < m - 1) ? c0 + 63 : m - 1;   // C[kk] is not in this window
+    }
     }
     if (lane == 0) {
         ReadOut* O = a.out + r;
@@ -3950,8 +3993,13 @@ __global__ __launch_bounds__(1024) void k_batch_sums(uint32_t n, const uint32_t*
     }
 }
 
-__global__ void k_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot) {
+// Also clears the batch's per-read outputs and status block (when given): the
+// first kernel of a map, in place of two memset launches.
+__global__ void k_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, ReadOut* zout,
+                          unsigned long long* zst, int zst_words) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (zout && r <= n) { uint4* o = (uint4*)(zout + r); for (int q = 0; q < (int)(sizeof(ReadOut) / 16); ++q) o[q] = make_uint4(0u, 0u, 0u, 0u); }
+    if (zst && r < (uint32_t)zst_words) zst[r] = 0ULL;
     if (r >= n) return;
     if (slot) { base[r] = (uint64_t)slot * r; end[r] = (uint64_t)slot * (r + 1); return; }   // tests: fixed slots
     base[r] = rd_off[r] + 16ull * r;
@@ -4229,9 +4277,11 @@ int launch_view_compact(uint32_t n, const uint64_t* vo, const uint64_t* v_off, c
     LAUNCH_CHECK();
     return 0;
 }
-int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st) {
+int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st,
+                   mm2g::ReadOut* zout, unsigned long long* zst, int zst_words) {
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_mz_base, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, base, end, slot);
+    const uint32_t nt = std::max<uint32_t>(n + 1, zst ? (uint32_t)zst_words : 0u);
+    hipLaunchKernelGGL(k_mz_base, dim3((nt + 255) / 256), dim3(256), 0, st, n, rd_off, base, end, slot, zout, zst, zst_words);
     LAUNCH_CHECK();
     return 0;
 }

@@ -87,14 +87,16 @@ def test_workspace_exact_fallback(small_world, dense_world):
 
 
 @pytest.mark.parametrize("kn", [dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1), dict(seg_sparse=0),
-                                dict(spec_rounds=1), dict(spec_batch=8), dict(sort_small=1, spec_rounds=16, sketch_view=300, seg_chunk=128)])
+                                dict(spec_rounds=1), dict(spec_batch=8), dict(dv_par=0),
+                                dict(sort_small=1, spec_rounds=16, sketch_view=300, seg_chunk=128)])
 def test_round4_paths_vs_oracle(dev, small_world, dense_world, kn):
     """Production paths, on and off, against the oracle (PAF and per-read
     outcome, small and dense worlds at mid_occ 20 and 5000): the rescue pass's
     pruning by pass 0's bound, query sketch views, every read through
     k_sort_read (sort_small=1), k_chain_seg's sparse items off (seg_sparse=0) and
-    over 128-anchor items (their segment-start words cut mid-segment), and
-    k_chain_long's speculative rounds."""
+    over 128-anchor items (their segment-start words cut mid-segment),
+    k_chain_long's speculative rounds and step widths, and k_dv's sequential
+    walk (dv_par=0) beside its parallel match."""
     with knobs(dev, **kn):
         _production_vs_oracle(dev, small_world, dense_world, tag=str(kn))
 
