@@ -342,7 +342,10 @@ enum {
     MM2G_KNOB_SPEC_BATCH = 32,   /* predecessors per step of k_chain_long's speculative rounds: 4 or 8 [4]     */
     MM2G_KNOB_DV_PAR = 33,       /* odd index k: k_dv matches the chain against the minimizer positions by one
                                     parallel search per chain anchor instead of the sequential walk [1]     */
-    MM2G_KNOB_COUNT = 34
+    MM2G_KNOB_SPEC_SWEEPS = 34,  /* k_chain_long: cheap guess sweeps (no marks, no n_skip) before the speculative
+                                    rounds of a block, 0..4 [0]                                              */
+    MM2G_KNOB_SPEC_SWEEP_W = 35, /* ... over this many nearest predecessors, 1..64 [16]                       */
+    MM2G_KNOB_COUNT = 36
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

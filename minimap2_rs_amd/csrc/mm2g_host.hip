@@ -107,6 +107,8 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SEG_SPARSE: return 1;
     case MM2G_KNOB_SPEC_BATCH: return 4;
     case MM2G_KNOB_DV_PAR: return 1;
+    case MM2G_KNOB_SPEC_SWEEPS: return 0;
+    case MM2G_KNOB_SPEC_SWEEP_W: return 16;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -937,6 +939,8 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     ca.seg_chunk = std::max<uint32_t>(64u, (uint32_t)K[MM2G_KNOB_SEG_CHUNK] & ~63u);
     ca.spec_rounds = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(16, K[MM2G_KNOB_SPEC_ROUNDS]));
     ca.spec_batch = K[MM2G_KNOB_SPEC_BATCH] == 8 ? 8u : 4u;
+    ca.spec_sweeps = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(4, K[MM2G_KNOB_SPEC_SWEEPS]));
+    ca.spec_sweep_w = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(64, K[MM2G_KNOB_SPEC_SWEEP_W]));
     // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
     // settle in a few no-break policy-iteration rounds.  Pass 0's long segments
     // are real chains whose windows carry many mark sources: k_chain_long is

@@ -214,6 +214,8 @@ struct ChainArgs {
     void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
     uint32_t spec_rounds = 3; // k_chain_long: speculative rounds per 64-anchor block (MM2G_KNOB_SPEC_ROUNDS)
     uint32_t spec_batch = 4;  // k_chain_long: predecessors per step of a speculative round, 4 or 8 (MM2G_KNOB_SPEC_BATCH)
+    uint32_t spec_sweeps = 0; // k_chain_long: cheap guess sweeps before the rounds (MM2G_KNOB_SPEC_SWEEPS)
+    uint32_t spec_sweep_w = 16; // ... over this many nearest predecessors (MM2G_KNOB_SPEC_SWEEP_W)
     int32_t est_lane = 0;    // k_chain_seg (production): estimated DP pairs up to which a segment takes one lane
     uint32_t full_dp = 0;    // debug mode (exact f/pprev everywhere): pass 0 uses EST_LANE instead of est_lane
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)

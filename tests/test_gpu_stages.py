@@ -87,7 +87,7 @@ def test_workspace_exact_fallback(small_world, dense_world):
 
 
 @pytest.mark.parametrize("kn", [dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1), dict(seg_sparse=0),
-                                dict(spec_rounds=1), dict(spec_batch=8), dict(dv_par=0),
+                                dict(spec_rounds=1), dict(spec_batch=8), dict(dv_par=0), dict(spec_sweeps=2, spec_sweep_w=8),
                                 dict(sort_small=1, spec_rounds=16, sketch_view=300, seg_chunk=128)])
 def test_round4_paths_vs_oracle(dev, small_world, dense_world, kn):
     """Production paths, on and off, against the oracle (PAF and per-read
