@@ -1565,7 +1565,9 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                     s = (rk ? c16(rk - 1) : 0u) - oa;
                     e = c16(rk) - oa;
                 };
-                // A: chunks holding a segment longer than SEG_TINY: one wave sorts 64 keys
+                // A: every chunk holding a segment of two keys or more: one wave sorts its 64
+                // keys by (rank, key), so a segment inside one chunk ends up in place (round 5:
+                // the rank phase then only counts across chunk edges)
                 const uint32_t nch = (nwin + 63) >> 6;
                 for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 2 * NW) {   // two chunks at a time (q, q + NW)
                     const uint32_t ia = q * 64 + (uint32_t)lane, ib = ia + NW * 64;
@@ -1575,8 +1577,8 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                     seg_of(xa, sa, ea);
                     seg_of(xb, sb, eb);
                     xa = va ? xa : U64MAX; xb = vb ? xb : U64MAX;
-                    const bool na = any(va && ea - sa > SEG_TINY && ea - sa <= a.seg_small);
-                    const bool nb = any(vb && eb - sb > SEG_TINY && eb - sb <= a.seg_small);
+                    const bool na = any(va && ea - sa > 1u);
+                    const bool nb = any(vb && eb - sb > 1u);
                     if (na) { wave_bitonic64_np(xa); if (va) S[ia] = xa; }
                     if (nb) { wave_bitonic64_np(xb); if (vb) S[ib] = xb; }
                 }
@@ -1603,20 +1605,18 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                         continue;
                     }
                     const uint32_t xl = (uint32_t)x;
-                    uint32_t rank = 0;
                     if (pq) {
                         if (L <= SEG_TINY) ++pc_tiny;
                         else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
                     }
-                    if (L <= SEG_TINY) {
-                        for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
-                    } else {
-                        const uint32_t co = i >> 6;
-                        rank = i - max(s, co << 6);
-                        for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
-                            if (c == co) continue;
-                            rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
-                        }
+                    // the chunk sorts left every key at its place inside its chunk's part of the
+                    // segment; a segment inside one chunk is therefore in place, and otherwise the
+                    // rank adds the keys below it in the segment's parts in the other chunks
+                    const uint32_t co = i >> 6;
+                    uint32_t rank = i - max(s, co << 6);
+                    for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
+                        if (c == co) continue;
+                        rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
                     }
                     O[oa + s + rank] = x & kmask;
                 }
@@ -2003,14 +2003,15 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                 s0 = lo_m ? q * 32 + 31 - (uint32_t)__builtin_clz(lo_m) : LS[q ? q - 1 : 0];
                 e0 = hi_m ? q * 32 + (uint32_t)__builtin_ctz(hi_m) : NS[q + 1];
             };
-            // A: sort every 64-key chunk holding a bucket of 17..SEG_RANK keys
+            // A: sort every 64-key chunk holding a bucket of 2..SEG_RANK keys (a bucket inside one
+            // chunk is then in place; round 5)
             const uint32_t nch = (nwin + 63) >> 6;
             for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 16) {
                 const uint32_t i = q * 64 + (uint32_t)lane;
                 const bool v = i < nwin;
                 uint32_t s0 = 0, e0 = 0;
                 if (v) seg_of(i, s0, e0);
-                if (any(v && e0 - s0 > SEG_TINY && e0 - s0 <= SEG_RANK)) {
+                if (any(v && e0 - s0 > 1u && e0 - s0 <= SEG_RANK)) {
                     uint64_t x = v ? S[i] : U64MAX;
                     wave_bitonic64_np(x);
                     if (v) S[i] = x;
@@ -2030,16 +2031,11 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                     if (i == s0) { const uint32_t slot = atomicAdd(&s_nbig, 1u); if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s0, oa + e0); }
                     continue;
                 }
-                uint32_t rank = 0;
-                if (L <= SEG_TINY) {
-                    for (uint32_t j = s0; j < e0; ++j) { const uint64_t y = S[j]; rank += (y < x || (y == x && j < i)) ? 1u : 0u; }
-                } else {
-                    const uint32_t co = i >> 6;
-                    rank = i - max(s0, co << 6);
-                    for (uint32_t c = s0 >> 6; c <= (e0 - 1) >> 6; ++c) {
-                        if (c == co) continue;
-                        rank += count_below(S, max(s0, c << 6), min(e0, (c << 6) + 64), x, c < co);
-                    }
+                const uint32_t co = i >> 6;
+                uint32_t rank = i - max(s0, co << 6);
+                for (uint32_t c = s0 >> 6; c <= (e0 - 1) >> 6; ++c) {
+                    if (c == co) continue;
+                    rank += count_below(S, max(s0, c << 6), min(e0, (c << 6) + 64), x, c < co);
                 }
                 O[oa + s0 + rank] = x;
             }
