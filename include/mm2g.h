@@ -345,7 +345,10 @@ enum {
     MM2G_KNOB_SPEC_SWEEPS = 34,  /* k_chain_long: cheap guess sweeps (no marks, no n_skip) before the speculative
                                     rounds of a block, 0..4 [0]                                              */
     MM2G_KNOB_SPEC_SWEEP_W = 35, /* ... over this many nearest predecessors, 1..64 [16]                       */
-    MM2G_KNOB_COUNT = 36
+    MM2G_KNOB_SEED_FUSE = 36,    /* reads the cell sort takes (k_sort_read) get their anchor keys from its first
+                                    pass instead of k_seed_write (no separate write-then-read of the keys) [1] */
+    MM2G_KNOB_SKETCH_X32 = 37,   /* k <= 15: k_sketch keeps the 32-bit hash alone in its LDS window [1]           */
+    MM2G_KNOB_COUNT = 38
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

@@ -109,6 +109,8 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_DV_PAR: return 1;
     case MM2G_KNOB_SPEC_SWEEPS: return 0;
     case MM2G_KNOB_SPEC_SWEEP_W: return 16;
+    case MM2G_KNOB_SEED_FUSE: return 1;
+    case MM2G_KNOB_SKETCH_X32: return 1;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -245,7 +247,7 @@ static void dump_sort_prof(mm2g_ctx* c, uint64_t* d, uint32_t n) {
     fprintf(stderr, "[sort_prof] A0 q10/50/90/99/max=%u/%u/%u/%u/%u  A q10/50/90/99/max=%u/%u/%u/%u/%u  kept cells q10/50/90/99/max=%u/%u/%u/%u/%u\n",
             Q(q0, .1), Q(q0, .5), Q(q0, .9), Q(q0, .99), q0.back(), Q(q2, .1), Q(q2, .5), Q(q2, .9), Q(q2, .99), q2.back(),
             Q(q3, .1), Q(q3, .5), Q(q3, .9), Q(q3, .99), q3.back());
-    fprintf(stderr, "[sort_prof] reads=%u (whole-read radix %.0f, bucket path %.0f) A0=%.0f A=%.0f nbig=%.2f windows=%.2f us/read: p1+kc=%.1f p2=%.1f gather=%.1f segs=%.1f chunk=%.1f rank=%.1f p4b/radix=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
+    fprintf(stderr, "[sort_prof] reads=%u (whole-read radix %.0f, bucket path %.0f) A0=%.0f A=%.0f nbig=%.2f windows=%.2f us/read: p1+kc=%.1f p2=%.1f gather=%.1f fuse_stage=%.1f chunk=%.1f rank=%.1f p4b/radix=%.1f total=%.1f span_us=%.1f concurrency=%.1f\n",
             m, nleg, nbigp, a0 / m, a2 / m, np / m, ph[7] / m, ph[0] / m / 100, ph[1] / m / 100, ph[2] / m / 100, ph[3] / m / 100, ph[4] / m / 100,
             ph[5] / m / 100, ph[6] / m / 100, tot / m / 100, (double)(t_hi - t_lo) / 100, tot / (double)(t_hi - t_lo));
     fprintf(stderr, "[sort_prof] keys per read in segments <= %u: %.0f, 17..64: %.0f, > 64: %.0f (%.2f other-chunk searches each)\n",
@@ -766,6 +768,7 @@ static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf, Re
         if (zst) HIPCHK(hipMemsetAsync(zst, 0, STAT_WORDS * 8, c->stream));
     }
     SketchArgs a{nullptr, c->d_rd_off, n, w, k, base, end, x, y, cnt, ovf};
+    a.x64 = c->knob[MM2G_KNOB_SKETCH_X32] ? 0u : 1u;
     a.pk_words = c->d_words; a.pk_off = c->d_pk_off; a.amb_off = c->d_amb_off; a.mz_need = need;
     // query views (odd k only: the fixed warm-up is exact there; a re-run
     // after a slot overflow has them off, so the exact per-read layout needs one pass)
@@ -1239,18 +1242,30 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     ENSURE(c->order, uint32_t, n, rorder);
     LCHK(launch_read_order(n, a_cnt, rorder, c->stream));
     sa.order = rorder;
+    // 4. anchor sort (seeds.rs:58).  The singleton filter needs every max_dist_x
+    //    of both DP passes within one 2^CELL_SHIFT cell (DESIGN.md "Anchor sort");
+    //    it is off in debug mode (full anchor/DP arrays for the parity tests).
+    const bool filt = !full && !stop_after_sort && K[MM2G_KNOB_FILTER] && std::max(mdx0, mdx1) <= (1 << CELL_SHIFT);
+    const uint32_t sort_small_max = (uint32_t)std::min<int64_t>(K[MM2G_KNOB_SORT_SMALL], 4096);
+    // fused seeding: k_sort_read's first pass makes the keys of the reads it sorts when their
+    // minimizers (16 B each) fit in its LDS above the two cell bitmaps
+    uint32_t fuse_mmax = 0;
+    if (filt && K[MM2G_KNOB_SEED_FUSE]) {
+        SortArgs t{};
+        t.cells = c->dix->cells;
+        t.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
+        const uint32_t LW = sort_read_lds_words(t), nw = (t.cells + 31) / 32;
+        if (LW > 2 * nw + 64 + 2048) fuse_mmax = std::min<uint32_t>((LW - 2 * nw - 64 - 2048) / 4, 0xffffu);   // 4 words per minimizer + 4096 u16 owner starts
+    }
+    sa.fuse_mmax = fuse_mmax; sa.small_max = sort_small_max;
     {
         ProfScope ps(c, "seed_write");
         LCHK(launch_seed_write(sa, grid_for(n), c->stream));
     }
-    // 4. anchor sort (seeds.rs:58).  The singleton filter needs every max_dist_x
-    //    of both DP passes within one 2^CELL_SHIFT cell (DESIGN.md "Anchor sort");
-    //    it is off in debug mode (full anchor/DP arrays for the parity tests).
     uint32_t* cnt2; uint64_t* smax; uint32_t* rlist;
     ENSURE(c->cnt2, uint32_t, n, cnt2);
     ENSURE(c->rlist, uint32_t, n + 2, rlist);
     ENSURE(c->smax, uint64_t, n, smax);
-    const bool filt = !full && !stop_after_sort && K[MM2G_KNOB_FILTER] && std::max(mdx0, mdx1) <= (1 << CELL_SHIFT);
     const int64_t stop_at = K[MM2G_KNOB_STOP_AT];   // measurement only: later stages skipped, results invalid
     // pass-0 chain parameters (main.rs:201-214): the sort's LB pass uses them too
     ChainKParams P{};
@@ -1261,13 +1276,17 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     const int npass = stop_at == 3 ? 1 : 2;
     const bool chain = !stop_after_sort && stop_at != 1 && stop_at != 2;
     SortArgs so{n, a_off, keys, ktmp, kl.qb, kl.rb, kl.n_seq, c->keys.cap / 8, (const uint32_t*)c->dix->goff.p,
-                filt ? c->dix->cells : 0u, cnt2, smax, (uint32_t)std::min<int64_t>(K[MM2G_KNOB_SORT_SMALL], 4096), nullptr, 0u,
+                filt ? c->dix->cells : 0u, cnt2, smax, sort_small_max, nullptr, 0u,
                 (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_SEG_SMALL], SEG_THREAD)), nullptr};
     so.abort = st32;
     so.meta = (uint32_t*)fb;
     so.rlist = rlist; so.rcount = rlist + n; so.rwork = rlist + n + 1;
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
+    so.fuse_mmax = fuse_mmax;
+    so.rd_off = c->d_rd_off; so.mz_base = mz_base; so.mz_cnt = mz_cnt; so.mz_y = (const uint32_t*)c->sk1.y.p;
+    so.mz_n = mz_n; so.mz_poff = mz_poff; so.ix_pos = (const uint64_t*)c->dix->ix_pos.p; so.kl = kl; so.span = o->k;
+    so.cap_pos = c->dix->ix_pos.cap / 8;
     uint64_t* sprof = nullptr;
     if (K[MM2G_KNOB_SORT_PROF]) { HIPCHK(hipMalloc(&sprof, (size_t)n * 192)); HIPCHK(hipMemsetAsync(sprof, 0, (size_t)n * 192, c->stream)); so.prof = sprof; }
     if (stop_at != 1) {

@@ -118,6 +118,7 @@ struct SketchArgs {
     // view r is [view_off[r], + view_len[r]) of read view_read[r] (view_off a
     // multiple of 8), with the same view_pre / emit_from / view_last meaning.
     const uint32_t* view_read = nullptr;
+    uint32_t x64 = 0;              // k <= 15: keep the 64-bit LDS window (MM2G_KNOB_SKETCH_X32 = 0) instead of the hash-only one
 };
 struct FilterArgs {
     uint32_t n;
@@ -144,6 +145,9 @@ struct SeedArgs {
     uint32_t* a_part;                     // per read, SEED_PARTS-1 entries: anchors before part k (k = 1..)
     const uint32_t* abort = nullptr;      // batch status word (BS_*): kernels after the anchor scan exit on BS_ANCHORS
     const uint32_t* order = nullptr;      // k_seed_write: reads heaviest first (null = batch order)
+    // fused seeding: reads with small_max < A <= 65535 anchors and at most fuse_mmax minimizers
+    // get their keys from k_sort_read's first pass instead (0 = off; SortArgs::fuse_mmax)
+    uint32_t fuse_mmax = 0, small_max = 0;
 };
 // seed_write splits each read's minimizers into this many contiguous parts
 // (whole 64-minimizer chunks), one wave each; seed_count records where they start
@@ -173,6 +177,11 @@ struct SortArgs {
     uint32_t* rcount = nullptr;
     const uint32_t* order = nullptr;   // k_sort_read: block b sorts read order[b] (heaviest first); null = b
     uint32_t* rwork = nullptr;         // k_sort_big: next list entry to take (zeroed by k_sort_small)
+    // fused seeding (k_sort_read P1 writes the keys of the reads k_seed_write skipped; SeedArgs)
+    uint32_t fuse_mmax = 0;
+    const uint64_t* rd_off = nullptr; const uint64_t* mz_base = nullptr; const uint32_t* mz_cnt = nullptr;
+    const uint32_t* mz_y = nullptr; const uint32_t* mz_n = nullptr; const uint32_t* mz_poff = nullptr;
+    const uint64_t* ix_pos = nullptr; KeyLayout kl{}; int span = 0; uint64_t cap_pos = 0;
 };
 struct ChainArgs {
     uint32_t n;
@@ -253,7 +262,9 @@ int launch_filter(const mm2g::FilterArgs& a, int k, int n_blocks, hipStream_t st
 int launch_seed_count(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 int launch_seed_write(const mm2g::SeedArgs& a, int n_blocks, hipStream_t st);
 // per-read MSD bucket sort on (group, rpos) + per-bucket full-key sort (qb = query bits of the key)
-int launch_sort_read(int stage, const mm2g::SortArgs& a, hipStream_t st);   // 0 small reads, 1 large
+int launch_sort_read(int stage, const mm2g::SortArgs& a, hipStream_t st);
+// dynamic LDS words k_sort_read runs with (launch_sort_read; the host sizes fuse_mmax from it)
+uint32_t sort_read_lds_words(const mm2g::SortArgs& a);   // 0 small reads, 1 large
 // MM2G_CHECKED builds: first recorded bounds violation {line, index, cap}; 0 = none
 int mm2g_checked_read(unsigned long long out[4], hipStream_t st);
 // chain DP of one pass, stage 0..4: k_chain_seg, k_chain_med, k_lseg_order, k_chain_long, k_chain_fin

@@ -237,15 +237,21 @@ struct SeqNt4 {
     }
 };
 
-template <bool K32, typename Src, bool HPC = false>
+// X32 (k <= 15, not HPC): the LDS window holds the 32-bit hash alone (hash < 4^k < 2^30, so
+// ~0u stays free for "no info"); every x = hash << 8 | k then, so x and hash order alike
+template <bool K32, typename Src, bool HPC = false, bool X32 = false>
 #ifndef SK_WPE
 #define SK_WPE(Src) (std::is_same<Src, SeqNt4>::value ? 5 : 4)   // waves per SIMD: the query sketch (nt4) at 96 VGPRs, 5 waves per SIMD; the index build (ASCII) at 128
 #endif
-__global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
+__global__ __launch_bounds__(256, X32 ? 6 : SK_WPE(Src)) void k_sketch(SketchArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
+    static_assert(!X32 || (K32 && !HPC), "X32: k <= 15 query/index sketch without HPC spans");
+    using XT = typename std::conditional<X32, uint32_t, uint64_t>::type;
+    constexpr XT XMAX = (XT)~(XT)0;
     const int w = a.w, k = a.k;
+    auto xout = [&](XT v) -> uint64_t { return X32 ? (v == XMAX ? U64MAX : ((uint64_t)v << 8) | (uint64_t)k) : (uint64_t)v; };
     const int wv = wave_id(), lane = lane_id();
-    uint64_t* X = (uint64_t*)(smem + sketch_wave_lds(w) * wv);
+    XT* X = (XT*)(smem + sketch_wave_lds(w) * wv);
     uint16_t* LZ = (uint16_t*)(X + sketch_wave_slots(w));
     const int CAP = w + k;
     const uint64_t mask = (k >= 32) ? U64MAX : ((1ULL << (2 * k)) - 1);
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
         // history slots = positions [-w, -1]: MAX
         for (int t0 = 0; t0 < w; t0 += 64) {
             const int t = t0 + lane;
-            if (t < w) { X[SKP(t)] = U64MAX; LZ[SKP(t)] = 0; }
+            if (t < w) { X[SKP(t)] = XMAX; LZ[SKP(t)] = 0; }
         }
         uint64_t count = 0;
         uint32_t n_tiles = 0, n_slow = 0;      // MM2G_SKETCH_PROF: tiles, tiles on the exact (2-pass) step path
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                 if (p < pe) {
                     const int ix = (int)(p - hbase);
                     const uint32_t c = (code16 >> (2 * (7 - t))) & 3u;
-                    uint64_t x = U64MAX; uint16_t fl = 0, z = 0;
+                    XT x = XMAX; uint16_t fl = 0, z = 0;
                     if ((valid8 >> t) & 1u) {
                         kf2 = ((kf2 << 2) | (KT)c) & kmask; kr2 = (kr2 >> 2) | ((KT)(3 ^ c) << shift1);
                         fl = 1;
@@ -380,6 +386,8 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                             if constexpr (HPC) {               // TinyQueue span (sketch.rs:51-64, 72)
                                 const uint32_t sp = a.hpc_span[roff + (uint64_t)p];
                                 x = sp < 256u ? (h << 8) | (uint64_t)sp : U64MAX;
+                            } else if constexpr (X32) {
+                                x = (XT)h;                     // X32: the hash alone (span == k)
                             } else {
                                 x = (h << 8) | (uint64_t)k;    // kmer_span == k whenever info is valid
                             }
@@ -415,7 +423,7 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                     const uint16_t fl = v & 3u;
                     if (fl == 0) lv = 0; else if (fl == 2) lv = lv + 1 < CAP ? lv + 1 : CAP;
                     LZ[SKP(ix)] = (uint16_t)((v & 0x8000u) | (uint16_t)lv);
-                    if (!(fl == 2 && lv >= k)) X[SKP(ix)] = U64MAX;
+                    if (!(fl == 2 && lv >= k)) X[SKP(ix)] = XMAX;
                 }
             }
             {
@@ -431,7 +439,7 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
             // ---- phase 2: reference step logic, count then write
             uint32_t myoff = 0, tot = 0;
             bool fast_done = false;
-#define SK_EMIT(xv, yv) do { if (em_ok) { if (WR && o < oend) { a.mz_x[o] = (xv); a.mz_y[o] = (yv); } ++o; ++n_em; } } while (0)
+#define SK_EMIT(xv, yv) do { if (em_ok) { if (WR && o < oend) { a.mz_x[o] = xout(xv); a.mz_y[o] = (yv); } ++o; ++n_em; } } while (0)
             if (w > SK_CH) {
                 // The reference's `min` after step i is the newest minimum of slots
                 // [i-w+1, i] (DESIGN.md "Sketch").  Window = [i-w+1, ps-1] u [ps, i]:
@@ -440,18 +448,18 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                 // while stepping; both carry the multiplicity of the minimum, so
                 // tie scans run only where the minimum really occurs twice.
                 // s*: (x, LDS slot | multiple<<16) of the newest minimum of [j, ps-1]
-                uint64_t sx[SK_CH + 1]; uint32_t sp[SK_CH + 1];
+                XT sx[SK_CH + 1]; uint32_t sp[SK_CH + 1];
                 {
-                    uint64_t cx = U64MAX; uint32_t cp = 0xffffffffu;
+                    XT cx = XMAX; uint32_t cp = 0xffffffffu;
                     const int q0 = (int)(ps - hbase);
                     for (int d = 1; d < w - SK_CH; ++d) {          // slot q0 - d (newest first)
-                        const uint64_t x = X[SKP(q0 - d)];
+                        const XT x = X[SKP(q0 - d)];
                         if (cp == 0xffffffffu || x < cx) { cx = x; cp = (uint32_t)(q0 - d); } else if (x == cx) cp |= 0x10000u;
                     }
 #pragma unroll
                     for (int t = 0; t <= SK_CH; ++t) {
                         const int d = w - SK_CH + t;                 // j = ps - w + (SK_CH - t)
-                        const uint64_t x = X[SKP(q0 - d)];
+                        const XT x = X[SKP(q0 - d)];
                         if (cp == 0xffffffffu || x < cx) { cx = x; cp = (uint32_t)(q0 - d); } else if (x == cx) cp |= 0x10000u;
                         sx[SK_CH - t] = cx; sp[SK_CH - t] = cp;
                     }
@@ -462,30 +470,30 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                 bool need = false;
                 uint32_t em = 0, eq[SK_CH / 2] = {};
                 {
-                    uint64_t px = U64MAX; uint32_t pp = 0xffffffffu;   // prefix minimum of [ps, i]
-                    uint64_t mxo = sx[0]; int mqo = (int)(sp[0] & 0xffffu);
+                    XT px = XMAX; uint32_t pp = 0xffffffffu;   // prefix minimum of [ps, i]
+                    XT mxo = sx[0]; int mqo = (int)(sp[0] & 0xffffu);
 #pragma unroll
                     for (int t = 0; t < SK_CH; ++t) {
                         const int64_t i = ps + t;
                         const bool act = i < pe;
                         const int ii = (int)(i - hbase);
-                        const uint64_t xi = act ? X[SKP(ii)] : U64MAX;
+                        const XT xi = act ? X[SKP(ii)] : XMAX;
                         const int32_t l = act ? (int32_t)(LZ[SKP(ii)] & 0x7fffu) : 0;
-                        need |= act && l == w + k - 1 && mxo != U64MAX;                 // A (sketch.rs:90-93)
+                        need |= act && l == w + k - 1 && mxo != XMAX;                 // A (sketch.rs:90-93)
                         const bool doB = act && xi <= mxo;                              // B (94-96)
                         const bool doC = act && !doB && mqo == ii - w;                  // C (97-105)
-                        if (((doB && l >= w + k && mxo != U64MAX) || (doC && l >= w + k - 1)) && i >= efrom) {
+                        if (((doB && l >= w + k && mxo != XMAX) || (doC && l >= w + k - 1)) && i >= efrom) {
                             em |= 1u << t; eq[t >> 1] |= (uint32_t)mqo << (16 * (t & 1));
                         }
                         if (act) {
                             if (pp == 0xffffffffu || xi < px) { px = xi; pp = (uint32_t)ii; }
                             else if (xi == px) pp = (uint32_t)ii | 0x10000u;
                         }
-                        uint64_t mxn; uint32_t mpn;
+                        XT mxn; uint32_t mpn;
                         if (px < sx[t + 1]) { mxn = px; mpn = pp; }
                         else if (px > sx[t + 1]) { mxn = sx[t + 1]; mpn = sp[t + 1]; }
                         else { mxn = px; mpn = pp | 0x10000u; }
-                        need |= doC && l >= w + k - 1 && mxn != U64MAX && (mpn & 0x10000u);   // T
+                        need |= doC && l >= w + k - 1 && mxn != XMAX && (mpn & 0x10000u);   // T
                         mxo = mxn; mqo = (int)(mpn & 0xffffu);
                     }
                 }
@@ -496,7 +504,7 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                     for (int t = 0; t < SK_CH; ++t) {
                         if ((em >> t) & 1u) {
                             const int q = (int)((eq[t >> 1] >> (16 * (t & 1))) & 0xffffu);
-                            if (o < oend) { a.mz_x[o] = X[SKP(q)]; a.mz_y[o] = SK_Y(q); }
+                            if (o < oend) { a.mz_x[o] = xout(X[SKP(q)]); a.mz_y[o] = SK_Y(q); }
                             ++o;
                         }
                     }
@@ -512,11 +520,11 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                 uint64_t o = obase + count + myoff;
                 uint32_t n_em = 0;
                 // newest minimum of the w slots before the chunk (same for every ln count)
-                uint64_t mx = U64MAX; uint32_t my = 0xffffffffu; int64_t mp = ps - w - 1;
+                XT mx = XMAX; uint32_t my = 0xffffffffu; int64_t mp = ps - w - 1;
                 for (int d = 0; d < w; ++d) {
                     const int64_t p = ps - w + d;
                     const int q = (int)(p - hbase);
-                    const uint64_t x = X[SKP(q)];
+                    const XT x = X[SKP(q)];
                     if (mx >= x) { mx = x; my = SK_Y(q); mp = p; }
                 }
                 for (int t = 0; t < SK_CH; ++t) {
@@ -524,10 +532,10 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                     const bool act = i < pe;
                     const bool em_ok = i >= efrom;   // warm-up steps of an index view emit nothing
                     const int ii = (int)(i - hbase);
-                    const uint64_t ix_x = act ? X[SKP(ii)] : U64MAX;
+                    const XT ix_x = act ? X[SKP(ii)] : XMAX;
                     const uint32_t ix_y = act ? SK_Y(ii) : 0xffffffffu;
                     const int32_t l = act ? (int32_t)(LZ[SKP(ii)] & 0x7fffu) : 0;
-                    const bool doA = act && l == w + k - 1 && mx != U64MAX;
+                    const bool doA = act && l == w + k - 1 && mx != XMAX;
                     if (any(doA)) {
                         for (int d = 1; d < w; ++d) {
                             const int q = ii - w + d;
@@ -536,17 +544,17 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
                     }
                     const bool doB = act && ix_x <= mx;
                     const bool doC = act && !doB && mp == i - w;
-                    if ((doB && l >= w + k && mx != U64MAX) || (doC && l >= w + k - 1)) SK_EMIT(mx, my);
+                    if ((doB && l >= w + k && mx != XMAX) || (doC && l >= w + k - 1)) SK_EMIT(mx, my);
                     if (doB) { mx = ix_x; my = ix_y; mp = i; }
                     if (any(doC)) {
-                        uint64_t nx = U64MAX; uint32_t ny = 0; int64_t np = mp;
+                        XT nx = XMAX; uint32_t ny = 0; int64_t np = mp;
                         for (int d = 1; d <= w; ++d) {
                             const int q = ii - w + d;
-                            const uint64_t x = X[SKP(q)];
+                            const XT x = X[SKP(q)];
                             if (nx >= x) { nx = x; ny = SK_Y(q); np = i - w + d; }
                         }
                         if (doC) { mx = nx; my = ny; mp = np; }
-                        const bool doT = doC && l >= w + k - 1 && mx != U64MAX;
+                        const bool doT = doC && l >= w + k - 1 && mx != XMAX;
                         if (any(doT)) {
                             for (int d = 1; d <= w; ++d) {
                                 const int q = ii - w + d;
@@ -579,15 +587,15 @@ __global__ __launch_bounds__(256, SK_WPE(Src)) void k_sketch(SketchArgs a) {
         {
             const int64_t tl = ((L - 1) / SK_TS) * SK_TS;   // last tile start
             const int64_t hbase = tl - w;
-            uint64_t mx = U64MAX; uint32_t my = 0;
+            XT mx = XMAX; uint32_t my = 0;
             for (int d = 0; d < w; ++d) {
                 const int q = (int)(L - w + d - hbase);
-                const uint64_t x = X[SKP(q)];
+                const XT x = X[SKP(q)];
                 if (mx >= x) { mx = x; my = SK_Y(q); }
             }
-            if (mx != U64MAX && flush) {
+            if (mx != XMAX && flush) {
                 const uint64_t o = obase + count;
-                if (lane == 0 && o < oend) { a.mz_x[o] = mx; a.mz_y[o] = my; }
+                if (lane == 0 && o < oend) { a.mz_x[o] = xout(mx); a.mz_y[o] = my; }
                 ++count;
             }
             if (lane == 0) {
@@ -883,8 +891,12 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
         const uint32_t nch = (m + 63) >> 6;
         const uint32_t cb = (nch * part) / SEED_PARTS, ce = (nch * (part + 1)) / SEED_PARTS;
         if (cb >= ce) continue;
-        const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
         const uint64_t obase = uni64(a.a_off[r]);
+        if (a.fuse_mmax && m <= a.fuse_mmax) {   // k_sort_read writes this read's keys (its first pass)
+            const uint64_t A0 = uni64(a.a_off[r + 1]) - obase;
+            if (A0 > a.small_max && A0 <= 65535u) continue;
+        }
+        const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
         uint64_t* out = a.keys;
         uint64_t run = part ? (uint64_t)(uint32_t)uni((int32_t)a.a_part[(uint64_t)r * (SEED_PARTS - 1) + part - 1]) : 0;
         const uint32_t cend = ce * 64 < m ? ce * 64 : m;
@@ -1027,6 +1039,9 @@ constexpr int SORT_LDS_HALF = 76 * 1024; // ... two 512-thread workgroups per CU
 #endif
 #ifndef SORT_UG
 #define SORT_UG SORT_U                    // ... in the window gathers
+#endif
+#ifndef SORT_FUSE_U
+#define SORT_FUSE_U 16                    // ... in the fused seeding pass (index gathers: more in flight)
 #endif
 
 // 8 independent loads per thread, then fn(i, x) for each (i < n): hides HBM
@@ -1408,6 +1423,106 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
     {
         // ---- P1: seen / seen-twice bitmaps
         for (uint32_t i = tid; i < 2 * nw; i += NT) dyn[i] = 0;
+        const uint32_t fm = a.fuse_mmax ? a.mz_cnt[r] : 0u;
+        if (a.fuse_mmax && fm <= a.fuse_mmax) {
+            // fused seeding: k_seed_write skipped this read, so P1 makes its keys (push_anchor,
+            // seeds.rs:62-79) in k_seed_write's order (minimizer order, then index position
+            // order) from the read's minimizers staged above the bitmaps, writes them to K for
+            // P2 and the windows, and sets the bitmaps on the way (no HBM read of K here)
+            uint32_t* Mi = dyn + 2 * nw;           // inclusive anchor offsets (searched)
+            uint32_t* Mp = Mi + fm;                // index position offsets
+            uint32_t* My = Mp + fm;                // query y
+            uint32_t* Mh = My + fm;                // raw n (IX_INLINE | position high word for a Single)
+            const uint64_t mb = a.mz_base[r];
+            uint32_t carry = 0;
+            constexpr int FS = 2;   // minimizers per thread per step (a 10 kb read's ~1.8 k in one step)
+            for (uint32_t i0 = 0; i0 < fm; i0 += NT * FS) {
+                uint32_t nraw[FS], po[FS], yy[FS], cs = 0;
+#pragma unroll
+                for (int j = 0; j < FS; ++j) {
+                    const uint32_t i = i0 + (uint32_t)tid * FS + (uint32_t)j;
+                    const bool v = i < fm;
+                    nraw[j] = v ? a.mz_n[mb + i] : 0u;
+                    po[j] = v ? a.mz_poff[mb + i] : 0u; yy[j] = v ? a.mz_y[mb + i] : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < FS; ++j) cs += ix_count(nraw[j]);
+                uint32_t tot;
+                uint32_t run = carry + block_excl_sum<NW>(cs, tot, s_sc);
+#pragma unroll
+                for (int j = 0; j < FS; ++j) {
+                    const uint32_t i = i0 + (uint32_t)tid * FS + (uint32_t)j;
+                    run += ix_count(nraw[j]);
+                    if (i < fm) { Mi[i] = run; Mp[i] = po[j]; My[i] = yy[j]; Mh[i] = nraw[j]; }
+                }
+                carry += tot;
+            }
+            __syncthreads();
+            // owner of key 16 b (where each key's search starts; its owner lies between that and
+            // the owner of key 16 (b + 1), usually the same or the next non-empty minimizer)
+            uint16_t* O16 = (uint16_t*)(Mh + fm);
+            const uint32_t nb16 = (A0 + 15) >> 4;
+            for (uint32_t i = tid; i < fm; i += NT) {
+                const uint32_t lo = i ? Mi[i - 1] : 0u, hi = Mi[i];
+                for (uint32_t b = (lo + 15) >> 4; (b << 4) < hi; ++b) O16[b] = (uint16_t)i;
+            }
+            __syncthreads();
+            SORT_PH(3);   // MM2G_KNOB_SORT_PROF "fuse_stage": the minimizer staging (the rest of P1 counts as p1)
+            const int32_t qlen = (int32_t)(a.rd_off[r + 1] - a.rd_off[r]);
+            constexpr int FU = SORT_FUSE_U;
+            for (uint32_t i0 = 0; i0 < A0; i0 += NT * FU) {
+                uint32_t lo[FU], hi[FU];
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const uint32_t t = i0 + (uint32_t)u * NT + tid, b = t < A0 ? t >> 4 : 0u;
+                    lo[u] = O16[b];
+                    hi[u] = t >= A0 ? lo[u] : (b + 1 < nb16 ? (uint32_t)O16[b + 1] : fm - 1);
+                }
+                // first minimizer from lo with inclusive offset > t (all lanes' searches step together)
+                while (true) {
+                    bool act = false;
+#pragma unroll
+                    for (int u = 0; u < FU; ++u) {
+                        if (lo[u] < hi[u]) {
+                            const uint32_t t = i0 + (uint32_t)u * NT + tid, mid = (lo[u] + hi[u]) >> 1;
+                            if (Mi[mid] > t) hi[u] = mid; else lo[u] = mid + 1;
+                            act |= lo[u] < hi[u];
+                        }
+                    }
+                    if (!any(act)) break;
+                }
+                uint64_t x[FU];
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const uint32_t t = i0 + (uint32_t)u * NT + tid;
+                    x[u] = 0;
+                    if (t < A0) {
+                        const uint32_t ow = lo[u];
+                        const uint32_t h = Mh[ow], exo = ow ? Mi[ow - 1] : 0u;
+                        x[u] = (h & IX_INLINE) ? ((uint64_t)(h & ~IX_INLINE) << 32) | Mp[ow]   // Single: no gather
+                                               : a.ix_pos[CK((uint64_t)Mp[ow] + (t - exo), a.cap_pos)];
+                    }
+                }
+                uint32_t c[FU];
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const uint32_t t = i0 + (uint32_t)u * NT + tid;
+                    x[u] = pack_anchor(x[u], My[lo[u]], qlen, a.span, a.kl);
+                    if (t < A0) K[t] = x[u];
+                    c[u] = cell_of(x[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const uint32_t t = i0 + (uint32_t)u * NT + tid;
+                    lo[u] = t < A0 ? atomicOr(&B1[c[u] >> 5], 1u << (c[u] & 31)) : 0u;   // (lo: the old words)
+                }
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const uint32_t t = i0 + (uint32_t)u * NT + tid, bit = 1u << (c[u] & 31);
+                    if (t < A0 && (lo[u] & bit)) atomicOr(&B2[c[u] >> 5], bit);
+                }
+            }
+        } else {
         __syncthreads();
         // staged per group of SORT_U1 keys: all cells, then all first atomics
         // (LDS round trips overlap instead of one chain per key)
@@ -1428,6 +1543,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                 const uint32_t i = i0 + (uint32_t)u * NT + tid, bit = 1u << (c[u] & 31);
                 if (i < A0 && (old[u] & bit)) atomicOr(&B2[c[u] >> 5], bit);   // seen before: seen twice
             }
+        }
         }
         __syncthreads();
         // ---- KC (in place of B2) and the word prefix of its popcounts (in place of B1)
@@ -1565,9 +1681,7 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                     s = (rk ? c16(rk - 1) : 0u) - oa;
                     e = c16(rk) - oa;
                 };
-                // A: every chunk holding a segment of two keys or more: one wave sorts its 64
-                // keys by (rank, key), so a segment inside one chunk ends up in place (round 5:
-                // the rank phase then only counts across chunk edges)
+                // A: chunks holding a segment longer than SEG_TINY: one wave sorts 64 keys
                 const uint32_t nch = (nwin + 63) >> 6;
                 for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 2 * NW) {   // two chunks at a time (q, q + NW)
                     const uint32_t ia = q * 64 + (uint32_t)lane, ib = ia + NW * 64;
@@ -1577,8 +1691,8 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                     seg_of(xa, sa, ea);
                     seg_of(xb, sb, eb);
                     xa = va ? xa : U64MAX; xb = vb ? xb : U64MAX;
-                    const bool na = any(va && ea - sa > 1u);
-                    const bool nb = any(vb && eb - sb > 1u);
+                    const bool na = any(va && ea - sa > SEG_TINY && ea - sa <= a.seg_small);
+                    const bool nb = any(vb && eb - sb > SEG_TINY && eb - sb <= a.seg_small);
                     if (na) { wave_bitonic64_np(xa); if (va) S[ia] = xa; }
                     if (nb) { wave_bitonic64_np(xb); if (vb) S[ib] = xb; }
                 }
@@ -1605,18 +1719,20 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                         continue;
                     }
                     const uint32_t xl = (uint32_t)x;
+                    uint32_t rank = 0;
                     if (pq) {
                         if (L <= SEG_TINY) ++pc_tiny;
                         else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
                     }
-                    // the chunk sorts left every key at its place inside its chunk's part of the
-                    // segment; a segment inside one chunk is therefore in place, and otherwise the
-                    // rank adds the keys below it in the segment's parts in the other chunks
-                    const uint32_t co = i >> 6;
-                    uint32_t rank = i - max(s, co << 6);
-                    for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
-                        if (c == co) continue;
-                        rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
+                    if (L <= SEG_TINY) {
+                        for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
+                    } else {
+                        const uint32_t co = i >> 6;
+                        rank = i - max(s, co << 6);
+                        for (uint32_t c = s >> 6; c <= (e - 1) >> 6; ++c) {
+                            if (c == co) continue;
+                            rank += count_below_lo(S32, max(s, c << 6), min(e, (c << 6) + 64), xl, c < co);
+                        }
                     }
                     O[oa + s + rank] = x & kmask;
                 }
@@ -2003,15 +2119,14 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                 s0 = lo_m ? q * 32 + 31 - (uint32_t)__builtin_clz(lo_m) : LS[q ? q - 1 : 0];
                 e0 = hi_m ? q * 32 + (uint32_t)__builtin_ctz(hi_m) : NS[q + 1];
             };
-            // A: sort every 64-key chunk holding a bucket of 2..SEG_RANK keys (a bucket inside one
-            // chunk is then in place; round 5)
+            // A: sort every 64-key chunk holding a bucket of 17..SEG_RANK keys
             const uint32_t nch = (nwin + 63) >> 6;
             for (uint32_t q = (uint32_t)wave_id(); q < nch; q += 16) {
                 const uint32_t i = q * 64 + (uint32_t)lane;
                 const bool v = i < nwin;
                 uint32_t s0 = 0, e0 = 0;
                 if (v) seg_of(i, s0, e0);
-                if (any(v && e0 - s0 > 1u && e0 - s0 <= SEG_RANK)) {
+                if (any(v && e0 - s0 > SEG_TINY && e0 - s0 <= SEG_RANK)) {
                     uint64_t x = v ? S[i] : U64MAX;
                     wave_bitonic64_np(x);
                     if (v) S[i] = x;
@@ -2031,11 +2146,16 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                     if (i == s0) { const uint32_t slot = atomicAdd(&s_nbig, 1u); if (slot < (uint32_t)BIG_MAX) s_big[slot] = make_uint2(oa + s0, oa + e0); }
                     continue;
                 }
-                const uint32_t co = i >> 6;
-                uint32_t rank = i - max(s0, co << 6);
-                for (uint32_t c = s0 >> 6; c <= (e0 - 1) >> 6; ++c) {
-                    if (c == co) continue;
-                    rank += count_below(S, max(s0, c << 6), min(e0, (c << 6) + 64), x, c < co);
+                uint32_t rank = 0;
+                if (L <= SEG_TINY) {
+                    for (uint32_t j = s0; j < e0; ++j) { const uint64_t y = S[j]; rank += (y < x || (y == x && j < i)) ? 1u : 0u; }
+                } else {
+                    const uint32_t co = i >> 6;
+                    rank = i - max(s0, co << 6);
+                    for (uint32_t c = s0 >> 6; c <= (e0 - 1) >> 6; ++c) {
+                        if (c == co) continue;
+                        rank += count_below(S, max(s0, c << 6), min(e0, (c << 6) + 64), x, c < co);
+                    }
                 }
                 O[oa + s0 + rank] = x;
             }
@@ -4143,14 +4263,17 @@ __global__ __launch_bounds__(256) void k_mid_hist(const IxEntry* tab, uint64_t c
 
 int launch_sketch(const SketchArgs& a, int n_blocks, hipStream_t st) {
     const size_t lds = sketch_wave_lds(a.w) * 4;
+    const bool x32 = a.k <= 15 && !a.x64;   // 32-bit LDS window (k_sketch X32)
     if (a.pk_words) {
-        if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqNt4>), dim3(n_blocks), dim3(256), lds, st, a);
+        if (x32) hipLaunchKernelGGL((k_sketch<true, SeqNt4, false, true>), dim3(n_blocks), dim3(256), lds, st, a);
+        else if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqNt4>), dim3(n_blocks), dim3(256), lds, st, a);
         else hipLaunchKernelGGL((k_sketch<false, SeqNt4>), dim3(n_blocks), dim3(256), lds, st, a);
     } else {
         if (a.hpc_span) {
             if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqAscii, true>), dim3(n_blocks), dim3(256), lds, st, a);
             else hipLaunchKernelGGL((k_sketch<false, SeqAscii, true>), dim3(n_blocks), dim3(256), lds, st, a);
-        } else if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqAscii>), dim3(n_blocks), dim3(256), lds, st, a);
+        } else if (x32) hipLaunchKernelGGL((k_sketch<true, SeqAscii, false, true>), dim3(n_blocks), dim3(256), lds, st, a);
+        else if (a.k <= 16) hipLaunchKernelGGL((k_sketch<true, SeqAscii>), dim3(n_blocks), dim3(256), lds, st, a);
         else hipLaunchKernelGGL((k_sketch<false, SeqAscii>), dim3(n_blocks), dim3(256), lds, st, a);
     }
     LAUNCH_CHECK();
@@ -4182,14 +4305,17 @@ int launch_seed_write(const SeedArgs& a, int n_blocks, hipStream_t st) {
     LAUNCH_CHECK();
     return 0;
 }
+uint32_t sort_read_lds_words(const SortArgs& a) {
+    // the requested LDS (default SORT_LDS: one workgroup per CU), at least the two bitmaps
+    const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4;
+    size_t lds = std::max<size_t>(a.lds_words ? (size_t)a.lds_words * 4 : (size_t)SORT_LDS, bmb);
+    return (uint32_t)(std::min<size_t>(lds, (size_t)SORT_LDS) / 4);
+}
 int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
     if (a.n == 0) return 0;
-    const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4;
     if (stage == 0) hipLaunchKernelGGL(k_sort_small, dim3(a.n), dim3(256), 0, st, a);
     else if (stage == 1) {
-        // the requested LDS (default SORT_LDS: one workgroup per CU), at least the two bitmaps
-        size_t lds = std::max<size_t>(a.lds_words ? (size_t)a.lds_words * 4 : (size_t)SORT_LDS, bmb);
-        lds = std::min<size_t>(lds, (size_t)SORT_LDS);
+        const size_t lds = (size_t)sort_read_lds_words(a) * 4;
         SortArgs b = a;
         b.lds_words = (uint32_t)(lds / 4);
         // up to SORT_LDS_HALF: 512-thread workgroups, two per CU (one read's
@@ -4214,6 +4340,7 @@ int launch_sort_read(int stage, const SortArgs& a, hipStream_t st) {
         if (2u * b.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_big<true>, dim3(grid), dim3(1024), (size_t)SORT_LDS, st, b);
         else hipLaunchKernelGGL(k_sort_big<false>, dim3(grid), dim3(1024), (size_t)SORT_LDS, st, b);
     } else {
+        const size_t bmb = (size_t)2 * ((a.cells + 31) / 32) * 4;
         const size_t hb = (size_t)(RS_MAXP + 16) * RS_ND * 4;
         const size_t lds = std::min<size_t>(std::max<size_t>(bmb, hb), (size_t)SORT_LDS);
         if (2u * a.n_seq + 2u > (uint32_t)GOFF_LDS) hipLaunchKernelGGL(k_sort_radix<true>, dim3(std::min<uint32_t>(a.n, 512)), dim3(1024), lds, st, a);
