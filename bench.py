@@ -682,9 +682,21 @@ def main():
     pair_peak = VALU_INT32_OPS / OPS_PER_PAIR
     iso_prof, iso_cnt, iso_res, iso_nb = quiet_gpu_profile(lib, L, devs[0], units, batches, P, opts, n_batches, args) \
         if rank == 0 else (None, None, None, 0)
+    excluded = {}
     if iso_prof:
         slots = {k: v for k, v in iso_prof.items() if v[1] > 0}
-        dom = max(slots, key=lambda k: slots[k][0])
+        # the figure called frac must fit the step (its kernel time per step <= ms_per_step).  A
+        # tail-bound kernel (C5's k_chain_long: one wave on its longest segment for most of the
+        # launch) can take longer on the quiet GPU than the whole step, where the other contexts'
+        # kernels fill its idle CUs; such a slot is named in `excluded` and the next one is used
+        def fits(k):
+            return slots[k][0] / max(iso_nb, 1) <= ms_per_step * 1.0001
+        for k in sorted(slots, key=lambda k: -slots[k][0]):
+            if fits(k):
+                break
+            excluded[k] = {"quiet_ms_per_step": round(slots[k][0] / max(iso_nb, 1), 4),
+                           "reason": "quiet-GPU time per step exceeds the in-situ step (tail-bound; contexts overlap it)"}
+        dom = max((k for k in slots if k not in excluded), key=lambda k: slots[k][0], default=max(slots, key=lambda k: slots[k][0]))
         d_ms, d_calls = slots[dom]
         d_bytes = alg_bytes(iso_cnt, iso_res).get(dom, 0)
         frac_src = f"quiet GPU: one context, {iso_nb} batches x {P} units mapped back to back after the timed region"
@@ -726,7 +738,7 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_row": traffic_row,
         "avg_launch_ms": round(avg_s * 1e3, 4), "launches_per_step": launches_per_step,
         "kernel_ms_per_step": round(kernel_ms_per_step, 4), "alg_bytes_per_launch": int(bytes_per_launch),
-        "share_of_kernel_time": round(share, 4), "measured": frac_src,
+        "share_of_kernel_time": round(share, 4), "measured": frac_src, "excluded": excluded or None,
         "path_frac": round(path_frac, 6) if path_frac is not None else None,
         "path_note": "SURVEY.md §8d B(read) summed over the timed batches / step time / 8 TB/s (all kernels, host included)",
         "in_situ": in_situ,

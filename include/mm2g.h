@@ -348,7 +348,9 @@ enum {
     MM2G_KNOB_SEED_FUSE = 36,    /* reads the cell sort takes (k_sort_read) get their anchor keys from its first
                                     pass instead of k_seed_write (no separate write-then-read of the keys) [1] */
     MM2G_KNOB_SKETCH_X32 = 37,   /* k <= 15: k_sketch keeps the 32-bit hash alone in its LDS window [1]           */
-    MM2G_KNOB_COUNT = 38
+    MM2G_KNOB_BIG_WND = 38,      /* k_sort_big (reads over 65535 anchors): most windows its bucket pass appends
+                                    the kept keys to, <= 126; 0 = the per-key scatter to bucket slots [126]   */
+    MM2G_KNOB_COUNT = 39
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

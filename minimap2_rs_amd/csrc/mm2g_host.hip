@@ -111,6 +111,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SPEC_SWEEP_W: return 16;
     case MM2G_KNOB_SEED_FUSE: return 1;
     case MM2G_KNOB_SKETCH_X32: return 1;
+    case MM2G_KNOB_BIG_WND: return 126;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -1284,6 +1285,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     so.fuse_mmax = fuse_mmax;
+    so.big_wnd = (uint32_t)std::max<int64_t>(0, K[MM2G_KNOB_BIG_WND]);
     so.rd_off = c->d_rd_off; so.mz_base = mz_base; so.mz_cnt = mz_cnt; so.mz_y = (const uint32_t*)c->sk1.y.p;
     so.mz_n = mz_n; so.mz_poff = mz_poff; so.ix_pos = (const uint64_t*)c->dix->ix_pos.p; so.kl = kl; so.span = o->k;
     so.cap_pos = c->dix->ix_pos.cap / 8;

@@ -177,6 +177,7 @@ struct SortArgs {
     uint32_t* rcount = nullptr;
     const uint32_t* order = nullptr;   // k_sort_read: block b sorts read order[b] (heaviest first); null = b
     uint32_t* rwork = nullptr;         // k_sort_big: next list entry to take (zeroed by k_sort_small)
+    uint32_t big_wnd = 1u << 30;       // k_sort_big: most windows its P3 appends to (0: per-key scatter by bucket)
     // fused seeding (k_sort_read P1 writes the keys of the reads k_seed_write skipped; SeedArgs)
     uint32_t fuse_mmax = 0;
     const uint64_t* rd_off = nullptr; const uint64_t* mz_base = nullptr; const uint32_t* mz_cnt = nullptr;

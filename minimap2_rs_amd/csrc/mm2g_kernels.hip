@@ -1913,6 +1913,8 @@ DEVI uint32_t block_incl_min(uint32_t v, uint32_t* sc) {
 // work counter (the list is roughly heaviest first: k_sort_read defers in its
 // heaviest-first order).
 constexpr uint32_t BIG_NB_MAX = 16384;
+constexpr int BIG_WND = 126;                      // windows appended to by k_sort_big's P3 (more: per-key scatter)
+constexpr uint32_t BIG_WREG = 3 * BIG_WND + 4;   // LDS words of their bounds, starts and cursors (below the bucket counts)
 // k_sort_big / k_sort_read keep both cell bitmaps (2 x MAX_CELLS bits) plus the
 // bucket counts in SORT_LDS; `LW - 2 * nw - 64` below is unsigned
 static_assert(SORT_LDS / 4 > 2 * (MAX_CELLS / 32) + 64 + 4096, "MAX_CELLS bitmaps must leave LDS for the bucket counts");
@@ -1994,7 +1996,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
         BIG_PH(0);
         if (pq && tid == 0) pq[13] = nkc;
         // buckets of 2^bsh kept cells; their counts (then ends) CNT[0..NB] at the top of the LDS
-        const uint32_t nbmax = min(BIG_NB_MAX, LW - 2 * nw - 64);
+        const uint32_t nbmax = min(BIG_NB_MAX, LW - 2 * nw - 64 - BIG_WREG);
         uint32_t bsh = 0;
         while (((nkc + (1u << bsh) - 1) >> bsh) > nbmax) ++bsh;
         const uint32_t NB = (nkc + (1u << bsh) - 1) >> bsh;
@@ -2035,7 +2037,73 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
         if (tid == 0) { a.cnt2[r] = A; a.smax[r] = smx; s_nbig = 0; }
         __syncthreads();
         BIG_PH(1);
-        // ---- P3: scatter of the kept keys by bucket; CNT[b] turns into bucket b's end
+        // ---- windows of whole buckets (<= W keys; a bucket over W alone is radix-sorted in
+        // HBM), fixed before P3 from the bucket starts.  P3 then appends every kept key to its
+        // window's range of O (a few append streams per read, so the writes fill whole lines)
+        // with its bucket inside the window as a u16 tag, and each window gathers its keys by
+        // bucket into LDS.  (Round 4's P3 scattered each key straight to its bucket slot: a
+        // partial line per key, 470 us of a C5 read's 1400; measured: P3 473 -> 268 us per
+        // read.  Tagging the kept cell instead, with a count pass per window so the segments
+        // are single cells, measured slower: 10.7 against 10.0 ms per C5 batch.)  More than
+        // BIG_WND windows: that per-key scatter.  WB / WC / WS sit just below CNT.
+        uint32_t* WB = dyn + cofs - BIG_WREG;      // window w = buckets [WB[w], WB[w + 1])
+        uint32_t* WC = WB + BIG_WND + 1;           // P3 append cursors
+        uint32_t* WS = WC + BIG_WND;               // window starts in O (WS[nwnd] = A)
+        const uint32_t W = (((cofs - BIG_WREG - 16) * 32u) / 67u) & ~63u;
+        auto bstart0 = [&](uint32_t b) -> uint32_t { return b < NB ? CNT[b] : A; };   // bucket starts (before P4)
+        if (tid == 0) {
+            uint32_t nwnd = 0, ba = 0;
+            while (ba < NB && nwnd < min(a.big_wnd, (uint32_t)BIG_WND)) {
+                const uint32_t oa = bstart0(ba);
+                uint32_t lo = ba + 1, hi = NB;                  // last bb with bstart0(bb) <= oa + W
+                while (lo < hi) { const uint32_t mid = (lo + hi + 1) >> 1; if (bstart0(mid) - oa <= W) lo = mid; else hi = mid - 1; }
+                WB[nwnd] = ba; WS[nwnd] = oa; WC[nwnd] = oa;
+                ++nwnd;
+                ba = lo;
+            }
+            WB[nwnd] = ba; WS[nwnd] = A;
+            s_read = ba == NB ? nwnd : 0u;                      // 0: too many windows
+        }
+        __syncthreads();
+        const uint32_t nwnd = s_read;
+        uint16_t* T16 = (uint16_t*)(a.meta + base);
+        if (nwnd) {
+            uint32_t wpw = 1;
+            while (wpw * 2 <= nwnd) wpw *= 2;
+            for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U2) {
+                uint64_t x[SORT_U2];
+                uint32_t c[SORT_U2], kw[SORT_U2], pw[SORT_U2];
+#pragma unroll
+                for (int u = 0; u < SORT_U2; ++u) { const uint32_t i = i0 + (uint32_t)u * 1024 + tid; x[u] = i < A0 ? K[i] : 0; }
+#pragma unroll
+                for (int u = 0; u < SORT_U2; ++u) c[u] = cell_of(x[u]);
+#pragma unroll
+                for (int u = 0; u < SORT_U2; ++u) { kw[u] = B2[c[u] >> 5]; pw[u] = B1[c[u] >> 5]; }
+#pragma unroll
+                for (int u = 0; u < SORT_U2; ++u) {
+                    const uint32_t i = i0 + (uint32_t)u * 1024 + tid;
+                    const uint32_t b = c[u] & 31;
+                    const bool kept = i < A0 && ((kw[u] >> b) & 1u);
+                    const uint32_t bk = kept ? (pw[u] + (uint32_t)__popc(kw[u] & ((1u << b) - 1u))) >> bsh : 0u;
+                    uint32_t wd = 0;                                 // last window with WB[wd] <= bk
+                    for (uint32_t st = wpw; st; st >>= 1) if (wd + st < nwnd && WB[wd + st] <= bk) wd += st;
+                    // lanes of one window take consecutive slots: one LDS atomic per window per wave
+                    uint64_t peers = ballot(kept);
+                    for (uint32_t bit = 1; bit < nwnd; bit <<= 1) {
+                        const bool on = (wd & bit) != 0;
+                        const uint64_t m = ballot(on);
+                        peers &= on ? m : ~m;
+                    }
+                    const uint64_t lt = peers & lanemask_lt();
+                    uint32_t slot = 0;
+                    if (kept && lt == 0) slot = atomicAdd(&WC[wd], (uint32_t)__popcll(peers));
+                    const int leader = kept ? (int)__builtin_ctzll(peers) : lane;
+                    slot = (uint32_t)__shfl((int)slot, leader, 64) + (uint32_t)__popcll(lt);
+                    if (kept) { O[CK(slot, A0)] = x[u]; T16[CK(slot, A0)] = (uint16_t)(bk - WB[wd]); }
+                }
+            }
+        } else {
+        // ---- P3 (more than BIG_WND windows): scatter of the kept keys by bucket; CNT[b] turns into bucket b's end
         for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U2) {
             uint64_t x[SORT_U2];
             uint32_t c[SORT_U2], kw[SORT_U2], pw[SORT_U2];
@@ -2055,12 +2123,12 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                 }
             }
         }
+        }
         __syncthreads();
         BIG_PH(2);
-        // ---- P4: windows of whole buckets.  LDS below CNT: S[W] keys, then the
-        // bucket-start bitmap SB and its word scans LS / NS (W/32 + 2 words each).
-        auto bstart = [&](uint32_t b) -> uint32_t { return b ? CNT[b - 1] : 0u; };
-        const uint32_t W = (((cofs - 16) * 32u) / 67u) & ~63u;
+        // ---- P4: windows.  LDS below WB: S[W] keys, then the segment-start bitmap SB
+        // and its word scans LS / NS (W/32 + 2 words each).
+        auto bstart = [&](uint32_t b) -> uint32_t { return b ? CNT[b - 1] : 0u; };   // (fallback: bucket ends)
         uint64_t* S = dyn64;
         uint32_t* SB = dyn + 2 * W;
         uint32_t* LS = SB + (W >> 5) + 2;
@@ -2069,26 +2137,54 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
             __syncthreads();
             radix_range(O + s0, K + s0, O + s0, e0 - s0, qb, dyn, red);
         };
-        uint32_t ba = 0;
+        uint32_t ba = 0, wi = 0;
         while (ba < NB) {
-            const uint32_t oa = bstart(ba);
-            if (CNT[ba] - oa > W) {                 // one bucket beyond a window: radix in HBM
-                radix_big(oa, CNT[ba]);
-                if (pq && tid == 0) pq[7] += 1;
-                ba = ba + 1;
-                continue;
+            uint32_t bb, oa, nwin;
+            if (nwnd) {
+                bb = WB[wi + 1];
+                oa = WS[wi];
+                const uint32_t oe = WS[wi + 1];
+                ++wi;
+                if (bb == ba + 1 && oe - oa > W) {             // one bucket beyond a window: radix in HBM
+                    radix_big(oa, oe);
+                    __syncthreads();
+                    if (tid == 0) CNT[ba] = oe;                // its end, for the next window's bstart
+                    if (pq && tid == 0) pq[7] += 1;
+                    ba = bb;
+                    continue;
+                }
+                nwin = oe - oa;
+                __syncthreads();
+                // the window's keys by bucket into LDS; CNT[b] (its start) turns into bucket b's end
+                block_pass_km<SORT_UG>(O + oa, T16 + oa, nwin, [&](uint32_t, uint64_t x, uint16_t m) {
+                    S[atomicAdd(&CNT[ba + (uint32_t)m], 1u) - oa] = x;
+                });
+                const uint32_t nwd0 = (nwin + 31) >> 5;
+                for (uint32_t q = tid; q < nwd0; q += 1024) SB[q] = 0;
+                __syncthreads();
+                for (uint32_t b = ba + tid; b < bb; b += 1024) { const uint32_t p = bstart(b) - oa; atomicOr(&SB[p >> 5], 1u << (p & 31)); }
+                __syncthreads();
+            } else {
+                oa = bstart(ba);
+                if (CNT[ba] - oa > W) {                 // one bucket beyond a window: radix in HBM
+                    radix_big(oa, CNT[ba]);
+                    if (pq && tid == 0) pq[7] += 1;
+                    ba = ba + 1;
+                    continue;
+                }
+                uint32_t lo = ba + 1, hi = NB;          // last bb with bstart(bb) <= oa + W
+                while (lo < hi) { const uint32_t mid = (lo + hi + 1) >> 1; if (bstart(mid) - oa <= W) lo = mid; else hi = mid - 1; }
+                bb = lo;
+                nwin = bstart(bb) - oa;
+                __syncthreads();
+                block_pass8<SORT_UG>(O + oa, nwin, [&](uint32_t i, uint64_t x) { S[i] = x; });
+                const uint32_t nwd0 = (nwin + 31) >> 5;
+                for (uint32_t q = tid; q < nwd0; q += 1024) SB[q] = 0;
+                __syncthreads();
+                for (uint32_t b = ba + tid; b < bb; b += 1024) { const uint32_t p = bstart(b) - oa; atomicOr(&SB[p >> 5], 1u << (p & 31)); }
+                __syncthreads();
             }
-            uint32_t lo = ba + 1, hi = NB;          // last bb with bstart(bb) <= oa + W
-            while (lo < hi) { const uint32_t mid = (lo + hi + 1) >> 1; if (bstart(mid) - oa <= W) lo = mid; else hi = mid - 1; }
-            const uint32_t bb = lo;
-            const uint32_t nwin = bstart(bb) - oa;
             const uint32_t nwd = (nwin + 31) >> 5;
-            __syncthreads();
-            block_pass8<SORT_UG>(O + oa, nwin, [&](uint32_t i, uint64_t x) { S[i] = x; });
-            for (uint32_t q = tid; q < nwd; q += 1024) SB[q] = 0;
-            __syncthreads();
-            for (uint32_t b = ba + tid; b < bb; b += 1024) { const uint32_t p = bstart(b) - oa; atomicOr(&SB[p >> 5], 1u << (p & 31)); }
-            __syncthreads();
             // LS[q]: last bucket start in words <= q; NS[q]: first bucket start in words >= q (NS[nwd] = nwin)
             for (uint32_t q0 = 0; q0 < nwd; q0 += 1024) {
                 const uint32_t q = q0 + tid;

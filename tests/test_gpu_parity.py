@@ -349,15 +349,18 @@ def test_multi_chain_vs_oracle(dev, small_world, dense_world, mc, m):
     dev.set_debug(True)
 
 
-@pytest.mark.parametrize("seg_small,lds_kb", [(1024, 0), (64, 0), (8, 0), (1, 0), (1024, 76), (8, 76)])
-def test_filtered_sort_parity(dev, small_world, dense_world, seg_small, lds_kb):
+@pytest.mark.parametrize("seg_small,lds_kb,big_wnd", [(1024, 0, 126), (64, 0, 126), (8, 0, 126), (1, 0, 126), (1024, 76, 126),
+                                                     (8, 76, 126), (1024, 0, 0), (1024, 0, 2)])
+def test_filtered_sort_parity(dev, small_world, dense_world, seg_small, lds_kb, big_wnd):
     """Production sort (cell buckets + per-segment ranking, singleton filter
     on): the anchors the DP runs on equal the oracle's sorted anchors minus
     the singletons, for every path -- thread-ranked small segments, block-
     ranked and radix-sorted big ones, the whole-read radix when too many big
     segments (seg_small 1) or too many anchors (> 65535) appear.  lds_kb 76:
-    the 512-thread, two-per-CU k_sort_read (smaller windows, more of them)."""
-    with knobs(dev, sort_small=1, seg_small=seg_small, sort_lds_kb=lds_kb):
+    the 512-thread, two-per-CU k_sort_read (smaller windows, more of them).
+    big_wnd: k_sort_big's bucket pass appends to at most that many windows
+    (0: the per-key scatter; 2: reads with more windows fall back to it)."""
+    with knobs(dev, sort_small=1, seg_small=seg_small, sort_lds_kb=lds_kb, big_wnd=big_wnd):
         rng = random.Random(5)
         for world, mids in ((small_world, (None,)), (dense_world, (20, 5000, 100000))):
             ref, reads, rnames, rseqs = world
