@@ -240,10 +240,18 @@ struct SeqNt4 {
 // X32 (k <= 15, not HPC): the LDS window holds the 32-bit hash alone (hash < 4^k < 2^30, so
 // ~0u stays free for "no info"); every x = hash << 8 | k then, so x and hash order alike
 template <bool K32, typename Src, bool HPC = false, bool X32 = false>
-#ifndef SK_WPE
-#define SK_WPE(Src) (std::is_same<Src, SeqNt4>::value ? 5 : 4)   // waves per SIMD: the query sketch (nt4) at 96 VGPRs, 5 waves per SIMD; the index build (ASCII) at 128
+// waves per SIMD (override with -D): the query sketch (nt4) at 96 VGPRs 5; the index build
+// (ASCII) at 128 4; the 32-bit window (X32) at 80 VGPRs 6 (no spills)
+#ifndef SK_WPE_NT4
+#define SK_WPE_NT4 5
 #endif
-__global__ __launch_bounds__(256, X32 ? 6 : SK_WPE(Src)) void k_sketch(SketchArgs a) {
+#ifndef SK_WPE_ASCII
+#define SK_WPE_ASCII 4
+#endif
+#ifndef SK_WPE_X32
+#define SK_WPE_X32 6
+#endif
+__global__ __launch_bounds__(256, X32 ? SK_WPE_X32 : (std::is_same<Src, SeqNt4>::value ? SK_WPE_NT4 : SK_WPE_ASCII)) void k_sketch(SketchArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     static_assert(!X32 || (K32 && !HPC), "X32: k <= 15 query/index sketch without HPC spans");
     using XT = typename std::conditional<X32, uint32_t, uint64_t>::type;

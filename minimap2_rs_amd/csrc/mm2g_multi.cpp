@@ -220,7 +220,10 @@ void multi_chain_read(const uint64_t* xy, const int32_t* f, const int32_t* pprev
             }
         }
     }
-    if (chains.empty()) {                             // fallback (lchain.rs:162-173): last argmax f, score v[best]
+    // fallback (lchain.rs:162-173): last argmax f, score v[best].  Unreachable under
+    // multi_chain_opts (-m <= k, min_cnt <= 1): anchor 0 has pprev -1 and f = span >= -m, so it
+    // always yields a one-anchor chain above; kept for callers with other f / pprev.
+    if (chains.empty()) {
         std::vector<int32_t> vv((size_t)n);
         int64_t best = 0;
         for (int64_t i = 0; i < n; ++i) {
