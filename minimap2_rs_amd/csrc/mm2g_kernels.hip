@@ -487,7 +487,16 @@ __global__ __launch_bounds__(256, X32 ? SK_WPE_X32 : (std::is_same<Src, SeqNt4>:
                         const int ii = (int)(i - hbase);
                         const XT xi = act ? X[SKP(ii)] : XMAX;
                         const int32_t l = act ? (int32_t)(LZ[SKP(ii)] & 0x7fffu) : 0;
-                        need |= act && l == w + k - 1 && mxo != XMAX;                 // A (sketch.rs:90-93)
+                        // A (sketch.rs:90-93): at the first full window, the slots before i that tie
+                        // the minimum (other than the minimum's own slot) are emitted.  Ties of random
+                        // hashes are rare, so the lane looks for one and only then takes the exact path
+                        // (every read start and every N run used to send its tile there: 5 % of tiles)
+                        if (act && l == w + k - 1 && mxo != XMAX) {
+                            for (int d = 1; d < w; ++d) {
+                                const int q = ii - w + d;
+                                need |= q != mqo && X[SKP(q)] == mxo;
+                            }
+                        }
                         const bool doB = act && xi <= mxo;                              // B (94-96)
                         const bool doC = act && !doB && mqo == ii - w;                  // C (97-105)
                         if (((doB && l >= w + k && mxo != XMAX) || (doC && l >= w + k - 1)) && i >= efrom) {
