@@ -375,36 +375,40 @@ __global__ __launch_bounds__(256, X32 ? SK_WPE_X32 : (std::is_same<Src, SeqNt4>:
             KT kf2 = (KT)kf, kr2 = (KT)kr;
             const KT kmask = (KT)mask;
             bool rs = false; int32_t lc = 0;
+            uint32_t flz = 0;   // per position t: fl (0 ambiguous, 1 symmetric, 2 info) | z << 2, at bits 3t
+            // branch-free per position (a divergent if per position cost exec-mask saves and
+            // SGPR spills); every slot of the tile exists in LDS, so a position past the read's
+            // end is written too (never read: the next tile's history needs positions < L)
 #pragma unroll
             for (int t = 0; t < SK_CH; ++t) {
                 const int64_t p = ps + t;
-                if (p < pe) {
-                    const int ix = (int)(p - hbase);
-                    const uint32_t c = (code16 >> (2 * (7 - t))) & 3u;
-                    XT x = XMAX; uint16_t fl = 0, z = 0;
-                    if ((valid8 >> t) & 1u) {
-                        kf2 = ((kf2 << 2) | (KT)c) & kmask; kr2 = (kr2 >> 2) | ((KT)(3 ^ c) << shift1);
-                        fl = 1;
-                        if (kf2 != kr2) {
-                            z = kf2 < kr2 ? 0 : 1;
-                            const uint64_t km = z ? kr2 : kf2;
-                            uint64_t h;
-                            if (K32) h = hash64d<uint32_t>((uint32_t)km, (uint32_t)mask);
-                            else h = hash64d<uint64_t>(km, mask);
-                            if constexpr (HPC) {               // TinyQueue span (sketch.rs:51-64, 72)
-                                const uint32_t sp = a.hpc_span[roff + (uint64_t)p];
-                                x = sp < 256u ? (h << 8) | (uint64_t)sp : U64MAX;
-                            } else if constexpr (X32) {
-                                x = (XT)h;                     // X32: the hash alone (span == k)
-                            } else {
-                                x = (h << 8) | (uint64_t)k;    // kmer_span == k whenever info is valid
-                            }
-                            fl = 2;
-                        }
-                    }
-                    X[SKP(ix)] = x; LZ[SKP(ix)] = (uint16_t)(fl | (z << 15));
-                    if (fl == 0) { rs = true; lc = 0; } else if (fl == 2) { lc = lc + 1 < CAP ? lc + 1 : CAP; }
+                const bool in = p < pe;
+                const int ix = (int)(p - hbase);
+                const uint32_t c = (code16 >> (2 * (7 - t))) & 3u;
+                const bool v = in && ((valid8 >> t) & 1u);
+                const KT nkf = ((kf2 << 2) | (KT)c) & kmask, nkr = (kr2 >> 2) | ((KT)(3 ^ c) << shift1);
+                kf2 = v ? nkf : kf2; kr2 = v ? nkr : kr2;
+                const bool ns = kf2 != kr2;
+                const uint32_t z = kf2 < kr2 ? 0u : 1u;
+                const uint64_t km = z ? kr2 : kf2;
+                uint64_t h;
+                if (K32) h = hash64d<uint32_t>((uint32_t)km, (uint32_t)mask);
+                else h = hash64d<uint64_t>(km, mask);
+                XT x;
+                if constexpr (HPC) {               // TinyQueue span (sketch.rs:51-64, 72)
+                    const uint32_t sp = (v && ns) ? a.hpc_span[roff + (uint64_t)p] : 256u;
+                    x = sp < 256u ? (h << 8) | (uint64_t)sp : U64MAX;
+                } else if constexpr (X32) {
+                    x = (v && ns) ? (XT)h : XMAX;  // X32: the hash alone (span == k)
+                } else {
+                    x = (v && ns) ? (h << 8) | (uint64_t)k : XMAX;   // kmer_span == k whenever info is valid
                 }
+                const uint32_t fl = v ? (ns ? 2u : 1u) : 0u;
+                X[SKP(ix)] = x;
+                flz |= (fl | ((v && ns ? z : 0u) << 2)) << (3 * t);
+                const bool r0 = in && fl == 0u;
+                rs |= r0;
+                lc = r0 ? 0 : ((in && fl == 2u) ? (lc + 1 < CAP ? lc + 1 : CAP) : lc);
             }
             // ---- segmented scan of l over lanes: (reset, count)
             int32_t er, ec;
@@ -419,20 +423,17 @@ __global__ __launch_bounds__(256, X32 ? SK_WPE_X32 : (std::is_same<Src, SeqNt4>:
                 if (ln == 0) { er = 0; ec = 0; }
             }
             const int32_t lin = er ? ec : (l_carry + ec < CAP ? l_carry + ec : CAP);
-            wave_lds_sync();
-            // ---- phase 1b: l per position; invalidate info where l < k
+            // ---- phase 1b: l per position (the flags from registers); invalidate info where l < k
             int32_t lv = lin;
 #pragma unroll
             for (int t = 0; t < SK_CH; ++t) {
                 const int64_t p = ps + t;
-                if (p < pe) {
-                    const int ix = (int)(p - hbase);
-                    const uint16_t v = LZ[SKP(ix)];
-                    const uint16_t fl = v & 3u;
-                    if (fl == 0) lv = 0; else if (fl == 2) lv = lv + 1 < CAP ? lv + 1 : CAP;
-                    LZ[SKP(ix)] = (uint16_t)((v & 0x8000u) | (uint16_t)lv);
-                    if (!(fl == 2 && lv >= k)) X[SKP(ix)] = XMAX;
-                }
+                const bool in = p < pe;
+                const int ix = (int)(p - hbase);
+                const uint32_t fl = (flz >> (3 * t)) & 3u, z = (flz >> (3 * t + 2)) & 1u;
+                lv = !in ? lv : (fl == 0u ? 0 : (fl == 2u ? (lv + 1 < CAP ? lv + 1 : CAP) : lv));
+                LZ[SKP(ix)] = (uint16_t)((z << 15) | (uint32_t)lv);
+                if (in && !(fl == 2u && lv >= k)) X[SKP(ix)] = XMAX;
             }
             {
                 const int64_t te = t0 + SK_TS < L ? t0 + SK_TS : L;
