@@ -342,9 +342,7 @@ enum {
     MM2G_KNOB_SPEC_BATCH = 32,   /* predecessors per step of k_chain_long's speculative rounds: 4 or 8 [4]     */
     MM2G_KNOB_DV_PAR = 33,       /* odd index k: k_dv matches the chain against the minimizer positions by one
                                     parallel search per chain anchor instead of the sequential walk [1]     */
-    MM2G_KNOB_SPEC_SWEEPS = 34,  /* k_chain_long: cheap guess sweeps (no marks, no n_skip) before the speculative
-                                    rounds of a block, 0..4 [0]                                              */
-    MM2G_KNOB_SPEC_SWEEP_W = 35, /* ... over this many nearest predecessors, 1..64 [16]                       */
+    /* 34, 35: retired (round 5: k_chain_long guess sweeps before the speculative rounds, measured no faster) */
     MM2G_KNOB_SEED_FUSE = 36,    /* reads the cell sort takes (k_sort_read) get their anchor keys from its first
                                     pass instead of k_seed_write (no separate write-then-read of the keys) [1] */
     MM2G_KNOB_SKETCH_X32 = 37,   /* k <= 15: k_sketch keeps the 32-bit hash alone in its LDS window [1]           */

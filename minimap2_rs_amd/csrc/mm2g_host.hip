@@ -107,8 +107,6 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SEG_SPARSE: return 1;
     case MM2G_KNOB_SPEC_BATCH: return 4;
     case MM2G_KNOB_DV_PAR: return 1;
-    case MM2G_KNOB_SPEC_SWEEPS: return 0;
-    case MM2G_KNOB_SPEC_SWEEP_W: return 16;
     case MM2G_KNOB_SEED_FUSE: return 1;
     case MM2G_KNOB_SKETCH_X32: return 1;
     case MM2G_KNOB_BIG_WND: return 126;
@@ -761,9 +759,18 @@ static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf, Re
     const uint32_t slot = c->redo ? 0u : (uint32_t)std::max<int64_t>(0, std::min<int64_t>(c->knob[MM2G_KNOB_WS_MIN], 1 << 30));
     if (!B.exact) B.cap = slot ? (uint64_t)slot * n + 16 : c->total_bases + 16ull * n + 16;
     ENSURE(B.x, uint64_t, B.cap, x); ENSURE(B.y, uint32_t, B.cap, y);
+    // query views (odd k only: the fixed warm-up is exact there, DESIGN.md §10; a re-run
+    // after a slot overflow has them off, so the exact per-read layout needs one pass)
+    const uint32_t V = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(c->knob[MM2G_KNOB_SKETCH_VIEW], 1 << 30));
+    // ... and only for batches too small to fill the GPU with one wave per read
+    // (C2's 500-read units; C3's 5,000-read units measured 4 % slower with views)
+    const bool few = (int64_t)n < c->knob[MM2G_KNOB_VIEW_READS];
+    const bool views = V >= 64 && (k & 1) && few && !c->views_off && c->max_read_len > V && !c->knob[MM2G_KNOB_SKETCH_PROF] && !slot;
     if (!B.exact) {   // (zout / zst: the batch's outputs and status block are cleared here too)
-        ProfScope ps(c, "mz_base");
-        LCHK(launch_mz_base(n, c->d_rd_off, base, end, slot, c->stream, zout, zst, STAT_WORDS));
+        if (!views) {   // (with views: k_view_plan does it)
+            ProfScope ps(c, "mz_base");
+            LCHK(launch_mz_base(n, c->d_rd_off, base, end, slot, c->stream, zout, zst, STAT_WORDS));
+        }
     } else {
         if (zout) HIPCHK(hipMemsetAsync(zout, 0, sizeof(ReadOut) * ((size_t)n + 1), c->stream));
         if (zst) HIPCHK(hipMemsetAsync(zst, 0, STAT_WORDS * 8, c->stream));
@@ -771,13 +778,7 @@ static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf, Re
     SketchArgs a{nullptr, c->d_rd_off, n, w, k, base, end, x, y, cnt, ovf};
     a.x64 = c->knob[MM2G_KNOB_SKETCH_X32] ? 0u : 1u;
     a.pk_words = c->d_words; a.pk_off = c->d_pk_off; a.amb_off = c->d_amb_off; a.mz_need = need;
-    // query views (odd k only: the fixed warm-up is exact there, DESIGN.md §10; a re-run
-    // after a slot overflow has them off, so the exact per-read layout needs one pass)
-    const uint32_t V = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(c->knob[MM2G_KNOB_SKETCH_VIEW], 1 << 30));
-    // ... and only for batches too small to fill the GPU with one wave per read
-    // (C2's 500-read units; C3's 5,000-read units measured 4 % slower with views)
-    const bool few = (int64_t)n < c->knob[MM2G_KNOB_VIEW_READS];
-    if (V >= 64 && (k & 1) && few && !c->views_off && c->max_read_len > V && !c->knob[MM2G_KNOB_SKETCH_PROF] && !slot) {
+    if (views) {
         const uint32_t W0 = (uint32_t)((2 * (w + k) + 64 + 7) & ~7);
         const uint64_t nvmax = (uint64_t)n + c->total_bases / V + 1;
         uint32_t *v_read, *v_len, *v_pre, *v_from, *v_cnt, *v_need, *nvr; uint64_t *v_off, *v_base, *v_end, *vo, *vx; uint8_t* v_last; uint32_t* vy;
@@ -790,10 +791,9 @@ static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf, Re
         ENSURE(Vb.x, uint64_t, vcap, vx); ENSURE(Vb.y, uint32_t, vcap, vy);
         {
             ProfScope ps(c, "sketch_views");
-            HIPCHK(hipMemsetAsync(v_len, 0, nvmax * 4, c->stream));     // views past the real count: empty
-            LCHK(launch_view_count(n, c->d_rd_off, V, nvr, c->stream));
-            LCHK(launch_excl_scan(nvr, n, vo, 0, 0, k, 0, nullptr, 0, 0, c->stream));
-            LCHK(launch_view_fill(n, c->d_rd_off, V, W0, vo, v_read, v_off, v_len, v_pre, v_from, v_last, v_base, v_end, c->stream));
+            (void)nvr;
+            LCHK(launch_view_plan(n, c->d_rd_off, V, W0, nvmax, vo, v_read, v_off, v_len, v_pre, v_from, v_last, v_base, v_end,
+                                  B.exact ? nullptr : base, end, zout, zst, STAT_WORDS, c->stream));
         }
         SketchArgs va = a;
         va.n = (uint32_t)nvmax; va.out_base = v_base; va.out_end = v_end; va.mz_x = vx; va.mz_y = vy; va.mz_cnt = v_cnt; va.mz_need = v_need;
@@ -889,7 +889,7 @@ static int check_opts(mm2g_ctx* c, const mm2g_map_opts* o, int32_t& mdx0, int32_
 static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const ChainKParams& P0, float gap, int npass, int32_t mdx1,
                      int32_t mdy1, int32_t bw_long, uint64_t A_cap, const uint64_t* a_off, const uint32_t* a_cnt, uint64_t* keys,
                      uint64_t* ktmp, const uint32_t* cnt2, const uint64_t* smax, ReadOut* out, const uint32_t* abort, bool full,
-                     unsigned long long* stat = nullptr, bool order_ready = false) {
+                     unsigned long long* stat = nullptr, bool order_ready = false, const uint32_t* sum_mz = nullptr) {
     int32_t *fb, *pb;
     ENSURE(c->fbuf, int32_t, A_cap, fb); ENSURE(c->ppbuf, int32_t, A_cap, pb);
     int16_t* lut; uint32_t* work;
@@ -943,8 +943,6 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     ca.seg_chunk = std::max<uint32_t>(64u, (uint32_t)K[MM2G_KNOB_SEG_CHUNK] & ~63u);
     ca.spec_rounds = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(16, K[MM2G_KNOB_SPEC_ROUNDS]));
     ca.spec_batch = K[MM2G_KNOB_SPEC_BATCH] == 8 ? 8u : 4u;
-    ca.spec_sweeps = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(4, K[MM2G_KNOB_SPEC_SWEEPS]));
-    ca.spec_sweep_w = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(64, K[MM2G_KNOB_SPEC_SWEEP_W]));
     // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
     // settle in a few no-break policy-iteration rounds.  Pass 0's long segments
     // are real chains whose windows carry many mark sources: k_chain_long is
@@ -979,6 +977,9 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         ca.zero_fmin = ca.fmin && (pass == 0 || !rescue_wider) ? 1u : 0u;   // cleared by k_seg_items
         ca.sq = nullptr; ca.sq_cap = 0;
         ca.sq_n = (ca.fmin && isob) ? sq_n : nullptr;                      // ... as is the item counter
+        // the last pass's k_seg_items also writes the batch sums (status words 3 and 4): one launch less
+        ca.bsum = (sum_mz && stat && pass == npass - 1) ? stat : nullptr;
+        ca.mz_cnt = sum_mz;
         {
             ProfScope ps(c, pass ? "chain_items_rescue" : "chain_items");
             LCHK(launch_chain_stage(6, ca, 1, c->stream));
@@ -1228,20 +1229,19 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     if (!c->ws_exact) c->cap_A = std::max<uint64_t>(c->cap_A, 3 * c->total_bases + 65536);   // exact-size mode: see reserve_anchor_ws
     if (c->knob[MM2G_KNOB_WS_MIN] > 0 && !c->redo) c->cap_A = (uint64_t)c->knob[MM2G_KNOB_WS_MIN];   // tests: force the re-map
     uint64_t A_cap = c->cap_A;
+    // reads heaviest first (anchor counts from seed_count): the hand-out order of
+    // seed_write, the sort and the chain work items; made by the anchor scan's block
+    uint32_t* rorder;
+    ENSURE(c->order, uint32_t, n, rorder);
     {
         ProfScope ps(c, "scan");
-        LCHK(launch_excl_scan(a_cnt, n, a_off, 0, 0, o->k, A_cap, st32, BS_ANCHORS, 2, c->stream));
+        LCHK(launch_excl_scan(a_cnt, n, a_off, 0, 0, o->k, A_cap, st32, BS_ANCHORS, 2, c->stream, rorder));
     }
     if (int e = reserve_anchor_ws(c, st, A_cap)) return e;
     uint64_t* keys = (uint64_t*)c->keys.p;
     uint64_t* ktmp = (uint64_t*)c->keys_tmp.p;
     int32_t* fb = (int32_t*)c->fbuf.p;      // the sort's per-key tags live here before the DP needs it
     sa.keys = keys; sa.cap_keys = c->keys.cap / 8;
-    // reads heaviest first (anchor counts from seed_count): the hand-out order of
-    // seed_write, the sort and the chain work items
-    uint32_t* rorder;
-    ENSURE(c->order, uint32_t, n, rorder);
-    LCHK(launch_read_order(n, a_cnt, rorder, c->stream));
     sa.order = rorder;
     // 4. anchor sort (seeds.rs:58).  The singleton filter needs every max_dist_x
     //    of both DP passes within one 2^CELL_SHIFT cell (DESIGN.md "Anchor sort");
@@ -1312,7 +1312,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     if (chain) {
         // 5. chain DP + fallback + rescue
         if (int e = run_chain(c, n, c->d_rd_off, P, gap, npass, mdx1, std::max(o->max_gap, o->bw_long), o->bw_long, A_cap,
-                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, full, st, true))
+                              a_off, a_cnt, keys, ktmp, cnt2, smax, out, st32, full, st, true, mz_cnt))
             return e;
         // 6. dv inputs (paf.rs:156-199): sketch with the INDEX w/k (Q3)
         const bool sep = (H.w != o->w || H.k != o->k);
@@ -1329,7 +1329,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         ProfScope ps(c, "dv");
         if (stop_at != 4) LCHK(launch_dv(da, c->stream));
     }
-    LCHK(launch_batch_sums(n, mz_cnt, cnt2, st, c->stream));
+    if (!chain) LCHK(launch_batch_sums(n, mz_cnt, cnt2, st, c->stream));   // (else the last chain pass's k_seg_items)
     HIPCHK(hipMemcpyAsync(c->h_out, out, (size_t)n * sizeof(ReadOut), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_stat, st, STAT_WORDS * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipEventRecord(c->ev_done, c->stream));

@@ -224,8 +224,8 @@ struct ChainArgs {
     void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
     uint32_t spec_rounds = 3; // k_chain_long: speculative rounds per 64-anchor block (MM2G_KNOB_SPEC_ROUNDS)
     uint32_t spec_batch = 4;  // k_chain_long: predecessors per step of a speculative round, 4 or 8 (MM2G_KNOB_SPEC_BATCH)
-    uint32_t spec_sweeps = 0; // k_chain_long: cheap guess sweeps before the rounds (MM2G_KNOB_SPEC_SWEEPS)
-    uint32_t spec_sweep_w = 16; // ... over this many nearest predecessors (MM2G_KNOB_SPEC_SWEEP_W)
+    const uint32_t* mz_cnt = nullptr;    // with bsum: k_seg_items writes bsum[3] = sum mz_cnt, bsum[4] = sum cnt2
+    unsigned long long* bsum = nullptr;
     int32_t est_lane = 0;    // k_chain_seg (production): estimated DP pairs up to which a segment takes one lane
     uint32_t full_dp = 0;    // debug mode (exact f/pprev everywhere): pass 0 uses EST_LANE instead of est_lane
     uint32_t giant_exact;    // 1: policy iteration on the reference loop itself (pass 0's real chains)
@@ -277,8 +277,9 @@ int launch_dv(const mm2g::DvArgs& a, hipStream_t st);
 // table size of a read with in[t] minimizers (0 when it fits k_filter_lds).  When
 // cap > 0 and the total exceeds it, `bit` is OR-ed into status[0]; status[slot]
 // receives the total.
+// order (mode 0 over anchor counts): also the heaviest-first read order (k_read_order's)
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k, uint64_t cap, uint32_t* status,
-                     uint32_t bit, int slot, hipStream_t st);
+                     uint32_t bit, int slot, hipStream_t st, uint32_t* order = nullptr);
 // per-batch sums for the counters: status64[3] = sum mz_cnt, status64[4] = sum cnt2
 int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, unsigned long long* status64, hipStream_t st);
 // minimizer slots: read r gets [rd_off[r] + 16r, rd_off[r+1] + 16(r+1)), or `slot` entries each when non-zero (tests)
@@ -289,6 +290,10 @@ int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t*
 int launch_view_count(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t* nv, hipStream_t st);
 int launch_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, const uint64_t* vo, uint32_t* v_read, uint64_t* v_off,
                      uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end, hipStream_t st);
+// the same view table in one single-workgroup launch, plus launch_mz_base's work when base is given
+int launch_view_plan(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, uint64_t nvmax, uint64_t* vo, uint32_t* v_read,
+                     uint64_t* v_off, uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end,
+                     uint64_t* base, uint64_t* end, mm2g::ReadOut* zout, unsigned long long* zst, int zst_words, hipStream_t st);
 int launch_view_compact(uint32_t n, const uint64_t* vo, const uint64_t* v_off, const uint64_t* v_base, const uint32_t* v_cnt,
                         const uint32_t* v_need, const uint64_t* vx, const uint32_t* vy, const uint64_t* base, const uint64_t* end, uint64_t* x,
                         uint32_t* y, uint32_t* cnt, uint32_t* need, int32_t* overflow, hipStream_t st);

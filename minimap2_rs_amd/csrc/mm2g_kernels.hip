@@ -2448,6 +2448,19 @@ __global__ __launch_bounds__(1024) void k_seg_items(ChainArgs a) {
         __syncthreads();
     }
     if (tid == 0) a.item_off[a.n] = carry;
+    if (a.bsum) {   // the batch sums of k_batch_sums (minimizers, anchors in the DP)
+        __shared__ unsigned long long ws[2][16];
+        unsigned long long v[2] = {0, 0};
+        for (uint32_t i = (uint32_t)tid; i < a.n; i += 1024) { v[0] += a.mz_cnt[i]; v[1] += a.cnt2[i]; }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) { v[q] = wave_sum64(v[q]); if (lane == 0) ws[q][wv] = v[q]; }
+        __syncthreads();
+        if (tid < 2) {
+            unsigned long long x = 0;
+            for (int t = 0; t < 16; ++t) x += ws[tid][t];
+            a.bsum[3 + tid] = x;
+        }
+    }
 }
 
 // item -> (position in order, chunk): last t with item_off[t] <= it
@@ -3184,40 +3197,6 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     if (kv) rfp[k & (RK - 1)] = make_int2(gf, okp ? k - 1 : -1);
                 }
                 wave_lds_sync();
-                // cheaper guess sweeps (Jacobi over the spec_sweep_w nearest predecessors, no marks or
-                // n_skip): the running maximum in the reference's visiting order (strict >, j
-                // descending) on the current guesses.  A guess only; the rounds below decide.  On
-                // dense 100 kb chains a block then needs ~25 % fewer full rounds (host simulation,
-                // DESIGN.md "Speculative blocks").
-                for (int sw = 0; sw < (int)a.spec_sweeps; ++sw) {
-                    int32_t mf = span, mj = -1;
-                    const int32_t wlim = min(dlim, (int32_t)a.spec_sweep_w);
-                    for (int d0 = 1; d0 <= (int)a.spec_sweep_w; d0 += SB) {
-                        if (!any(kv && d0 <= wlim)) break;
-                        int32_t svs[SB];
-                        bool oks[SB];
-#pragma unroll
-                        for (int u = 0; u < SB; ++u) {
-                            const int d = d0 + u;
-                            const bool inr = kv && d <= wlim;
-                            const int32_t j = k - d;
-                            uint64_t kj = 0;
-                            int32_t fj = 0;
-                            if (inr) { kj = rkey[j & (RK - 1)]; fj = rfp[j & (RK - 1)].x; }
-                            const int32_t dq = qk - (int32_t)(kj & qmask), dr = pk - (int32_t)((kj >> qb) & rmask);
-                            const int32_t dd = dr - dq < 0 ? dq - dr : dr - dq;
-                            oks[u] = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
-                            const int32_t dg = dr < dq ? dr : dq;
-                            svs[u] = (span < dg ? span : dg) - (int32_t)lut[oks[u] ? dd : 0] + fj;
-                        }
-#pragma unroll
-                        for (int u = 0; u < SB; ++u)
-                            if (oks[u] && svs[u] > mf) { mf = svs[u]; mj = k - (d0 + u); }
-                    }
-                    wave_lds_sync();                    // every lane has read the old guesses
-                    if (kv) rfp[k & (RK - 1)] = make_int2(mf, mj);
-                    wave_lds_sync();
-                }
                 int32_t committed = ib;
                 for (int rnd = 0; rnd < (int)a.spec_rounds && committed < ie; ++rnd) {
                     const bool act0 = kv && k >= committed;
@@ -4074,15 +4053,12 @@ __global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
     O->group = (int32_t)g; O->best_i = best_i;
 }
 
-// order[t] = reads by descending anchor count (largest-first hand-out to the
-// chain waves).  Counting sort on log2 buckets of the anchor count keeps it one
-// cheap pass: exact LPT is not needed, only "heavy reads first".
-// Reads heaviest first (buckets of 512 anchors, descending): the hand-out order
-// of the per-read sort and of the chain work items (longest-processing-time
-// first, so the heaviest reads do not form the kernels' tails).
-__global__ __launch_bounds__(1024) void k_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order) {
+// order[t] = reads heaviest first (a counting sort on buckets of 512 anchors,
+// descending): the hand-out order of the per-read sort and of the chain work
+// items (longest-processing-time first, so the heaviest reads do not form the
+// kernels' tails; exact LPT is not needed).  Block-wide.
+DEVI void read_order_block(uint32_t n, const uint32_t* a_cnt, uint32_t* order, uint32_t* hist, uint32_t* s_sc) {
     constexpr int NB = 1024;
-    __shared__ uint32_t hist[NB], s_sc[16];
     const int tid = threadIdx.x;
     hist[tid] = 0;
     __syncthreads();
@@ -4095,6 +4071,11 @@ __global__ __launch_bounds__(1024) void k_read_order(uint32_t n, const uint32_t*
     hist[tid] = ex;
     __syncthreads();
     for (uint32_t r = tid; r < n; r += 1024) order[atomicAdd(&hist[bucket(a_cnt[r])], 1u)] = r;
+}
+
+__global__ __launch_bounds__(1024) void k_read_order(uint32_t n, const uint32_t* a_cnt, uint32_t* order) {
+    __shared__ uint32_t hist[1024], s_sc[16];
+    read_order_block(n, a_cnt, order, hist, s_sc);
 }
 
 // 6. dv inputs — paf_from_chain_with_primary (src/paf.rs:156-199): binary
@@ -4206,9 +4187,10 @@ __global__ __launch_bounds__(64) void k_dv(DvArgs a) {
 // out[i] = sum_{t<i} f(in[t]) for i in [0, n]; mode 0: identity, mode 1: filter
 // table size.  Single workgroup, 1024 threads, chunked with carry.
 __global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k,
-                                                    uint64_t cap, uint32_t* status, uint32_t bit, int slot) {
+                                                    uint64_t cap, uint32_t* status, uint32_t bit, int slot, uint32_t* order) {
     __shared__ uint64_t wsum[16];
     __shared__ uint64_t carry_s;
+    __shared__ uint32_t hist[1024], s_sc[16];
     const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
     if (tid == 0) carry_s = 0;
     __syncthreads();
@@ -4239,6 +4221,7 @@ __global__ __launch_bounds__(1024) void k_excl_scan(const uint32_t* in, uint32_t
             if (cap && tot > cap) atomicOr(status, bit);
         }
     }
+    if (order) read_order_block(n, in, order, hist, s_sc);   // the anchor scan also orders the reads (one launch less)
 }
 
 // per-batch sums for mm2g_batch_counters (st[3] = minimizers, st[4] = anchors in the DP)
@@ -4300,6 +4283,50 @@ __global__ void k_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint
         v_base[v] = rd_off[r] + c0 + 16 * v; v_end[v] = v_base[v] + (ve - c0) + 16;
     }
 }
+// Round 5: the view plan in one single-workgroup launch (C2's 500-read units; was a memset,
+// k_view_count, a scan and k_view_fill), which also does k_mz_base's slots and clears when
+// `base` is given: per-read view counts, their exclusive scan vo, the view table, and
+// v_len = 0 for the views past the real count up to nvmax.
+__global__ __launch_bounds__(1024) void k_view_plan(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, uint64_t nvmax, uint64_t* vo,
+                                                    uint32_t* v_read, uint64_t* v_off, uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from,
+                                                    uint8_t* v_last, uint64_t* v_base, uint64_t* v_end, uint64_t* base, uint64_t* end,
+                                                    ReadOut* zout, unsigned long long* zst, int zst_words) {
+    __shared__ uint32_t s_sc[16];
+    const uint32_t tid = threadIdx.x;
+    if (base) {
+        for (uint32_t r = tid; r <= n; r += 1024) {
+            if (zout) { uint4* o = (uint4*)(zout + r); for (int q = 0; q < (int)(sizeof(ReadOut) / 16); ++q) o[q] = make_uint4(0u, 0u, 0u, 0u); }
+            if (r < n) { base[r] = rd_off[r] + 16ull * r; end[r] = rd_off[r + 1] + 16ull * (r + 1); }
+        }
+        if (zst) for (uint32_t q = tid; q < (uint32_t)zst_words; q += 1024) zst[q] = 0ULL;
+    }
+    auto nview = [&](uint32_t r) -> uint32_t { const uint64_t L = rd_off[r + 1] - rd_off[r]; return L <= V ? 1u : (uint32_t)((L + V - 1) / V); };
+    uint64_t carry = 0;
+    for (uint32_t r0 = 0; r0 < n; r0 += 1024) {
+        const uint32_t r = r0 + tid;
+        const uint32_t c = r < n ? nview(r) : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_sum(c, tot, s_sc);
+        if (r < n) vo[r] = carry + ex;
+        carry += tot;
+    }
+    if (tid == 0) vo[n] = carry;
+    __syncthreads();
+    for (uint32_t r = tid; r < n; r += 1024) {
+        const uint64_t L = rd_off[r + 1] - rd_off[r];
+        const uint32_t nv = nview(r);
+        for (uint32_t j = 0; j < nv; ++j) {
+            const uint64_t v = vo[r] + j;
+            const uint64_t c0 = (uint64_t)j * V, ve = c0 + V < L ? c0 + V : L;
+            const uint64_t vs = j ? (c0 > W0 ? (c0 - W0) & ~7ULL : 0) : 0;
+            v_read[v] = r; v_off[v] = vs; v_len[v] = (uint32_t)(ve - vs); v_pre[v] = (uint32_t)vs;
+            v_from[v] = (uint32_t)(c0 - vs); v_last[v] = ve == L ? 1 : 0;
+            v_base[v] = rd_off[r] + c0 + 16 * v; v_end[v] = v_base[v] + (ve - c0) + 16;
+        }
+    }
+    for (uint64_t v = carry + tid; v < nvmax; v += 1024) v_len[v] = 0;   // views past the real count: empty
+}
+
 // one wave per read: its views' minimizers, in view order, into the read's slot
 // (y + view start << 1: positions are view-relative), clamped and flagged like k_sketch
 __global__ __launch_bounds__(256) void k_view_compact(uint32_t n, const uint64_t* vo, const uint64_t* v_off, const uint64_t* v_base,
@@ -4515,8 +4542,8 @@ int launch_dv(const DvArgs& a, hipStream_t st) {
     return 0;
 }
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k, uint64_t cap, uint32_t* status,
-                     uint32_t bit, int slot, hipStream_t st) {
-    hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(1024), 0, st, in, n, out, mode, q_occ_max, k, cap, status, bit, slot);
+                     uint32_t bit, int slot, hipStream_t st, uint32_t* order) {
+    hipLaunchKernelGGL(k_excl_scan, dim3(1), dim3(1024), 0, st, in, n, out, mode, q_occ_max, k, cap, status, bit, slot, order);
     LAUNCH_CHECK();
     return 0;
 }
@@ -4536,6 +4563,15 @@ int launch_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_view_fill, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, V, W0, vo, v_read, v_off, v_len, v_pre, v_from,
                        v_last, v_base, v_end);
+    LAUNCH_CHECK();
+    return 0;
+}
+int launch_view_plan(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, uint64_t nvmax, uint64_t* vo, uint32_t* v_read,
+                     uint64_t* v_off, uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end,
+                     uint64_t* base, uint64_t* end, mm2g::ReadOut* zout, unsigned long long* zst, int zst_words, hipStream_t st) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_view_plan, dim3(1), dim3(1024), 0, st, n, rd_off, V, W0, nvmax, vo, v_read, v_off, v_len, v_pre, v_from, v_last,
+                       v_base, v_end, base, end, zout, zst, zst_words);
     LAUNCH_CHECK();
     return 0;
 }

@@ -144,8 +144,8 @@ def test_pipeline_parity(dev, small_world, tmp_path):
     assert _map_nodebug(dev, rnames, rseqs)[0] == got          # production path (singleton filter on)
 
 
-@pytest.mark.parametrize("mid_occ,sr,sb,sw", [(None, 3, 4, 0), (20, 3, 4, 1), (5000, 3, 4, 0), (None, 1, 8, 2), (20, 8, 8, 0), (5000, 16, 8, 1)])
-def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ, sr, sb, sw):
+@pytest.mark.parametrize("mid_occ,sr,sb", [(None, 3, 4), (20, 3, 4), (5000, 3, 4), (None, 1, 8), (20, 8, 8), (5000, 16, 8)])
+def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ, sr, sb):
     """The production DP shortcuts keep every f/pprev exact: k_chain_long's
     simple paths (no mark source can break the loop; a chain's maximum visited
     early with a break proven inside the first window) and lazy windows, and
@@ -158,7 +158,7 @@ def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ, sr, sb, sw):
     mid = max(idx.calc_mid_occ(2e-4), 10) if mid_occ is None else mid_occ
     dev.upload_index(idx, mid)
     # sr / sb: speculative rounds of k_chain_long per 64-anchor block and predecessors per step
-    with knobs(dev, lazy=2, giant_min=64, spec_rounds=sr, spec_batch=sb, spec_sweeps=sw):
+    with knobs(dev, lazy=2, giant_min=64, spec_rounds=sr, spec_batch=sb):
         dev.set_debug(True)
         dev.set_reads(rseqs)
         res = dev.map(M.map_opts())

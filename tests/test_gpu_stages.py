@@ -87,7 +87,7 @@ def test_workspace_exact_fallback(small_world, dense_world):
 
 
 @pytest.mark.parametrize("kn", [dict(prune_rescue=0), dict(sketch_view=0), dict(sort_small=1), dict(seg_sparse=0),
-                                dict(spec_rounds=1), dict(spec_batch=8), dict(dv_par=0), dict(spec_sweeps=2, spec_sweep_w=8),
+                                dict(spec_rounds=1), dict(spec_batch=8), dict(dv_par=0), dict(seed_fuse=0, sketch_x32=0),
                                 dict(sort_small=1, spec_rounds=16, sketch_view=300, seg_chunk=128)])
 def test_round4_paths_vs_oracle(dev, small_world, dense_world, kn):
     """Production paths, on and off, against the oracle (PAF and per-read
@@ -108,6 +108,8 @@ def test_sparse_items_taken(dev, small_world, dense_world):
     _production_vs_oracle(dev, small_world, dense_world, tag="sparse")
     c = dev.counters()
     assert c["dp_anchors"] > 0 and c["seg_stream_anchors"] < c["dp_anchors"], c
+    # the batch sums (written by the last chain pass's k_seg_items since round 5)
+    assert c["minimizers"] >= c["kept_minimizers"] > 0 and c["anchors"] >= c["dp_anchors"], c
     with knobs(dev, seg_sparse=0):
         _production_vs_oracle(dev, small_world, dense_world, tag="streamed")
         c = dev.counters()
