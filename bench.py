@@ -101,6 +101,8 @@ def parse(argv=None):
                    help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index")
     p.add_argument("--shares", type=int, default=2,
                    help="units each batch is cut into (0 = one per stream); contexts pull units from one queue")
+    p.add_argument("--min-cnt", type=int, default=3, help="-n (main.rs:45); <= 1 with --min-chain-score <= k: the multi-chain output")
+    p.add_argument("--min-chain-score", type=int, default=40, help="-m (main.rs:48)")
     p.add_argument("--iso-batches", type=int, default=3,
                    help="batches mapped by one context after the timed region for the roofline's quiet-GPU launch times")
     return p.parse_args(argv)
@@ -236,10 +238,12 @@ def spawn_ranks(n: int, argv, backend: str, ndev: int, cmd=None) -> int:
 
 
 def paf_lines_by_read(paf: bytes):
-    """PAF text -> {read name: line} (one line per mapped read)."""
+    """PAF text -> {read name: its lines} (one line per mapped read, SURVEY.md Q4;
+    several, newline-joined in output order, under -n <= 1 -m <= k)."""
     out = {}
     for ln in paf.splitlines():
-        out[ln.split(b"\t", 1)[0].decode()] = ln
+        nm = ln.split(b"\t", 1)[0].decode()
+        out[nm] = out[nm] + b"\n" + ln if nm in out else ln
     return out
 
 
@@ -254,7 +258,10 @@ def kernel_sha() -> str:
 
 
 def bench_config_tag(args) -> str:
-    return f"reads={args.reads},read_len={args.read_len},streams={max(1, args.streams)},shares={args.shares},scale={args.scale},preset={args.preset}"
+    tag = f"reads={args.reads},read_len={args.read_len},streams={max(1, args.streams)},shares={args.shares},scale={args.scale},preset={args.preset}"
+    if (getattr(args, "min_cnt", 3), getattr(args, "min_chain_score", 40)) != (3, 40):
+        tag += f",n={args.min_cnt},m={args.min_chain_score}"
+    return tag
 
 
 def pmc_traffic(kernel: str, hint: str, tag: str):
@@ -535,7 +542,8 @@ def main():
     log(f"rank {rank}: index upload {t_up:.1f}s ({S} contexts share it), mid_occ {mid} "
         f"(device {t_mid_dev * 1e3:.1f} ms, host sort {t_mid_host * 1e3:.0f} ms)")
 
-    opts = M.map_opts()
+    opts = M.map_opts(min_cnt=args.min_cnt, min_chain_score=args.min_chain_score)
+    multi = args.min_cnt <= 1 and args.min_chain_score <= 15   # the -n <= 1 -m <= k multi-chain output (k = 15)
     ih = idx._h
     P = args.shares if args.shares > 0 else S    # units per batch
     cuts = share_cuts(args.reads, P)
@@ -551,7 +559,7 @@ def main():
                 "b": b, "k": k, "lo": lo, "n": nr, "offs": sub,
                 "names": (C.c_char_p * max(nr, 1))(*[f"r{b}_{i}".encode() for i in range(lo, hi)]),
                 "res": (L.ReadResult * max(nr, 1))(),
-                "cap": 256 * nr + (1 << 20), "len": 0, "cnt": None,
+                "cap": (1024 if multi else 256) * nr + (1 << 20), "len": 0, "cnt": None,
             })
             units[-1]["buf"] = C.create_string_buffer(units[-1]["cap"])
 
@@ -565,7 +573,10 @@ def main():
         t.append(time.perf_counter())
         L.check(lib.mm2g_batch_results(h, u["res"], u["n"]), "batch_results")
         t.append(time.perf_counter())
-        u["len"] = L.check(lib.mm2g_format_paf(ih, u["res"], u["names"], u["n"], u["buf"], u["cap"]), "format_paf")
+        if multi:   # the host epilogue's several lines per read (mm2g_batch_paf)
+            u["len"] = L.check(lib.mm2g_batch_paf(h, u["names"], u["n"], u["buf"], u["cap"]), "batch_paf")
+        else:
+            u["len"] = L.check(lib.mm2g_format_paf(ih, u["res"], u["names"], u["n"], u["buf"], u["cap"]), "format_paf")
         t.append(time.perf_counter())
         u["cnt"] = d.counters()
         u["host_ms"] = [(t[i + 1] - t[i]) * 1e3 for i in range(4)]
@@ -639,7 +650,10 @@ def main():
             for _ in range(args.resident_steps):
                 L.check(lib.mm2g_batch_map(d._h, C.byref(opts)), "batch_map")
                 L.check(lib.mm2g_batch_results(d._h, u["res"], u["n"]), "batch_results")
-                L.check(lib.mm2g_format_paf(ih, u["res"], u["names"], u["n"], u["buf"], u["cap"]), "format_paf")
+                if multi:
+                    L.check(lib.mm2g_batch_paf(d._h, u["names"], u["n"], u["buf"], u["cap"]), "batch_paf")
+                else:
+                    L.check(lib.mm2g_format_paf(ih, u["res"], u["names"], u["n"], u["buf"], u["cap"]), "format_paf")
         barrier()
         tr = time.perf_counter()
         ths = [threading.Thread(target=resident_share, args=(d, u)) for d, u in zip(devs, us)]
@@ -798,6 +812,8 @@ def main():
                             f"{args.reads}x{args.read_len // 1000} kb ONT reads per GPU per step, from host RAM "
                             f"(nt4 pack + H2D + map + PAF in the timed region)",
                 "reads_per_gpu_step": args.reads, "read_len": args.read_len, "ref_bases": int(lens.sum()),
+                "chain_opts": f"-n {args.min_cnt} -m {args.min_chain_score}" + (" (multi-chain output: device map with full DP "
+                              "arrays, host backtrack/merge/select, mm2g_batch_paf)" if multi else ""),
                 "distinct_batches": n_batches, "mid_occ": mid,
                 "ranks": world, "distinct_devices": n_gpus,
                 "collective_backend": (dist.get_backend() if world > 1 else None),
@@ -901,9 +917,12 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
         gpu_paf.update(s["paf"])
     seqs = [r[1] for r in reads]
     rnames = [r[0] for r in reads]
-    rec = O.align_records(oi, seqs, mid_occ=mid, threads=thr)
+    rec = O.align_records(oi, seqs, mid_occ=mid, threads=thr, min_cnt=args.min_cnt)
+    multi = args.min_cnt <= 1 and args.min_chain_score <= 15
+    copt = {"min_cnt": args.min_cnt, "min_chain_score": args.min_chain_score}
     diff = []
-    for i in range(len(seqs)):
+    # (per-read records follow the reference's -m 40 best chain; under a non-default -m the PAF lines are the check)
+    for i in range(len(seqs) if args.min_chain_score == 40 else 0):
         g = tuple(int(gpu_res[f][i]) for f in REC_CMP)
         g = (g[0] & 11,) + g[1:]
         w = tuple(int(v) for v in rec[i][:10])
@@ -914,8 +933,8 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
     offs[1:] = np.cumsum([len(x) for x in seqs])
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "cpu.paf")
-        oi.align_buffer(rnames, cat, offs, out, mid_occ=mid, threads=thr)
-        cpu_lines = {ln.split(b"\t", 1)[0].decode(): ln for ln in open(out, "rb").read().splitlines()}
+        oi.align_buffer(rnames, cat, offs, out, mid_occ=mid, threads=thr, **copt)
+        cpu_lines = paf_lines_by_read(open(out, "rb").read())
     paf_same = cpu_lines == gpu_paf
     # paf.rs:178's binary_search as rustc 1.52-1.81 compiles it (the device and the
     # oracle default follow >= 1.82): how many sampled reads would change
@@ -923,8 +942,8 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
     try:
         with tempfile.TemporaryDirectory() as td:
             out = os.path.join(td, "cpu_pre182.paf")
-            oi.align_buffer(rnames, cat, offs, out, mid_occ=mid, threads=thr)
-            pre_lines = {ln.split(b"\t", 1)[0].decode(): ln for ln in open(out, "rb").read().splitlines()}
+            oi.align_buffer(rnames, cat, offs, out, mid_occ=mid, threads=thr, **copt)
+            pre_lines = paf_lines_by_read(open(out, "rb").read())
     finally:
         O.set_binary_search(False)
     bs_diff = sum(1 for k in set(cpu_lines) | set(pre_lines) if cpu_lines.get(k) != pre_lines.get(k))
@@ -932,7 +951,7 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
     parity = {"reads": len(seqs), "ranks_sampled": world, "identical": bool(paf_same and not diff),
               "paf_lines_identical": bool(paf_same), "gpu_lines": len(gpu_paf), "cpu_lines": len(cpu_lines),
               "per_read_outcome_identical": not diff, "per_read_outcome_diffs": diff[:10],
-              "cpu_panics": panics,
+              "cpu_panics": panics, "chain_opts": f"-n {args.min_cnt} -m {args.min_chain_score}" + (" (multi-chain output)" if multi else ""),
               "rustc_binary_search": {"assumed": ">= 1.82 (base/size halving)",
                                       "reads_whose_paf_differs_under_1_52_to_1_81": bs_diff,
                                       "note": "k = 15 is odd: minimizer positions are strictly increasing, so both std "
@@ -943,13 +962,13 @@ def oracle_check(args, names, lens, gbuf, mid, thr, gathered, world):
     if world == 1 and not args.no_cpu:
         # calibrate, then size the sample to ~cpu_seconds per run
         n_cal = min(20, len(seqs))
-        _, _, t_cal = oi.align_buffer(rnames[:n_cal], cat, offs[:n_cal + 1], None, mid_occ=mid, threads=1)
+        _, _, t_cal = oi.align_buffer(rnames[:n_cal], cat, offs[:n_cal + 1], None, mid_occ=mid, threads=1, **copt)
         per_read = max(t_cal / max(n_cal, 1), 1e-4)
         n_s = int(min(len(seqs), max(n_cal, args.cpu_seconds / per_read)))
         bases = int(offs[n_s])
-        t1 = [oi.align_buffer(rnames[:n_s], cat, offs[:n_s + 1], None, mid_occ=mid, threads=1)[2] for _ in range(3)]
+        t1 = [oi.align_buffer(rnames[:n_s], cat, offs[:n_s + 1], None, mid_occ=mid, threads=1, **copt)[2] for _ in range(3)]
         ncpu = affinity_cpus()   # every CPU in the affinity set, not the OMP_NUM_THREADS share
-        tN = [oi.align_buffer(rnames[:n_s], cat, offs[:n_s + 1], None, mid_occ=mid, threads=ncpu)[2] for _ in range(3)]
+        tN = [oi.align_buffer(rnames[:n_s], cat, offs[:n_s + 1], None, mid_occ=mid, threads=ncpu, **copt)[2] for _ in range(3)]
         v1 = bases / statistics.median(t1) / 1e9
         vN = bases / statistics.median(tN) / 1e9
         pf = float(((rec[:n_s, 0] & 8) != 0).sum()) / max(n_s, 1)

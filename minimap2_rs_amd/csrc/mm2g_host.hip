@@ -16,6 +16,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -1409,8 +1410,14 @@ static int multi_epilogue(mm2g_ctx* c) {
     const int32_t kdv = c->dv_separate ? H.k : o.k;
     mm2g::MultiParams P{o.min_cnt, o.min_chain_score, 500, o.max_gap, o.mask_level, o.pri_ratio, o.best_n};
     c->multi.assign(n, mm2g::MultiRead{});
+    // reads are independent: blocks of 64 handed out to the host_threads pool
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
     std::vector<int32_t> mp;
-    for (uint32_t i = 0; i < n; ++i) {
+    for (;;) {
+    const uint32_t b0 = next.fetch_add(64);
+    if (b0 >= n) break;
+    for (uint32_t i = b0; i < std::min(n, b0 + 64); ++i) {
         mm2g_read_result& r = c->h_res[i];
         if (!(r.flags & MM2G_R_MAPPED)) continue;
         const uint64_t a0 = aoff[i], na = aoff[i + 1] - aoff[i];
@@ -1433,6 +1440,13 @@ static int multi_epilogue(mm2g_ctx* c) {
         r.score = M.s1; r.cm = L.cm; r.qs = L.qs; r.qe = L.qe; r.ts = L.ts; r.te = L.te; r.rid = L.rid; r.rev = L.rev;
         r.n_match = L.n_match; r.dv_st = L.dv_st; r.dv_en = L.dv_en; r.dv = L.dv;
     }
+    }
+    };
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(c->knob[MM2G_KNOB_HOST_THREADS], (n + 63) / 64));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
     return 0;
 }
 
