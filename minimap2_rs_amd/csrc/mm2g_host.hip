@@ -1016,7 +1016,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
             if (stg == 2 && ca.lazy && ca.giant_min != 0xffffffffu && ca.P.max_iter <= 5120 && K[MM2G_KNOB_GIANT]) {
                 ProfScope ps(c, pass ? "chain_giant_rescue" : "chain_giant");
                 if (K[MM2G_KNOB_GIANT_LCAP] > 0) ca.giant_lcap = (uint32_t)std::max<int64_t>(16, K[MM2G_KNOB_GIANT_LCAP]) & ~15u;
-                LCHK(launch_chain_stage(7, ca, 256, c->stream));
+                LCHK(launch_chain_stage(7, ca, 0, c->stream));   // workgroups: as many as fit (giant_lcap sets their LDS)
                 // longer segments from a per-workgroup HBM slice (100 kb reads' rescue)
                 const uint32_t gmax = (uint32_t)std::max<int64_t>(0, K[MM2G_KNOB_GIANT_GMAX]) & ~15u;
                 if (gmax) {

@@ -4494,7 +4494,12 @@ static size_t chain_lds(int lut_n) {
     return (size_t)(((lut_n * 2) + 15) & ~15) + (size_t)DP_NW * (RING_WORDS * 4 + RK * 8 + RK * 8);
 }
 static size_t lut_lds(int lut_n) { return (size_t)(((lut_n * 2) + 15) & ~15); }
-static size_t giant_lds(int lut_n) { return lut_lds(lut_n) + (size_t)giant_cap(lut_n) * GIANT_B; }
+// LDS of the LDS variant: the pen LUT plus its segment capacity (giant_lcap, when set, lowers it:
+// smaller workgroups fit twice on a CU, the longer segments going to the HBM variant)
+static size_t giant_lds(int lut_n, uint32_t lcap) {
+    const int cap = lcap ? std::min<int>(giant_cap(lut_n), (int)lcap) : giant_cap(lut_n);
+    return lut_lds(lut_n) + (size_t)cap * GIANT_B;
+}
 static size_t seg_lds(int lut_n) { return lut_lds(lut_n) + (size_t)DP_NW * (KRING * 8 + 3 * TQ * 5 + MEDB * 8); }
 int chain_max_blocks(int lut_n, int which) {
     int dev = 0, ncu = 0, per = 0;
@@ -4528,7 +4533,16 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
     case 5: hipLaunchKernelGGL(k_chain_lb, dim3(blocks), dim3(256), lut_lds(a.P.lut_n), st, a); break;
     case 6: hipLaunchKernelGGL(k_seg_items, dim3(1), dim3(1024), 0, st, a); break;
     case 10: hipLaunchKernelGGL(k_seg_cands, dim3(blocks), dim3(SC_NW * 64), 0, st, a); break;
-    case 7: hipLaunchKernelGGL(k_chain_giant<false>, dim3(blocks), dim3(1024), giant_lds(a.P.lut_n), st, a); break;
+    case 7: {
+        const size_t lds = giant_lds(a.P.lut_n, a.giant_lcap);
+        if (blocks <= 0) {   // as many workgroups as fit on the CUs at once (they take segments from a counter)
+            int dev = 0, ncu = 256;
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+            blocks = std::max(1, ncu) * (int)std::max<size_t>(1, std::min<size_t>(2, (size_t)(158 * 1024) / std::max<size_t>(lds, 1)));
+        }
+        hipLaunchKernelGGL(k_chain_giant<false>, dim3(blocks), dim3(1024), lds, st, a);
+        break;
+    }
     case 8: hipLaunchKernelGGL(k_chain_giant<true>, dim3(blocks), dim3(1024), lut_lds(a.P.lut_n), st, a); break;
     default: hipLaunchKernelGGL(k_chain_fin, dim3((a.n + 3) / 4), dim3(256), 0, st, a); break;
     }
