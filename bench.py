@@ -97,9 +97,9 @@ def parse(argv=None):
                    help="context knob for A/B runs (include/mm2g.h MM2G_KNOB_*), e.g. sort_prof=1")
     p.add_argument("--index-knob", action="append", default=[], metavar="NAME=VALUE",
                    help="process-wide index-build knob (include/mm2g.h MM2G_IKNOB_*), e.g. force_fallback=1")
-    p.add_argument("--streams", type=int, default=6,
+    p.add_argument("--streams", type=int, default=4,
                    help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index "
-                        "(6: round-5 A/B over 4/5/6/8, profiles/r05_ab/c3_contexts_shares_*.txt)")
+                        "(6 is faster over 60 steps, 4 over 10-20: profiles/r05_ab/c3_contexts_*.txt)")
     p.add_argument("--shares", type=int, default=2,
                    help="units each batch is cut into (0 = one per stream); contexts pull units from one queue")
     p.add_argument("--min-cnt", type=int, default=3, help="-n (main.rs:45); <= 1 with --min-chain-score <= k: the multi-chain output")
