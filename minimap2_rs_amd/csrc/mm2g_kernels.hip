@@ -782,6 +782,31 @@ __global__ __launch_bounds__(256) void k_filter_lds(FilterArgs a, int k) {
         return;
     }
     if (!filter_lds_ok(ts, k)) return;
+    const float prod = (float)m * a.q_occ_frac;                       // (m as f32 * q_occ_frac) as usize
+    const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
+    {
+        // Round 5: upper bounds first.  4096 u16 counters (in T's first 8 KB) count the
+        // minimizers per fslot of their hash, an upper bound of every hash's count there
+        // (m <= 2048 here, so no counter overflows).  A minimizer is dropped only when its
+        // count exceeds both q_occ_max and the cutoff; when no counter does, every one is
+        // kept and the exact table is not built (nearly every read: a hash must occur over
+        // max(10, m / 100) times in one read).
+        uint32_t* CM = (uint32_t*)T;
+        for (uint32_t i = threadIdx.x; i < 2048; i += 256) CM[i] = 0u;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += 256) {
+            const uint32_t sl = fslot(a.mz_x[mb + i] >> 8, 4095u);
+            atomicAdd(&CM[sl >> 1], 1u << ((sl & 1u) << 4));
+        }
+        __syncthreads();
+        uint32_t mx = 0;
+        for (uint32_t i = threadIdx.x; i < 2048; i += 256) { const uint32_t v = CM[i]; mx = max(mx, max(v & 0xffffu, v >> 16)); }
+        const uint64_t thr = (uint64_t)a.q_occ_max > cutoff ? (uint64_t)a.q_occ_max : cutoff;
+        if (!__syncthreads_or((uint64_t)mx > thr)) {
+            for (uint32_t i = threadIdx.x; i < m; i += 256) keep[i] = 1;
+            return;
+        }
+    }
     const uint32_t tmask = ts - 1;
     for (uint32_t i = threadIdx.x; i < ts; i += 256) T[i] = 0ULL;
     __syncthreads();
@@ -796,8 +821,6 @@ __global__ __launch_bounds__(256) void k_filter_lds(FilterArgs a, int k) {
         }
     }
     __syncthreads();
-    const float prod = (float)m * a.q_occ_frac;                       // (m as f32 * q_occ_frac) as usize
-    const uint64_t cutoff = prod <= 0.0f ? 0ULL : (uint64_t)prod;
     for (uint32_t i = threadIdx.x; i < m; i += 256) {
         const uint32_t h = (uint32_t)(a.mz_x[mb + i] >> 8);
         uint32_t sl = fslot(h, tmask);

@@ -154,6 +154,26 @@ def test_seed_batch_vs_oracle(dev, small_world, dense_world):
             for r, q in enumerate(rseqs):
                 want, _ = oi.anchors(q, 10, 15, mid)
                 assert np.array_equal(got[r], want), (mid, r, len(got[r]), len(want))
+    # the query filter's drop path (seeds.rs:13-36): tandem repeats whose minimizers recur
+    # more than max(10, m/100) times in a read, beside reads where none does (k_filter_lds
+    # keeps every minimizer without its exact table only when no count can exceed that)
+    rng = random.Random(11)
+    ref, _, _, rseqs = dense_world
+    idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
+    oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
+    dev.upload_index(idx, 5000)
+    unit = _rand_seq(rng, 37, p_low=0.0)
+    qs = [rseqs[1][:3000] + unit * reps + rseqs[2][:3000] for reps in (5, 12, 30, 60)]
+    qs += [unit * 250, _rand_seq(rng, 9000, p_low=0.0) + (b"AC" * 40) * 20]
+    dev.set_reads(qs)
+    got = dev.seed_batch(M.map_opts())
+    dropped = 0
+    for r, q in enumerate(qs):
+        want, _ = oi.anchors(q, 10, 15, 5000)
+        assert np.array_equal(got[r], want), ("repeat", r, len(got[r]), len(want))
+        mv = O.sketch(q, 10, 15)
+        dropped += int(len(mv) - len(O.filter_minimizers(mv))) if mv is not None and len(mv) else 0
+    assert dropped > 0   # the drop path was exercised
     # (w, k) of the opts, not the index's (Q3)
     ref = small_world[0]
     oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
