@@ -348,7 +348,9 @@ enum {
     MM2G_KNOB_SKETCH_X32 = 37,   /* k <= 15: k_sketch keeps the 32-bit hash alone in its LDS window [1]           */
     MM2G_KNOB_BIG_WND = 38,      /* k_sort_big (reads over 65535 anchors): most windows its bucket pass appends
                                     the kept keys to, <= 126; 0 = the per-key scatter to bucket slots [126]   */
-    MM2G_KNOB_COUNT = 39
+    MM2G_KNOB_CANDS_LONGW = 39,  /* k_seg_cands: reads over this many 64-anchor segment-start words are walked
+                                    by a whole workgroup instead of one wave; 0 = never [1024]               */
+    MM2G_KNOB_COUNT = 40
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

@@ -111,6 +111,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SEED_FUSE: return 1;
     case MM2G_KNOB_SKETCH_X32: return 1;
     case MM2G_KNOB_BIG_WND: return 126;
+    case MM2G_KNOB_CANDS_LONGW: return 1024;
     case MM2G_KNOB_HOST_THREADS: return (int64_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     default: return 0;
     }
@@ -944,6 +945,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     ca.seg_chunk = std::max<uint32_t>(64u, (uint32_t)K[MM2G_KNOB_SEG_CHUNK] & ~63u);
     ca.spec_rounds = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(16, K[MM2G_KNOB_SPEC_ROUNDS]));
     ca.spec_batch = K[MM2G_KNOB_SPEC_BATCH] == 8 ? 8u : 4u;
+    ca.cands_longw = K[MM2G_KNOB_CANDS_LONGW] > 0 ? (uint32_t)std::min<int64_t>(K[MM2G_KNOB_CANDS_LONGW], 0x7fffffff) : 0x7fffffffu;
     // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
     // settle in a few no-break policy-iteration rounds.  Pass 0's long segments
     // are real chains whose windows carry many mark sources: k_chain_long is
@@ -993,7 +995,10 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
             if (ca.isob) {   // candidate segments per read; k_chain_seg streams only the reads left over
                 ca.sq = sq; ca.sq_cap = sq_cap;
                 ProfScope ps(c, pass ? "chain_cands_rescue" : "chain_cands");
-                LCHK(launch_chain_stage(10, ca, (int)std::min<uint32_t>((n + 15) / 16, 1024), c->stream));
+                // one workgroup per 16 reads; with long reads (over ~64 kb) also one per read (up to
+                // 1024), since each such read takes a whole workgroup
+                const uint32_t cb = std::max<uint32_t>((n + 15) / 16, c->max_read_len >= 65536 ? n : 0u);
+                LCHK(launch_chain_stage(10, ca, (int)std::min<uint32_t>(cb, 1024), c->stream));
             }
         }
         ca.lseg_prof = K[MM2G_KNOB_LSEG_PROF] ? 1u : 0u;

@@ -224,6 +224,7 @@ struct ChainArgs {
     void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
     uint32_t spec_rounds = 3; // k_chain_long: speculative rounds per 64-anchor block (MM2G_KNOB_SPEC_ROUNDS)
     uint32_t spec_batch = 4;  // k_chain_long: predecessors per step of a speculative round, 4 or 8 (MM2G_KNOB_SPEC_BATCH)
+    uint32_t cands_longw = 1024;         // k_seg_cands: reads over this many segment-start words take a whole workgroup
     const uint32_t* mz_cnt = nullptr;    // with bsum: k_seg_items writes bsum[3] = sum mz_cnt, bsum[4] = sum cnt2
     unsigned long long* bsum = nullptr;
     int32_t est_lane = 0;    // k_chain_seg (production): estimated DP pairs up to which a segment takes one lane

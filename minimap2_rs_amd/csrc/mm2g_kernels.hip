@@ -2824,7 +2824,9 @@ __global__ __launch_bounds__(SC_NW * 64) void k_seg_cands(ChainArgs a) {
             const uint64_t base = uni64(a.a_off[r]);
             const bool on = a.P.pass == 0 || (uni(a.out[r].flags) & RF_RESCUED);   // the rescue pass maps rescued reads only
             const uint64_t t0 = wall_clock64();
-            if (A > 0 && on && fm <= CHAIN_TINY * span) {
+            if (((A + 63) >> 6) > (int32_t)a.cands_longw) {
+                // a long read (100 kb): the whole workgroup walks it below
+            } else if (A > 0 && on && fm <= CHAIN_TINY * span) {
                 nit = (uint32_t)((A + (int32_t)a.seg_chunk - 1) / (int32_t)a.seg_chunk);
             } else if (A > 0 && on) {
                 const int32_t Lmin = (fm + span - 1) / span;
@@ -2922,6 +2924,103 @@ __global__ __launch_bounds__(SC_NW * 64) void k_seg_cands(ChainArgs a) {
         for (uint32_t k = (uint32_t)lane; k < myi; k += 64)
             if (oi + k < a.sq_cap) a.sq[oi + k] = make_uint2(rr, k);
         __syncthreads();                                     // s_buf / s_cnt are reused by the next round
+    }
+    // Long reads (over cands_longw words: C5's 100 kb reads, 3 k words), one workgroup each: the
+    // read's words split over all 16 waves (K words per lane), the first start after a lane's
+    // words is a suffix minimum over the lanes and then the waves; pass B as above, into every
+    // wave's buffer with the read's index (one wave per such read used a quarter of the GPU)
+    __shared__ int32_t s_wfirst[SC_NW], s_wml[SC_NW];
+    for (uint32_t r = blockIdx.x; r < a.n; r += gridDim.x) {
+        const int32_t A = (int32_t)uni((int32_t)a.cnt2[r]);
+        const int32_t nwd = (A + 63) >> 6;
+        if (nwd <= (int32_t)a.cands_longw) continue;         // (workgroup-uniform)
+        const bool on = a.P.pass == 0 || (uni(a.out[r].flags) & RF_RESCUED);
+        if (!on) continue;
+        const int32_t fm = uni(a.fmin[r]);
+        const uint64_t base = uni64(a.a_off[r]);
+        const uint64_t t0 = wall_clock64();
+        if (lane == 0) { s_cnt[wv] = 0; s_nit[wv] = 0; s_rd[wv] = r; }
+        __syncthreads();
+        int32_t mx = 0;
+        if (fm <= CHAIN_TINY * span) {
+            if (threadIdx.x == 0) s_nit[0] = (uint32_t)((A + (int32_t)a.seg_chunk - 1) / (int32_t)a.seg_chunk);
+        } else {
+            const int32_t Lmin = (fm + span - 1) / span;
+            const uint64_t* isw = a.isob + (base >> 6) + r;
+            const int32_t gl = wv * 64 + lane;                   // lane of the workgroup
+            const int32_t K = (nwd + SC_NW * 64 - 1) / (SC_NW * 64);
+            const int32_t w0 = min(nwd, gl * K), w1 = min(nwd, w0 + K);
+            int32_t first = INT_MAX;
+            for (int32_t w = w0; w < w1 && first == INT_MAX; ++w) { const uint64_t m = isw[w]; if (m) first = w * 64 + ctz64(m); }
+            int32_t sfx = first;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) { const int32_t o = __shfl_down(sfx, d, 64); if (lane + d < 64) sfx = min(sfx, o); }
+            if (lane == 0) s_wfirst[wv] = sfx;
+            __syncthreads();
+            int32_t later = A;                                   // first start of the later waves
+            for (int t = wv + 1; t < SC_NW; ++t) later = min(later, s_wfirst[t]);
+            int32_t after = __shfl_down(sfx, 1, 64);
+            after = lane == 63 ? later : min(after, later);
+            after = min(after, A);
+            auto push = [&](int32_t sl, int32_t el) {
+                const uint32_t k = atomicAdd(&s_cnt[wv], 1u);
+                if (k < (uint32_t)SC_BUF) s_buf[wv][k] = make_uint2((uint32_t)sl, (uint32_t)el);
+                else {
+                    const uint32_t q = atomicAdd(a.lseg_n, 1u);
+                    if (q < a.lseg_cap) a.lseg[q] = make_uint4(r, (uint32_t)sl, (uint32_t)el, 0u);
+                }
+                mx = max(mx, el - sl);
+            };
+            for (int32_t w = w1 - 1; w >= w0; --w) {
+                const uint64_t m = isw[w];
+                if (!m) continue;
+                if (Lmin >= 64) {
+                    const int32_t sl = w * 64 + 63 - clz64(m);
+                    if (after - sl >= Lmin) push(sl, after);
+                } else {
+                    uint64_t mm = m;
+                    int32_t e = after;
+                    while (mm) {
+                        const int b = 63 - clz64(mm);
+                        mm &= ~(1ULL << b);
+                        const int32_t sl = w * 64 + b;
+                        if (e - sl >= Lmin) push(sl, e);
+                        e = sl;
+                    }
+                }
+                after = w * 64 + ctz64(m);
+            }
+        }
+        const int32_t wml = rdl(scan_max(mx), 63);
+        if (lane == 0) s_wml[wv] = wml;                      // (not s_wfirst: other waves may still read it)
+        __syncthreads();
+        if (threadIdx.x == 0 && fm > CHAIN_TINY * span) {
+            int32_t ml = 0; uint32_t ncs = 0;
+            for (int t = 0; t < SC_NW; ++t) { ml = max(ml, s_wml[t]); ncs += s_cnt[t]; }
+            ReadOut* O = a.out + r;
+            O->t_pass[a.P.pass] = (uint32_t)(wall_clock64() - t0);
+            const uint32_t st6 = (uint32_t)(ml > 65535 ? 65535 : ml) | ((ncs > 65535 ? 65535u : ncs) << 16);
+            if (a.P.pass == 0) O->pad2 = st6; else O->n_deep = st6;
+        }
+        if (lane == 0) s_cnt[wv] = min(s_cnt[wv], (uint32_t)SC_BUF);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tc = 0, ti = 0;
+            for (int w = 0; w < SC_NW; ++w) { tc += s_cnt[w]; ti += s_nit[w]; }
+            s_base[0] = tc ? atomicAdd(a.lseg_n, tc) : 0u;
+            s_base[1] = ti ? atomicAdd(a.sq_n, ti) : 0u;
+        }
+        __syncthreads();
+        uint32_t oc = s_base[0], oi = s_base[1];
+        for (int w = 0; w < wv; ++w) { oc += s_cnt[w]; oi += s_nit[w]; }
+        const uint32_t myc = s_cnt[wv], myi = s_nit[wv];
+        for (uint32_t k = (uint32_t)lane; k < myc; k += 64) {
+            const uint2 e = s_buf[wv][k];
+            if (oc + k < a.lseg_cap) a.lseg[oc + k] = make_uint4(r, e.x, e.y, 0u);
+        }
+        for (uint32_t k = (uint32_t)lane; k < myi; k += 64)
+            if (oi + k < a.sq_cap) a.sq[oi + k] = make_uint2(r, k);
+        __syncthreads();
     }
 }
 

@@ -166,8 +166,9 @@ def test_c5_hg38_100kb(hg38, tmp_path):
                 assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
     # production defaults (the rescue pass pruned by pass 0's bound): PAF and per-read outcome
     _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5prune")
-    # pass 0's 100 kb chains with more speculative rounds per block, 8 predecessors per step
-    with knobs(dev, spec_rounds=8, spec_batch=8):
+    # pass 0's 100 kb chains with more speculative rounds per block, 8 predecessors per step,
+    # and the long reads' candidate segments found by one wave each (cands_longw=0)
+    with knobs(dev, spec_rounds=8, spec_batch=8, cands_longw=0):
         _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5sr8")
 
 
