@@ -1332,6 +1332,8 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
                   out, c->keys.cap / 8, D.y.cap / 4};
         da.abort = st32;
         da.strict = (H.k & 1) && c->knob[MM2G_KNOB_DV_PAR] ? 1u : 0u;   // odd k: positions strictly increase
+        // reads whose dv sketch outgrows k_dv's 4096 staged positions (~2 per w+1 bases): a workgroup each
+        da.long_m = da.strict && 2ull * c->max_read_len / (uint64_t)(H.w + 1) + 64 > 4096 ? 0xffffffffu : 0u;
         ProfScope ps(c, "dv");
         if (stop_at != 4) LCHK(launch_dv(da, c->stream));
     }

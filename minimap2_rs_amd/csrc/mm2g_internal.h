@@ -253,6 +253,7 @@ struct DvArgs {
     uint64_t cap_keys, cap_mz;
     const uint32_t* abort = nullptr;
     uint32_t strict = 0;      // the dv sketch's k is odd: its minimizer positions strictly increase (parallel match)
+    uint32_t long_m = 0;      // strict: reads with more minimizers than k_dv stages (<= long_m) go to k_dv_long (0 = none)
 };
 
 }  // namespace mm2g

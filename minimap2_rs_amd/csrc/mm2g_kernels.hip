@@ -4233,6 +4233,7 @@ __global__ __launch_bounds__(64) void k_dv(DvArgs a) {
         for (uint32_t j0 = 0; j0 < m; j0 += 64) { const uint32_t j = j0 + lane; if (j < m) Ps[j] = (int32_t)(Y[j] >> 1); }
         __syncthreads();
     }
+    if (a.strict && !in_lds && m <= a.long_m) return;   // k_dv_long (a workgroup per read)
     auto mpos = [&](uint32_t j) -> int32_t { return in_lds ? Ps[j] : (int32_t)(Y[CK(j, m)] >> 1); };
     // t-th chain anchor in forward-query order (paf.rs:165-176)
     auto fwdq = [&](int32_t t) -> int32_t {
@@ -4300,6 +4301,79 @@ __global__ __launch_bounds__(64) void k_dv(DvArgs a) {
         ReadOut* O = a.out + r;
         O->m_dv = (int32_t)m;
         O->flags = flags | RF_DV_FOUND; O->n_match = n_match; O->dv_st = (int32_t)st; O->dv_en = (int32_t)en;
+    }
+}
+
+// Round 5: k_dv's strict match (odd k) for reads with more minimizers than one wave stages
+// (C5's 100 kb reads: ~18 k): a workgroup per read, the positions in LDS, and every chain
+// anchor's lower-bound search in parallel over 1024 lanes; the first anchor P lacks ends the
+// matches (its index is a workgroup minimum).  Same results as k_dv (paf.rs:156-199).
+constexpr uint32_t DV_LONG = 32768;   // positions staged (128 KB of LDS)
+__global__ __launch_bounds__(1024) void k_dv_long(DvArgs a) {
+    if (a.abort && (*a.abort & BS_ANCHORS)) return;
+    extern __shared__ int32_t Pl[];
+    __shared__ uint32_t s_miss, s_st, s_ok;
+    __shared__ int32_t s_en;
+    const int tid = threadIdx.x;
+    for (uint32_t r = blockIdx.x; r < a.n; r += gridDim.x) {
+        const uint32_t m = a.mz_cnt[r];
+        if (m <= (uint32_t)DV_LDS || m > a.long_m) continue;          // (k_dv's reads)
+        const int32_t flags = a.out[r].flags, cm = a.out[r].cm;
+        if (!((flags & RF_MAPPED) && !(flags & RF_PANIC) && cm > 0)) continue;   // k_dv wrote these
+        const uint64_t mzb = a.mz_base[r], ab = a.a_off[r];
+        const uint64_t An = a.a_off[r + 1] - ab;
+        const uint32_t* Y = a.mz_y + mzb;
+        const uint32_t* CB = a.chain + ab;
+        const uint64_t* K = a.keys + ab;
+        const uint64_t qmask = (1ULL << a.kl.qb) - 1;
+        const bool rev = (uint32_t)a.out[r].group >= a.kl.n_seq;
+        const int32_t qlen = a.out[r].qlen, span = a.span;
+        auto fwdq = [&](int32_t t) -> int32_t {
+            if (!rev) return (int32_t)(K[CK(CB[cm - 1 - t], An)] & qmask);
+            const int32_t q = (int32_t)(K[CK(CB[t], An)] & qmask);
+            return qlen - 1 - (q + 1 - span);
+        };
+        for (uint32_t j = tid; j < m; j += 1024) Pl[j] = (int32_t)(Y[CK(j, m)] >> 1);
+        if (tid == 0) s_miss = (uint32_t)cm;
+        __syncthreads();
+        if (tid == 0) {   // Rust >= 1.82 slice::binary_search of the first chain position (paf.rs:178)
+            const int32_t first = fwdq(0);
+            uint32_t size = m, b = 0;
+            while (size > 1) { const uint32_t half = size / 2, mid = b + half; if (!(Pl[mid] > first)) b = mid; size -= half; }
+            s_ok = Pl[b] == first ? 1u : 0u;
+            uint32_t st = b;
+            while (st > 0 && Pl[st - 1] == first) --st;
+            s_st = st;
+            s_en = (int32_t)st;
+        }
+        __syncthreads();
+        if (s_ok) {
+            // chain anchor t >= 1: its lower bound in P; the first miss ends the matches
+            for (int32_t t = 1 + tid; t < cm; t += 1024) {
+                const int32_t v = fwdq(t);
+                uint32_t b0 = 0, sz = m;
+                while (sz > 1) { const uint32_t half = sz / 2; if (Pl[b0 + half] < v) b0 += half; sz -= half; }
+                const uint32_t ix = b0 + (Pl[b0] < v ? 1u : 0u);
+                if (!(ix < m && Pl[ix < m ? ix : 0] == v)) atomicMin(&s_miss, (uint32_t)t);
+            }
+            __syncthreads();
+            const uint32_t tm = s_miss;                                   // matches: anchors 0 .. tm-1
+            if (tm > 1 && (int32_t)(tm - 1) % 1024 == tid) {             // en = the last match's position
+                const int32_t v = fwdq((int32_t)tm - 1);
+                uint32_t b0 = 0, sz = m;
+                while (sz > 1) { const uint32_t half = sz / 2; if (Pl[b0 + half] < v) b0 += half; sz -= half; }
+                s_en = (int32_t)(b0 + (Pl[b0] < v ? 1u : 0u));
+            }
+            __syncthreads();
+            if (tid == 0) {
+                ReadOut* O = a.out + r;
+                O->m_dv = (int32_t)m;
+                O->flags = flags | RF_DV_FOUND; O->n_match = (int32_t)tm; O->dv_st = (int32_t)s_st; O->dv_en = s_en;
+            }
+        } else if (tid == 0) {
+            a.out[r].m_dv = (int32_t)m; a.out[r].flags = flags & ~RF_DV_FOUND;
+        }
+        __syncthreads();
     }
 }
 
@@ -4673,8 +4747,16 @@ int launch_chain_stage(int stage, const ChainArgs& a, int blocks, hipStream_t st
 }
 int launch_dv(const DvArgs& a, hipStream_t st) {
     if (a.n == 0) return 0;
-    hipLaunchKernelGGL(k_dv, dim3(a.n), dim3(64), 0, st, a);
+    DvArgs b = a;
+    b.long_m = a.strict ? std::min<uint32_t>(a.long_m, DV_LONG) : 0u;   // both kernels see the same split
+    hipLaunchKernelGGL(k_dv, dim3(a.n), dim3(64), 0, st, b);
     LAUNCH_CHECK();
+    if (b.long_m) {   // reads over DV_LDS minimizers (the host sets long_m only when some may be)
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        hipLaunchKernelGGL(k_dv_long, dim3(std::min<uint32_t>(a.n, (uint32_t)std::max(ncu, 1))), dim3(1024), (size_t)b.long_m * 4, st, b);
+        LAUNCH_CHECK();
+    }
     return 0;
 }
 int launch_excl_scan(const uint32_t* in, uint32_t n, uint64_t* out, int mode, int q_occ_max, int k, uint64_t cap, uint32_t* status,
