@@ -151,7 +151,7 @@ struct SeedArgs {
 };
 // seed_write splits each read's minimizers into this many contiguous parts
 // (whole 64-minimizer chunks), one wave each; seed_count records where they start
-constexpr int SEED_PARTS = 4;
+constexpr int SEED_PARTS = 16;   // (round 5: 4 -> 16; C5's 1,000-read units then give 16 k waves instead of 4 k)
 // per-read anchor sort + singleton filter (k_sort_small / k_sort_read)
 constexpr int32_t SEG_CHUNK = 4096;     // anchors per work item of the streaming chain kernels
 constexpr uint32_t SEG_THREAD = 1024;   // cell segments up to this length: one thread per anchor (default seg_small)
