@@ -839,27 +839,33 @@ __global__ __launch_bounds__(256) void k_filter_lds(FilterArgs a, int k) {
 // 3. LOOKUP + ANCHORS — Index::get (src/index.rs:143-154), the mid_occ skip of
 // build_anchors_filtered (src/seeds.rs:42-57) and push_anchor (seeds.rs:62-79).
 // ============================================================================
-__global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
+// One workgroup per read, one wave per part: parts are the same runs of whole 64-minimizer
+// chunks k_seed_write takes (round 5; one wave per read left most of the GPU idle on C5's
+// 1,000-read units).  The part totals give the read's count and k_seed_write's part starts.
+__global__ __launch_bounds__(SEED_PARTS * 64) void k_seed_count(SeedArgs a) {
+    static_assert(SEED_PARTS == 16, "a wave per part, 16 per workgroup");
+    __shared__ uint32_t s_tot[SEED_PARTS], s_kept[SEED_PARTS];
     const int lane = lane_id();
-    const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
     const uint32_t cmask = (1u << a.log2cap) - 1;
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wave_id(); r < a.n; r += nwaves) {
+    for (uint32_t r = blockIdx.x; r < a.n; r += gridDim.x) {
+        const uint32_t part = (uint32_t)wave_id();
         const uint64_t mb = uni64(a.mz_base[r]);
         const uint32_t m = (uint32_t)uni((int32_t)a.mz_cnt[r]);
         const uint32_t nch = (m + 63) >> 6;
+        const uint32_t cb = (nch * part) / SEED_PARTS, ce = (nch * (part + 1)) / SEED_PARTS;
+        const uint32_t iend = ce * 64 < m ? ce * 64 : m;
         uint32_t acc = 0, kept = 0;
-        int kn = 1;                        // next seed_write part boundary
         // SC_U chunks of 64 minimizers at a time: their table probes are
         // independent, so SC_U loads per lane are in flight together
         constexpr int SC_U = 4;
-        for (uint32_t b0 = 0; b0 < m; b0 += 64 * SC_U) {
+        for (uint32_t b0 = cb * 64; b0 < iend; b0 += 64 * SC_U) {
             uint64_t h[SC_U];
             uint32_t sl[SC_U], n[SC_U], off[SC_U];
             bool done[SC_U];
 #pragma unroll
             for (int u = 0; u < SC_U; ++u) {
                 const uint32_t i = b0 + (uint32_t)u * 64 + lane;
-                const bool act = i < m;
+                const bool act = i < iend;
                 done[u] = !(act && a.keep[mb + i]);
                 kept += done[u] ? 0u : 1u;
                 h[u] = act ? (a.mz_x[mb + i] >> 8) : 0;
@@ -881,25 +887,27 @@ __global__ __launch_bounds__(256) void k_seed_count(SeedArgs a) {
             }
 #pragma unroll
             for (int u = 0; u < SC_U; ++u) {
-                const uint32_t c = (b0 >> 6) + (uint32_t)u;
-                if (c >= nch) break;
-                while (kn < SEED_PARTS && c == (nch * (uint32_t)kn) / SEED_PARTS) {
-                    const uint32_t sofar = wave_sum(acc);
-                    if (lane == 0) a.a_part[(uint64_t)r * (SEED_PARTS - 1) + kn - 1] = sofar;
-                    ++kn;
-                }
                 const uint32_t i = b0 + (uint32_t)u * 64 + lane;
                 // mz_n: the anchor count, or IX_INLINE | position high word for a Single
                 uint32_t nn = n[u];
                 if (!(nn & IX_INLINE) && nn > 1 && (int64_t)nn > (int64_t)a.mid_occ) nn = 0;   // Multi with len > mid_occ: skip
-                if (i < m) { a.mz_n[mb + i] = nn; a.mz_poff[mb + i] = off[u]; }
+                if (i < iend) { a.mz_n[mb + i] = nn; a.mz_poff[mb + i] = off[u]; }
                 acc += ix_count(nn);
             }
         }
         acc = wave_sum(acc);
         kept = wave_sum(kept);
-        for (; kn < SEED_PARTS; ++kn) if (lane == 0) a.a_part[(uint64_t)r * (SEED_PARTS - 1) + kn - 1] = acc;
-        if (lane == 0) { a.a_cnt[r] = acc; a.out[r].m_kept = (int32_t)kept; }
+        if (lane == 0) { s_tot[part] = acc; s_kept[part] = kept; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0, kt = 0;
+            for (int q = 0; q < SEED_PARTS; ++q) {
+                if (q) a.a_part[(uint64_t)r * (SEED_PARTS - 1) + q - 1] = run;
+                run += s_tot[q]; kt += s_kept[q];
+            }
+            a.a_cnt[r] = run; a.out[r].m_kept = (int32_t)kt;
+        }
+        __syncthreads();                                       // s_tot is reused by the next read
     }
 }
 
@@ -4630,7 +4638,9 @@ int launch_filter(const FilterArgs& a, int k, int n_blocks, hipStream_t st) {
     return 0;
 }
 int launch_seed_count(const SeedArgs& a, int n_blocks, hipStream_t st) {
-    hipLaunchKernelGGL(k_seed_count, dim3(n_blocks), dim3(256), 0, st, a);
+    (void)n_blocks;
+    if (a.n == 0) return 0;
+    hipLaunchKernelGGL(k_seed_count, dim3(std::min<uint32_t>(a.n, 16384)), dim3(SEED_PARTS * 64), 0, st, a);
     LAUNCH_CHECK();
     return 0;
 }
