@@ -87,7 +87,7 @@ struct SketchBufs {
     uint64_t cap = 0;      // minimizer slots allocated
 };
 // query sketch views (run_sketch): the view table, per-view slots, per-read view offsets
-struct ViewBufs { DevBuf read, len, pre, from, cnt, need, off, base, end, last, nvr, vo, x, y; };
+struct ViewBufs { DevBuf read, len, pre, from, cnt, need, off, base, end, last, vo, x, y; };
 
 static int64_t knob_default(int k) {
     switch (k) {
@@ -783,17 +783,16 @@ static int run_sketch(mm2g_ctx* c, int w, int k, SketchBufs& B, int32_t* ovf, Re
     if (views) {
         const uint32_t W0 = (uint32_t)((2 * (w + k) + 64 + 7) & ~7);
         const uint64_t nvmax = (uint64_t)n + c->total_bases / V + 1;
-        uint32_t *v_read, *v_len, *v_pre, *v_from, *v_cnt, *v_need, *nvr; uint64_t *v_off, *v_base, *v_end, *vo, *vx; uint8_t* v_last; uint32_t* vy;
+        uint32_t *v_read, *v_len, *v_pre, *v_from, *v_cnt, *v_need; uint64_t *v_off, *v_base, *v_end, *vo, *vx; uint8_t* v_last; uint32_t* vy;
         ViewBufs& Vb = c->vw;
         ENSURE(Vb.read, uint32_t, nvmax, v_read); ENSURE(Vb.len, uint32_t, nvmax, v_len); ENSURE(Vb.pre, uint32_t, nvmax, v_pre);
         ENSURE(Vb.from, uint32_t, nvmax, v_from); ENSURE(Vb.cnt, uint32_t, nvmax, v_cnt); ENSURE(Vb.need, uint32_t, nvmax, v_need);
         ENSURE(Vb.off, uint64_t, nvmax, v_off); ENSURE(Vb.base, uint64_t, nvmax, v_base); ENSURE(Vb.end, uint64_t, nvmax, v_end);
-        ENSURE(Vb.last, uint8_t, nvmax, v_last); ENSURE(Vb.nvr, uint32_t, n + 1, nvr); ENSURE(Vb.vo, uint64_t, n + 1, vo);
+        ENSURE(Vb.last, uint8_t, nvmax, v_last); ENSURE(Vb.vo, uint64_t, n + 1, vo);
         const uint64_t vcap = c->total_bases + 16 * nvmax + 16;
         ENSURE(Vb.x, uint64_t, vcap, vx); ENSURE(Vb.y, uint32_t, vcap, vy);
         {
             ProfScope ps(c, "sketch_views");
-            (void)nvr;
             LCHK(launch_view_plan(n, c->d_rd_off, V, W0, nvmax, vo, v_read, v_off, v_len, v_pre, v_from, v_last, v_base, v_end,
                                   B.exact ? nullptr : base, end, zout, zst, STAT_WORDS, c->stream));
         }

@@ -288,11 +288,8 @@ int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, 
 // (zout / zst: also zero out[0, n] and zst[0, zst_words) -- the map's first kernel)
 int launch_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, uint64_t* end, uint32_t slot, hipStream_t st,
                    mm2g::ReadOut* zout = nullptr, unsigned long long* zst = nullptr, int zst_words = 0);
-// query sketch views: per-read view counts; view table from their exclusive scan vo; per-read concatenation
-int launch_view_count(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t* nv, hipStream_t st);
-int launch_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, const uint64_t* vo, uint32_t* v_read, uint64_t* v_off,
-                     uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end, hipStream_t st);
-// the same view table in one single-workgroup launch, plus launch_mz_base's work when base is given
+// query sketch views: the view table (per-read view counts, their exclusive scan vo, the views) in one
+// single-workgroup launch, plus launch_mz_base's work when base is given; per-read concatenation
 int launch_view_plan(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, uint64_t nvmax, uint64_t* vo, uint32_t* v_read,
                      uint64_t* v_off, uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end,
                      uint64_t* base, uint64_t* end, mm2g::ReadOut* zout, unsigned long long* zst, int zst_words, hipStream_t st);

@@ -4329,7 +4329,7 @@ __global__ __launch_bounds__(1024) void k_dv_long(DvArgs a) {
         const int32_t flags = a.out[r].flags, cm = a.out[r].cm;
         if (!((flags & RF_MAPPED) && !(flags & RF_PANIC) && cm > 0)) continue;   // k_dv wrote these
         const uint64_t mzb = a.mz_base[r], ab = a.a_off[r];
-        const uint64_t An = a.a_off[r + 1] - ab;
+        [[maybe_unused]] const uint64_t An = a.a_off[r + 1] - ab;   // (CK's bound in checked builds)
         const uint32_t* Y = a.mz_y + mzb;
         const uint32_t* CB = a.chain + ab;
         const uint64_t* K = a.keys + ab;
@@ -4462,35 +4462,12 @@ __global__ void k_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, ui
 // >= W0 bases (W0 = 2(w+k)+64 rounded up to 8: enough for odd k, DESIGN.md
 // §10), one wave per view, so a 10 kb read is not 20 sequential tiles of one
 // wave.  View outputs go to their own slots and are concatenated per read.
-__global__ void k_view_count(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t* nv) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
-    const uint64_t L = rd_off[r + 1] - rd_off[r];
-    nv[r] = L <= V ? 1u : (uint32_t)((L + V - 1) / V);
-}
-// view v = vo[r] + j of read r: emitting [jV, min(L, (j+1)V)), starting W0 (or
-// more, to a multiple of 8) bases earlier; its output slot is [rd_off[r] + jV +
-// 16 v, + emitting bases + 16), disjoint across all views
-__global__ void k_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, const uint64_t* vo, uint32_t* v_read,
-                            uint64_t* v_off, uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base,
-                            uint64_t* v_end) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
-    const uint64_t L = rd_off[r + 1] - rd_off[r];
-    const uint32_t nv = L <= V ? 1u : (uint32_t)((L + V - 1) / V);
-    for (uint32_t j = 0; j < nv; ++j) {
-        const uint64_t v = vo[r] + j;
-        const uint64_t c0 = (uint64_t)j * V, ve = c0 + V < L ? c0 + V : L;
-        const uint64_t vs = j ? (c0 > W0 ? (c0 - W0) & ~7ULL : 0) : 0;
-        v_read[v] = r; v_off[v] = vs; v_len[v] = (uint32_t)(ve - vs); v_pre[v] = (uint32_t)vs;
-        v_from[v] = (uint32_t)(c0 - vs); v_last[v] = ve == L ? 1 : 0;
-        v_base[v] = rd_off[r] + c0 + 16 * v; v_end[v] = v_base[v] + (ve - c0) + 16;
-    }
-}
-// Round 5: the view plan in one single-workgroup launch (C2's 500-read units; was a memset,
-// k_view_count, a scan and k_view_fill), which also does k_mz_base's slots and clears when
+// The view plan in one single-workgroup launch (C2's 500-read units; round 4 used four
+// launches: a memset, a count, a scan and a fill), which also does k_mz_base's slots and clears when
 // `base` is given: per-read view counts, their exclusive scan vo, the view table, and
-// v_len = 0 for the views past the real count up to nvmax.
+// v_len = 0 for the views past the real count up to nvmax.  View v = vo[r] + j of read r
+// emits [jV, min(L, (j+1)V)), starting W0 (or more, to a multiple of 8) bases earlier; its
+// output slot is [rd_off[r] + jV + 16v, + emitting bases + 16), disjoint across all views.
 __global__ __launch_bounds__(1024) void k_view_plan(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, uint64_t nvmax, uint64_t* vo,
                                                     uint32_t* v_read, uint64_t* v_off, uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from,
                                                     uint8_t* v_last, uint64_t* v_base, uint64_t* v_end, uint64_t* base, uint64_t* end,
@@ -4531,28 +4508,53 @@ __global__ __launch_bounds__(1024) void k_view_plan(uint32_t n, const uint64_t* 
     for (uint64_t v = carry + tid; v < nvmax; v += 1024) v_len[v] = 0;   // views past the real count: empty
 }
 
-// one wave per read: its views' minimizers, in view order, into the read's slot
-// (y + view start << 1: positions are view-relative), clamped and flagged like k_sketch
-__global__ __launch_bounds__(256) void k_view_compact(uint32_t n, const uint64_t* vo, const uint64_t* v_off, const uint64_t* v_base,
-                                                      const uint32_t* v_cnt, const uint32_t* v_need, const uint64_t* vx, const uint32_t* vy,
-                                                      const uint64_t* base, const uint64_t* end, uint64_t* x, uint32_t* y,
+// a workgroup per read: its views' minimizers, in view order, into the read's slot
+// (y + view start << 1: positions are view-relative), clamped and flagged like k_sketch.
+// Wave w copies views w, w + 4, ... at their offsets (a wave scan of the view counts,
+// 64 views at a time), 4 entries per lane in flight: round 4's one wave per read copied
+// a 100 kb read's ~18 k minimizers one dependent 64-entry step at a time.
+__global__ __launch_bounds__(256) void k_view_compact(uint32_t n, const uint64_t* __restrict__ vo, const uint64_t* __restrict__ v_off,
+                                                      const uint64_t* __restrict__ v_base, const uint32_t* __restrict__ v_cnt,
+                                                      const uint32_t* __restrict__ v_need, const uint64_t* __restrict__ vx,
+                                                      const uint32_t* __restrict__ vy, const uint64_t* __restrict__ base,
+                                                      const uint64_t* __restrict__ end, uint64_t* __restrict__ x, uint32_t* __restrict__ y,
                                                       uint32_t* cnt, uint32_t* need, int32_t* overflow) {
-    const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    constexpr int CU = 4;
+    const uint32_t r = blockIdx.x;
     if (r >= n) return;
-    const int lane = lane_id();
+    const int lane = lane_id(), wv = wave_id();
     const uint64_t b = base[r], capn = end[r] - b;
-    uint64_t o = 0, tn = 0;   // copied so far; the views' true (unclamped) counts
-    for (uint64_t v = vo[r]; v < vo[r + 1]; ++v) {
-        const uint64_t vb = v_base[v];
-        const uint32_t c = v_cnt[v];
-        const uint32_t add = (uint32_t)(v_off[v] << 1);
-        for (uint32_t i = lane; i < c; i += 64) {
-            if (o + i < capn) { x[b + o + i] = vx[vb + i]; y[b + o + i] = vy[vb + i] + add; }
+    const uint64_t v0 = vo[r], v1 = vo[r + 1];
+    uint64_t o = 0, tn = 0;   // the views before this chunk: entries (unclamped), true counts
+    for (uint64_t c0 = v0; c0 < v1; c0 += 64) {
+        const uint64_t v = c0 + lane;
+        const uint32_t c = v < v1 ? v_cnt[v] : 0u;
+        uint32_t tot;
+        const uint32_t ex = wave_excl_sum(c, tot);
+        const int nc = (int)(v1 - c0 < 64 ? v1 - c0 : 64);
+        for (int j = wv; j < nc; j += 4) {
+            const uint32_t cj = rdlu(c, j);
+            const uint64_t oj = o + rdlu(ex, j), vb = v_base[c0 + j];
+            const uint32_t add = (uint32_t)(v_off[c0 + j] << 1);
+            for (uint32_t i0 = 0; i0 < cj; i0 += 64 * CU) {
+                uint64_t xv[CU];
+                uint32_t yv[CU];
+#pragma unroll
+                for (int u = 0; u < CU; ++u) {
+                    const uint32_t i = i0 + u * 64 + lane;
+                    if (i < cj) { xv[u] = vx[vb + i]; yv[u] = vy[vb + i]; }
+                }
+#pragma unroll
+                for (int u = 0; u < CU; ++u) {
+                    const uint32_t i = i0 + u * 64 + lane;
+                    if (i < cj && oj + i < capn) { x[b + oj + i] = xv[u]; y[b + oj + i] = yv[u] + add; }
+                }
+            }
         }
-        o += c;
-        tn += v_need[v];
+        o += tot;
+        tn += wave_sum64(v < v1 ? (uint64_t)v_need[v] : 0ULL);
     }
-    if (lane == 0) {   // a view that overflowed its own slot flagged it already; the re-run has views off
+    if (threadIdx.x == 0) {   // a view that overflowed its own slot flagged it already; the re-run has views off
         cnt[r] = (uint32_t)(o > capn ? capn : o);
         need[r] = (uint32_t)(tn > 0xffffffffULL ? 0xffffffffULL : tn);
         if (o > capn) atomicOr(overflow, 1);
@@ -4780,20 +4782,6 @@ int launch_batch_sums(uint32_t n, const uint32_t* mz_cnt, const uint32_t* cnt2, 
     LAUNCH_CHECK();
     return 0;
 }
-int launch_view_count(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t* nv, hipStream_t st) {
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_view_count, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, V, nv);
-    LAUNCH_CHECK();
-    return 0;
-}
-int launch_view_fill(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, const uint64_t* vo, uint32_t* v_read, uint64_t* v_off,
-                     uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end, hipStream_t st) {
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_view_fill, dim3((n + 255) / 256), dim3(256), 0, st, n, rd_off, V, W0, vo, v_read, v_off, v_len, v_pre, v_from,
-                       v_last, v_base, v_end);
-    LAUNCH_CHECK();
-    return 0;
-}
 int launch_view_plan(uint32_t n, const uint64_t* rd_off, uint32_t V, uint32_t W0, uint64_t nvmax, uint64_t* vo, uint32_t* v_read,
                      uint64_t* v_off, uint32_t* v_len, uint32_t* v_pre, uint32_t* v_from, uint8_t* v_last, uint64_t* v_base, uint64_t* v_end,
                      uint64_t* base, uint64_t* end, mm2g::ReadOut* zout, unsigned long long* zst, int zst_words, hipStream_t st) {
@@ -4807,7 +4795,7 @@ int launch_view_compact(uint32_t n, const uint64_t* vo, const uint64_t* v_off, c
                         const uint32_t* v_need, const uint64_t* vx, const uint32_t* vy, const uint64_t* base, const uint64_t* end, uint64_t* x,
                         uint32_t* y, uint32_t* cnt, uint32_t* need, int32_t* overflow, hipStream_t st) {
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_view_compact, dim3((n + 3) / 4), dim3(256), 0, st, n, vo, v_off, v_base, v_cnt, v_need, vx, vy, base, end, x, y,
+    hipLaunchKernelGGL(k_view_compact, dim3(n), dim3(256), 0, st, n, vo, v_off, v_base, v_cnt, v_need, vx, vy, base, end, x, y,
                        cnt, need, overflow);
     LAUNCH_CHECK();
     return 0;
