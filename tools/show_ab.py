@@ -6,7 +6,7 @@ from collections import defaultdict
 rows = defaultdict(list)
 for ln in open(sys.argv[1]):
     p = ln.split()
-    if len(p) < 4:
+    if len(p) < 4 or ln.startswith("#"):
         continue
     cfg, ks, v = p[0], " ".join(p[1:-2]), float(p[-2])
     rows[(cfg, ks)].append(v)
