@@ -4462,6 +4462,7 @@ __global__ void k_mz_base(uint32_t n, const uint64_t* rd_off, uint64_t* base, ui
 // >= W0 bases (W0 = 2(w+k)+64 rounded up to 8: enough for odd k, DESIGN.md
 // §10), one wave per view, so a 10 kb read is not 20 sequential tiles of one
 // wave.  View outputs go to their own slots and are concatenated per read.
+constexpr int VIEW_PLAN_LDS = 4096;
 // The view plan in one single-workgroup launch (C2's 500-read units; round 4 used four
 // launches: a memset, a count, a scan and a fill), which also does k_mz_base's slots and clears when
 // `base` is given: per-read view counts, their exclusive scan vo, the view table, and
@@ -4473,6 +4474,7 @@ __global__ __launch_bounds__(1024) void k_view_plan(uint32_t n, const uint64_t* 
                                                     uint8_t* v_last, uint64_t* v_base, uint64_t* v_end, uint64_t* base, uint64_t* end,
                                                     ReadOut* zout, unsigned long long* zst, int zst_words) {
     __shared__ uint32_t s_sc[16];
+    __shared__ uint32_t s_vo[VIEW_PLAN_LDS];   // the view offsets of batches of up to VIEW_PLAN_LDS reads
     const uint32_t tid = threadIdx.x;
     if (base) {
         for (uint32_t r = tid; r <= n; r += 1024) {
@@ -4482,27 +4484,38 @@ __global__ __launch_bounds__(1024) void k_view_plan(uint32_t n, const uint64_t* 
         if (zst) for (uint32_t q = tid; q < (uint32_t)zst_words; q += 1024) zst[q] = 0ULL;
     }
     auto nview = [&](uint32_t r) -> uint32_t { const uint64_t L = rd_off[r + 1] - rd_off[r]; return L <= V ? 1u : (uint32_t)((L + V - 1) / V); };
+    const bool lds = n <= (uint32_t)VIEW_PLAN_LDS;
     uint64_t carry = 0;
     for (uint32_t r0 = 0; r0 < n; r0 += 1024) {
         const uint32_t r = r0 + tid;
         const uint32_t c = r < n ? nview(r) : 0u;
         uint32_t tot;
         const uint32_t ex = block_excl_sum(c, tot, s_sc);
-        if (r < n) vo[r] = carry + ex;
+        if (r < n) { vo[r] = carry + ex; if (lds) s_vo[r] = (uint32_t)(carry + ex); }
         carry += tot;
     }
     if (tid == 0) vo[n] = carry;
     __syncthreads();
-    for (uint32_t r = tid; r < n; r += 1024) {
+    auto fill = [&](uint32_t r, uint32_t j, uint64_t v) {
         const uint64_t L = rd_off[r + 1] - rd_off[r];
-        const uint32_t nv = nview(r);
-        for (uint32_t j = 0; j < nv; ++j) {
-            const uint64_t v = vo[r] + j;
-            const uint64_t c0 = (uint64_t)j * V, ve = c0 + V < L ? c0 + V : L;
-            const uint64_t vs = j ? (c0 > W0 ? (c0 - W0) & ~7ULL : 0) : 0;
-            v_read[v] = r; v_off[v] = vs; v_len[v] = (uint32_t)(ve - vs); v_pre[v] = (uint32_t)vs;
-            v_from[v] = (uint32_t)(c0 - vs); v_last[v] = ve == L ? 1 : 0;
-            v_base[v] = rd_off[r] + c0 + 16 * v; v_end[v] = v_base[v] + (ve - c0) + 16;
+        const uint64_t c0 = (uint64_t)j * V, ve = c0 + V < L ? c0 + V : L;
+        const uint64_t vs = j ? (c0 > W0 ? (c0 - W0) & ~7ULL : 0) : 0;
+        v_read[v] = r; v_off[v] = vs; v_len[v] = (uint32_t)(ve - vs); v_pre[v] = (uint32_t)vs;
+        v_from[v] = (uint32_t)(c0 - vs); v_last[v] = ve == L ? 1 : 0;
+        v_base[v] = rd_off[r] + c0 + 16 * v; v_end[v] = v_base[v] + (ve - c0) + 16;
+    };
+    if (lds && carry <= 0xffffffffULL) {
+        // a thread per view (the table's stores coalesce): its read is the last r with
+        // vo[r] <= v (every read has a view, so vo rises strictly)
+        for (uint64_t v = tid; v < carry; v += 1024) {
+            uint32_t lo = 0, hi = n - 1;
+            while (lo < hi) { const uint32_t mid = (lo + hi + 1) >> 1; if (s_vo[mid] <= (uint32_t)v) lo = mid; else hi = mid - 1; }
+            fill(lo, (uint32_t)v - s_vo[lo], v);
+        }
+    } else {
+        for (uint32_t r = tid; r < n; r += 1024) {
+            const uint32_t nv = nview(r);
+            for (uint32_t j = 0; j < nv; ++j) fill(r, j, vo[r] + j);
         }
     }
     for (uint64_t v = carry + tid; v < nvmax; v += 1024) v_len[v] = 0;   // views past the real count: empty

@@ -82,6 +82,19 @@ def test_sketch_views_parity(dev, view):
                 assert np.array_equal(got[i], want), (view, w, k, i, len(s))
 
 
+@pytest.mark.parametrize("n_reads", [300, 4200])
+def test_sketch_views_plan_sizes(dev, n_reads):
+    """k_view_plan's two fills: a thread per view from the view offsets in LDS
+    (up to 4,096 reads) and a thread per read beyond that; both must give the
+    oracle's minimizers for every read (view_reads raised so both batches take views)."""
+    rng = random.Random(91 + n_reads)
+    seqs = [_rand_seq(rng, rng.choice([40, 64, 65, 200, 513]), p_n=0.003) for _ in range(n_reads)]
+    with knobs(dev, sketch_view=64, view_reads=8192):
+        got = dev.sketch_sequences(seqs, 10, 15, rid=0)
+    for i, s in enumerate(seqs):
+        assert np.array_equal(got[i], O.sketch(s, 10, 15, 0, False)), (n_reads, i, len(s))
+
+
 def test_sketch_rid(dev):
     rng = random.Random(5)
     seqs = [_rand_seq(rng, 3000, p_n=0.01) for _ in range(3)]
