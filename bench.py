@@ -45,7 +45,6 @@ import json
 import os
 import socket
 import statistics
-import subprocess
 import sys
 import threading
 import time
@@ -184,14 +183,6 @@ def count_devices(dist, world: int, ident) -> int:
     return len(set(got))
 
 
-def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def rank_env(argv_gpus: int, env=None):
     """(rank, world, local_rank) from the launcher's environment, checked
     against --gpus: a mismatch is an error, never a silent smaller run."""
@@ -210,32 +201,13 @@ def spawn_ranks(n: int, argv, backend: str, ndev: int, cmd=None) -> int:
     """`--gpus N` (N > 1) without a launcher: start the N rank processes of this
     script as fresh children (this process never touches a GPU, so nothing is
     exec'd from a GPU process), with the environment torch.distributed.run
-    gives them, and wait.  Rank 0 prints the line.  One failing rank stops the
-    others; the exit code is the first failure's."""
+    gives them, and wait (minimap2_rs_amd.shard.spawn_ranks).  Rank 0 prints the
+    line.  One failing rank stops the others; the exit code is the first failure's."""
     if backend == "nccl" and ndev < n:
         raise SystemExit(f"bench.py: --gpus {n} needs {n} GPUs for {n} RCCL ranks, {ndev} visible "
                          f"(MM2G_DIST_BACKEND=gloo rehearses {n} ranks on fewer GPUs)")
-    port = free_port()
-    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
-                LOCAL_WORLD_SIZE=str(n), MM2G_BENCH_SPAWNED="1")
-    cmd = cmd or [sys.executable, os.path.abspath(__file__)]
-    procs = [subprocess.Popen(list(cmd) + list(argv), env=dict(base, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
-    log(f"started {n} rank processes (pids {[p.pid for p in procs]}, master 127.0.0.1:{port})")
-    rc = 0
-    alive = list(procs)
-    while alive:
-        for p in list(alive):
-            c = p.poll()
-            if c is None:
-                continue
-            alive.remove(p)
-            if c != 0 and rc == 0:
-                rc = c if c > 0 else 128 - c
-                log(f"rank process {p.pid} exited with {c}; stopping the others")
-                for q in alive:
-                    q.terminate()
-        time.sleep(0.1)
-    return rc
+    from minimap2_rs_amd.shard import spawn_ranks as spawn
+    return spawn(n, list(cmd or [sys.executable, os.path.abspath(__file__)]) + list(argv), log=log)
 
 
 def paf_lines_by_read(paf: bytes):
@@ -380,9 +352,15 @@ def alg_bytes(cnt: dict, res) -> dict:
     mm2g_batch_counters, res: the per-read results (RES_DTYPE).
     Sorts are priced at 16 B per anchor (each key read once and written once),
     whatever passes an implementation makes; chain kernels at 8 B of key in and
-    8 B of f/pprev out per anchor of the segments they process."""
+    8 B of f/pprev out per anchor of the segments they process.
+    Fused seeding (counters 16/17): k_sort_read makes the keys of the reads it
+    sorts, so k_seed_write is charged only for the other reads, and the sort
+    for those reads' minimizer records (12 B) and position fetches (8 B per
+    anchor) on top of its 16 B: SURVEY.md §8d's per-anchor position fetch +
+    anchor write + anchor read at 8-B keys."""
     n = len(res)
     A, m, mk, L = cnt["anchors"], cnt["minimizers"], cnt["kept_minimizers"], cnt["bases"]
+    Af, mf = cnt.get("fused_anchors", 0), cnt.get("fused_minimizers", 0)
     Adp = cnt.get("dp_anchors", A)
     na = res["n_anchors"].astype(np.int64)
     mapped = (res["flags"] & 1) != 0
@@ -394,9 +372,9 @@ def alg_bytes(cnt: dict, res) -> dict:
         "scan": 24 * n,                                   # two scans: u32 in, u64 out per read
         "filter": 9 * m,                                  # x in, keep flag out
         "seed_count": 9 * m + 16 * mk + 8 * m,            # keep+x in, 16 B table entry per kept, (n, poff) out
-        "seed_write": 12 * m + 16 * A,                    # (n, poff, y) in; 8 B position in + 8 B key out per anchor
+        "seed_write": 12 * (m - mf) + 16 * (A - Af),      # (n, poff, y) in; 8 B position in + 8 B key out per anchor
         "sort_small": 16 * int(na[(na > 1) & (na <= SORT_SMALL)].sum()),
-        "sort_large": 16 * int(na[(na > SORT_SMALL) & (na <= SORT_CELL_MAX)].sum()),
+        "sort_large": 16 * int(na[(na > SORT_SMALL) & (na <= SORT_CELL_MAX)].sum()) + 12 * mf + 8 * Af,
         "sort_radix": 16 * int(na[na > SORT_CELL_MAX].sum()),
         "sort_big": 16 * int(na[na > SORT_CELL_MAX].sum()),
         "chain_items": 8 * n,
@@ -672,15 +650,8 @@ def main():
     value = all_bases / elapsed / 1e9
     ms_per_step = elapsed / max(args.steps, 1) * 1e3
 
-    # ---- roofline of the dominant kernel (HIP events on the library streams) --
-    # Every kernel slot is priced (alg_bytes).  In the timed region four
-    # contexts' kernels share the GPU, so a launch's duration there includes the
-    # other contexts' work (a kernel's in-situ time per step can exceed the step).
-    # The headline `frac` therefore comes from the same kernels on a quiet GPU:
-    # after the timed region one context maps --iso-batches batches back to
-    # back (every launch alone on the GPU, as `rocprofv3 --stats` of a
-    # --streams 1 run sees them), and the dominant kernel is the slot with the
-    # most device time there.  The in-situ figure is kept as `in_situ`.
+    # ---- roofline of the dominant kernel (HIP events on the library streams; roofline_of) --
+    # every kernel slot is priced (alg_bytes); per_kernel holds the timed region's in-situ figures
     kb = alg_bytes(cnt, res_np)
     per_kernel = {}
     for name, (ms, calls) in prof.items():
@@ -694,89 +665,12 @@ def main():
             per_kernel[name] = e
     timed_slots = {k: v for k, v in prof.items() if v[1] > 0}
     chain_ms = sum(v[0] for k, v in timed_slots.items() if k in CHAIN_SLOTS)
-    pair_peak = VALU_INT32_OPS / OPS_PER_PAIR
-    iso_prof, iso_cnt, iso_res, iso_nb = quiet_gpu_profile(lib, L, devs[0], units, batches, P, opts, n_batches, args) \
-        if rank == 0 else (None, None, None, 0)
-    excluded = {}
-    if iso_prof:
-        slots = {k: v for k, v in iso_prof.items() if v[1] > 0}
-        # the figure called frac must fit the step (its kernel time per step <= ms_per_step).  A
-        # tail-bound kernel (C5's k_chain_long: one wave on its longest segment for most of the
-        # launch) can take longer on the quiet GPU than the whole step, where the other contexts'
-        # kernels fill its idle CUs; such a slot is named in `excluded` and the next one is used
-        def fits(k):
-            return slots[k][0] / max(iso_nb, 1) <= ms_per_step * 1.0001
-        for k in sorted(slots, key=lambda k: -slots[k][0]):
-            if fits(k):
-                break
-            excluded[k] = {"quiet_ms_per_step": round(slots[k][0] / max(iso_nb, 1), 4),
-                           "reason": "quiet-GPU time per step exceeds the in-situ step (tail-bound; contexts overlap it)"}
-        dom = max((k for k in slots if k not in excluded), key=lambda k: slots[k][0], default=max(slots, key=lambda k: slots[k][0]))
-        d_ms, d_calls = slots[dom]
-        d_bytes = alg_bytes(iso_cnt, iso_res).get(dom, 0)
-        frac_src = f"quiet GPU: one context, {iso_nb} batches x {P} units mapped back to back after the timed region"
-        launches_per_step = d_calls / max(iso_nb, 1)
-        share = d_ms / max(sum(v[0] for v in slots.values()), 1e-9)
-    else:   # ranks > 0: the in-situ figure (only rank 0 prints)
-        slots = timed_slots
-        dom = max(slots, key=lambda k: slots[k][0])
-        d_ms, d_calls = slots[dom]
-        d_bytes = kb.get(dom, 0)
-        frac_src = "in situ"
-        launches_per_step = d_calls / max(args.steps, 1)
-        share = d_ms / max(sum(v[0] for v in slots.values()), 1e-9)
-    d_sym, d_hint = KERNEL_SYMBOLS.get(dom, (dom, ""))
-    avg_s = d_ms / 1e3 / max(d_calls, 1)
-    bytes_per_launch = d_bytes / max(d_calls, 1)
-    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic, traffic_row = pmc_traffic(d_sym, d_hint, bench_config_tag(args))
-    # the figure called frac must fit the step: its kernel time per step <= ms_per_step
-    kernel_ms_per_step = avg_s * 1e3 * launches_per_step
-    if kernel_ms_per_step > ms_per_step * 1.0001:
-        raise SystemExit(f"bench.py: roofline kernel {d_sym} takes {kernel_ms_per_step:.3f} ms per step "
-                         f"({avg_s * 1e3:.4f} ms x {launches_per_step:g} launches) > the step's {ms_per_step:.3f} ms")
-    ins = timed_slots.get(dom)
-    in_situ = None
-    if ins:
-        ins_avg = ins[0] / 1e3 / ins[1]
-        ins_ach = kb.get(dom, 0) / ins[1] / ins_avg / 1e9 if ins_avg > 0 else 0.0
-        in_situ = {"avg_launch_ms": round(ins_avg * 1e3, 4), "launches_per_step": ins[1] / args.steps,
-                   "achieved": round(ins_ach, 3), "frac": round(ins_ach / HBM_PEAK_GBS, 6),
-                   "share_of_kernel_time": round(ins[0] / max(sum(v[0] for v in timed_slots.values()), 1e-9), 4),
-                   "note": f"the timed region's launches ({max(1, args.streams)} contexts share the GPU: durations include "
-                           f"the other contexts' kernels, so ms x launches may exceed the step)"}
-    A_, Ar_, mk_, L_ = cnt["anchors"], cnt["rescued_anchors"], cnt["kept_minimizers"], cnt["bases"]
-    B_path_ = (L_ + 3) // 4 + 16 * mk_ + 48 * A_ + 24 * Ar_
-    path_frac = B_path_ / elapsed / 1e9 / HBM_PEAK_GBS if world == 1 else None
-    roofline = {
-        "bound": "hbm", "kernel": d_sym, "slot": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_row": traffic_row,
-        "avg_launch_ms": round(avg_s * 1e3, 4), "launches_per_step": launches_per_step,
-        "kernel_ms_per_step": round(kernel_ms_per_step, 4), "alg_bytes_per_launch": int(bytes_per_launch),
-        "share_of_kernel_time": round(share, 4), "measured": frac_src, "excluded": excluded or None,
-        "path_frac": round(path_frac, 6) if path_frac is not None else None,
-        "path_note": "SURVEY.md §8d B(read) summed over the timed batches / step time / 8 TB/s (all kernels, host included)",
-        "in_situ": in_situ,
-        # SURVEY.md §8d secondary figure: DP pair evaluations against the int32 VALU rate at 15 ops per pair
-        "compute": {"dp_pairs_per_step": cnt["dp_pairs"] / args.steps,
-                    "pairs_per_s_wall": round(cnt["dp_pairs"] / elapsed, 1) if world == 1 else None,
-                    "pairs_per_s_in_chain_kernels": round(cnt["dp_pairs"] / (chain_ms / 1e3), 1) if chain_ms > 0 else None,
-                    "peak_pairs_per_s": pair_peak,
-                    "frac_wall": round(cnt["dp_pairs"] / elapsed / pair_peak, 6) if world == 1 else None,
-                    "note": "peak = 7.9e13 int32 ops/s / 15 ops per pair (SURVEY.md §8d); chain-kernel time overlaps "
-                            "other contexts' kernels, so the in-kernel rate is a lower bound"},
-        "seed_lookup_floor_bytes_per_step": 128 * cnt["kept_minimizers"] // args.steps,
-        "seed_lookup_note": "a hashed-table probe reads at least one 128-B request per kept minimizer "
-                            "(MI355X_MICROARCH.md: 128-B requests), against 16 B of table entry priced as algorithmic",
-    }
-    iso = None
-    if iso_prof:   # every slot on the quiet GPU (ms per batch, launches, alg GB/s)
-        ib = alg_bytes(iso_cnt, iso_res)
-        iso = {"batches": iso_nb, "per_kernel": {
-            k: {"ms_per_batch": round(v[0] / iso_nb, 4), "launches_per_batch": v[1] / iso_nb,
-                "alg_GBps": round(ib.get(k, 0) / (v[0] / 1e3) / 1e9, 2) if v[0] > 0 else None}
-            for k, v in sorted(iso_prof.items(), key=lambda kv: -kv[1][0]) if v[1] > 0},
-            "kernel_ms_per_batch": round(sum(v[0] for v in iso_prof.values()) / iso_nb, 4)}
+    # the roofline is rank 0's (only rank 0 prints); the other ranks go straight to the parity gather
+    roofline = iso = None
+    fatal = []
+    if rank == 0:
+        roofline, iso, fatal = roofline_of(args, lib, L, devs, units, batches, P, opts, n_batches, cnt, kb, prof,
+                                           timed_slots, chain_ms, per_kernel, ms_per_step, elapsed, world)
     # whole-path algorithmic bytes (SURVEY.md §8d B(read) summed) over the step time
     A, Ar, mk, L_tot = cnt["anchors"], cnt["rescued_anchors"], cnt["kept_minimizers"], cnt["bases"]
     B_path = (L_tot + 3) // 4 + 16 * mk + 48 * A + 24 * Ar
@@ -794,6 +688,8 @@ def main():
     if rank == 0 and n_sample:
         cpu, parity = oracle_check(args, names, lens, gbuf, mid, thr, gathered, world)
 
+    if fatal:   # after the gather (the other ranks are not left waiting in it)
+        raise SystemExit("bench.py: " + "; ".join(fatal))
     if rank == 0:
         line = {
             "metric": "aligned Gbases/sec (PAF out), 10k×10kb ONT reads vs hg38, 1/2/4/8 GPUs",
@@ -846,6 +742,112 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def roofline_of(args, lib, L, devs, units, batches, P, opts, n_batches, cnt, kb, prof, timed_slots, chain_ms, per_kernel,
+                ms_per_step, elapsed, world):
+    """Rank 0: the roofline of the dominant kernel, from the same kernels on a quiet GPU.
+    In the timed region four contexts' kernels share the GPU, so a launch's duration
+    there includes the other contexts' work (a kernel's in-situ time per step can
+    exceed the step).  The headline `frac` therefore comes from the same kernels on a
+    quiet GPU: after the timed region one context maps --iso-batches batches back to
+    back (every launch alone on the GPU, as `rocprofv3 --stats` of a --streams 1 run
+    sees them), and the dominant kernel is the slot with the most device time there.
+    The in-situ figure is kept as `in_situ`.  -> (roofline, quiet-GPU slots, fatal
+    errors): a slot priced above the HBM peak (its alg. bytes are not the work it
+    does) or a quiet-GPU dominant kernel longer than the step is an error."""
+    pair_peak = VALU_INT32_OPS / OPS_PER_PAIR
+    iso_prof, iso_cnt, iso_res, iso_nb = (quiet_gpu_profile(lib, L, devs[0], units, batches, P, opts, n_batches, args)
+                                          if args.iso_batches > 0 else (None, None, None, 0))
+    excluded = {}
+    fatal = []
+    if iso_prof:
+        slots = {k: v for k, v in iso_prof.items() if v[1] > 0}
+        # the figure called frac must fit the step (its kernel time per step <= ms_per_step).  A
+        # tail-bound kernel (C5's k_chain_long: one wave on its longest segment for most of the
+        # launch) can take longer on the quiet GPU than the whole step, where the other contexts'
+        # kernels fill its idle CUs; such a slot is named in `excluded` and the next one is used
+        def fits(k):
+            return slots[k][0] / max(iso_nb, 1) <= ms_per_step * 1.0001
+        for k in sorted(slots, key=lambda k: -slots[k][0]):
+            if fits(k):
+                break
+            excluded[k] = {"quiet_ms_per_step": round(slots[k][0] / max(iso_nb, 1), 4),
+                           "reason": "quiet-GPU time per step exceeds the in-situ step (tail-bound; contexts overlap it)"}
+        dom = max((k for k in slots if k not in excluded), key=lambda k: slots[k][0], default=max(slots, key=lambda k: slots[k][0]))
+        d_ms, d_calls = slots[dom]
+        d_bytes = alg_bytes(iso_cnt, iso_res).get(dom, 0)
+        frac_src = f"quiet GPU: one context, {iso_nb} batches x {P} units mapped back to back after the timed region"
+        launches_per_step = d_calls / max(iso_nb, 1)
+        share = d_ms / max(sum(v[0] for v in slots.values()), 1e-9)
+    else:   # --iso-batches 0: the in-situ figure (its launches overlap other contexts' kernels)
+        slots = timed_slots
+        dom = max(slots, key=lambda k: slots[k][0])
+        d_ms, d_calls = slots[dom]
+        d_bytes = kb.get(dom, 0)
+        frac_src = "in situ (--iso-batches 0)"
+        launches_per_step = d_calls / max(args.steps, 1)
+        share = d_ms / max(sum(v[0] for v in slots.values()), 1e-9)
+    d_sym, d_hint = KERNEL_SYMBOLS.get(dom, (dom, ""))
+    avg_s = d_ms / 1e3 / max(d_calls, 1)
+    bytes_per_launch = d_bytes / max(d_calls, 1)
+    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+    traffic, traffic_row = pmc_traffic(d_sym, d_hint, bench_config_tag(args))
+    kernel_ms_per_step = avg_s * 1e3 * launches_per_step
+    # the quiet-GPU figure called frac must fit the step (ADVICE r5: not the in-situ one, whose
+    # launches include the other contexts' kernels)
+    if iso_prof and kernel_ms_per_step > ms_per_step * 1.0001:
+        fatal.append(f"roofline kernel {d_sym} takes {kernel_ms_per_step:.3f} ms per step "
+                     f"({avg_s * 1e3:.4f} ms x {launches_per_step:g} launches) > the step's {ms_per_step:.3f} ms")
+    ins = timed_slots.get(dom)
+    in_situ = None
+    if ins:
+        ins_avg = ins[0] / 1e3 / ins[1]
+        ins_ach = kb.get(dom, 0) / ins[1] / ins_avg / 1e9 if ins_avg > 0 else 0.0
+        in_situ = {"avg_launch_ms": round(ins_avg * 1e3, 4), "launches_per_step": ins[1] / args.steps,
+                   "achieved": round(ins_ach, 3), "frac": round(ins_ach / HBM_PEAK_GBS, 6),
+                   "share_of_kernel_time": round(ins[0] / max(sum(v[0] for v in timed_slots.values()), 1e-9), 4),
+                   "note": f"the timed region's launches ({max(1, args.streams)} contexts share the GPU: durations include "
+                           f"the other contexts' kernels, so ms x launches may exceed the step)"}
+    A_, Ar_, mk_, L_ = cnt["anchors"], cnt["rescued_anchors"], cnt["kept_minimizers"], cnt["bases"]
+    B_path_ = (L_ + 3) // 4 + 16 * mk_ + 48 * A_ + 24 * Ar_
+    path_frac = B_path_ / elapsed / 1e9 / HBM_PEAK_GBS if world == 1 else None
+    roofline = {
+        "bound": "hbm", "kernel": d_sym, "slot": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_row": traffic_row,
+        "avg_launch_ms": round(avg_s * 1e3, 4), "launches_per_step": launches_per_step,
+        "kernel_ms_per_step": round(kernel_ms_per_step, 4), "alg_bytes_per_launch": int(bytes_per_launch),
+        "share_of_kernel_time": round(share, 4), "measured": frac_src, "excluded": excluded or None,
+        "path_frac": round(path_frac, 6) if path_frac is not None else None,
+        "path_note": "SURVEY.md §8d B(read) summed over the timed batches / step time / 8 TB/s (all kernels, host included)",
+        "in_situ": in_situ,
+        # SURVEY.md §8d secondary figure: DP pair evaluations against the int32 VALU rate at 15 ops per pair
+        "compute": {"dp_pairs_per_step": cnt["dp_pairs"] / args.steps,
+                    "pairs_per_s_wall": round(cnt["dp_pairs"] / elapsed, 1) if world == 1 else None,
+                    "pairs_per_s_in_chain_kernels": round(cnt["dp_pairs"] / (chain_ms / 1e3), 1) if chain_ms > 0 else None,
+                    "peak_pairs_per_s": pair_peak,
+                    "frac_wall": round(cnt["dp_pairs"] / elapsed / pair_peak, 6) if world == 1 else None,
+                    "note": "peak = 7.9e13 int32 ops/s / 15 ops per pair (SURVEY.md §8d); chain-kernel time overlaps "
+                            "other contexts' kernels, so the in-kernel rate is a lower bound"},
+        "seed_lookup_floor_bytes_per_step": 128 * cnt["kept_minimizers"] // args.steps,
+        "seed_lookup_note": "a hashed-table probe reads at least one 128-B request per kept minimizer "
+                            "(MI355X_MICROARCH.md: 128-B requests), against 16 B of table entry priced as algorithmic",
+    }
+    iso = None
+    if iso_prof:   # every slot on the quiet GPU (ms per batch, launches, alg GB/s)
+        ib = alg_bytes(iso_cnt, iso_res)
+        iso = {"batches": iso_nb, "per_kernel": {
+            k: {"ms_per_batch": round(v[0] / iso_nb, 4), "launches_per_batch": v[1] / iso_nb,
+                "alg_GBps": round(ib.get(k, 0) / (v[0] / 1e3) / 1e9, 2) if v[0] > 0 else None}
+            for k, v in sorted(iso_prof.items(), key=lambda kv: -kv[1][0]) if v[1] > 0},
+            "kernel_ms_per_batch": round(sum(v[0] for v in iso_prof.values()) / iso_nb, 4)}
+    # a slot above the HBM peak is not doing the work it is priced at (VERDICT r5 item 2)
+    over = [f"{k} {e['alg_GBps']} GB/s in situ" for k, e in per_kernel.items() if (e.get("alg_GBps") or 0) > HBM_PEAK_GBS]
+    if iso:
+        over += [f"{k} {e['alg_GBps']} GB/s quiet" for k, e in iso["per_kernel"].items() if (e.get("alg_GBps") or 0) > HBM_PEAK_GBS]
+    if over:
+        fatal.append("algorithmic bytes priced above the 8 TB/s HBM peak: " + ", ".join(over))
+    return roofline, iso, fatal
 
 
 def quiet_gpu_profile(lib, L, d0, units, batches, P, opts, n_batches, args):

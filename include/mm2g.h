@@ -378,9 +378,12 @@ int mm2g_prof_reset(mm2g_ctx* ctx);
  * in its medium segments [9] of pass 0, and [10], [11], [12] of the rescue pass;
  * DP anchors whose keys k_chain_seg streams in pass 0 (k_seg_cands finds the
  * other reads' candidate segments without reading keys) [13], that k_chain_lb
- * streams [14], and rescued anchors k_chain_seg streams in the rescue pass [15].
+ * streams [14] (0 when it did not run: debug, multi-chain or pruning off), and
+ * rescued anchors k_chain_seg streams in the rescue pass [15]; the anchors [16]
+ * and minimizers [17] of the reads whose keys k_sort_read makes itself (fused
+ * seeding: k_seed_write skips them).
  * Copies min(n, MM2G_N_COUNTERS) values; returns how many. */
-#define MM2G_N_COUNTERS 16
+#define MM2G_N_COUNTERS 18
 int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <atomic>
 #include <thread>
@@ -153,6 +154,7 @@ struct mm2g_ctx {
     bool mapped = false, collected = false, stop_after_sort = false, dv_separate = false;
     bool redo = false;                     // inside wait_batch's re-map (MM2G_KNOB_WS_MIN applies to first maps only)
     bool ws_exact = false;                 // anchor workspace sized to the batches' exact counts (HBM was short)
+    bool lb_ran0 = false;                  // the last map launched pass 0's k_chain_lb (counter 14)
     uint64_t n_anchors = 0;
     KeyLayout kl{};
     mm2g_map_opts last_opts{};
@@ -974,6 +976,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
         // (bw_long, bw] are rejected in the rescue and LB_0 does not bound it.
         const bool rescue_wider = bw_long >= P0.bw && mdx1 >= P0.max_dist_x && mdy1 >= P0.max_dist_y;
         ca.fmin = (pass == 0 || K[MM2G_KNOB_PRUNE_RESCUE]) ? fmin_buf : nullptr;
+        if (pass == 0) c->lb_ran0 = ca.fmin != nullptr;
         ca.isob = isob;
         ca.seg_streamed = stat ? stat + 5 + pass : nullptr;   // status words 5 / 6
         ca.zero_fmin = ca.fmin && (pass == 0 || !rescue_wider) ? 1u : 0u;   // cleared by k_seg_items
@@ -996,7 +999,9 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
                 ProfScope ps(c, pass ? "chain_cands_rescue" : "chain_cands");
                 // one workgroup per 16 reads; with long reads (over ~64 kb) also one per read (up to
                 // 1024), since each such read takes a whole workgroup
-                const uint32_t cb = std::max<uint32_t>((n + 15) / 16, c->max_read_len >= 65536 ? n : 0u);
+                // (the kernel's criterion, cnt2 > cands_longw * 64: at most A_cap / (64 cands_longw) such reads)
+                const uint64_t nlong = std::min<uint64_t>(n, A_cap / (64ull * ca.cands_longw) + 1);
+                const uint32_t cb = std::max<uint32_t>((n + 15) / 16, (uint32_t)nlong);
                 LCHK(launch_chain_stage(10, ca, (int)std::min<uint32_t>(cb, 1024), c->stream));
             }
         }
@@ -1416,9 +1421,15 @@ static int multi_epilogue(mm2g_ctx* c) {
     const int32_t kdv = c->dv_separate ? H.k : o.k;
     mm2g::MultiParams P{o.min_cnt, o.min_chain_score, 500, o.max_gap, o.mask_level, o.pri_ratio, o.best_n};
     c->multi.assign(n, mm2g::MultiRead{});
-    // reads are independent: blocks of 64 handed out to the host_threads pool
+    // reads are independent: blocks of 64 handed out to the host_threads pool.  A worker
+    // that throws (std::bad_alloc on a 100 kb read's vectors) records the first error and stops the
+    // others; every started thread is joined and the call returns an MM2G error
     std::atomic<uint32_t> next{0};
+    std::atomic<int> failed{0};
+    std::mutex err_mu;
+    std::string err_msg;
     auto work = [&]() {
+    try {
     std::vector<int32_t> mp;
     for (;;) {
     const uint32_t b0 = next.fetch_add(64);
@@ -1446,13 +1457,22 @@ static int multi_epilogue(mm2g_ctx* c) {
         r.score = M.s1; r.cm = L.cm; r.qs = L.qs; r.qe = L.qe; r.ts = L.ts; r.te = L.te; r.rid = L.rid; r.rev = L.rev;
         r.n_match = L.n_match; r.dv_st = L.dv_st; r.dv_en = L.dv_en; r.dv = L.dv;
     }
+    if (failed.load()) break;
+    }
+    } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (!failed.exchange(1)) err_msg = e.what();
+        next.store(n);
     }
     };
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(c->knob[MM2G_KNOB_HOST_THREADS], (n + 63) / 64));
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    try {
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    } catch (const std::exception&) {}    // fewer threads than asked: the started ones and this one finish the work
     work();
     for (auto& t : th) t.join();
+    if (failed.load()) return set_err(MM2G_E_NOMEM, "multi-chain epilogue: %s", err_msg.c_str());
     return 0;
 }
 
@@ -1509,8 +1529,10 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     c->counters[6] = c->h_stat[4];    // anchors left after the sort's singleton filter (the DP input)
     for (int t = 0; t < 6; ++t) c->counters[7 + t] = c->h_stat[8 + t];   // anchors per chain kernel class and pass
     c->counters[13] = c->h_stat[5];   // DP anchors whose keys k_chain_seg streams (pass 0; the rest: sparse items)
-    c->counters[14] = c->h_stat[4];   // ... that k_chain_lb streams (pass 0)
+    c->counters[14] = c->lb_ran0 ? c->h_stat[4] : 0;   // ... that k_chain_lb streams (pass 0; 0 when it did not run)
     c->counters[15] = c->h_stat[6];   // rescued anchors whose keys k_chain_seg streams (pass 1)
+    c->counters[16] = c->h_stat[7];   // anchors of the reads k_sort_read seeds itself (fused seeding)
+    c->counters[17] = c->h_stat[14];  // ... and their minimizers
     return 0;
 }
 

@@ -1483,6 +1483,10 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
             uint32_t* My = Mp + fm;                // query y
             uint32_t* Mh = My + fm;                // raw n (IX_INLINE | position high word for a Single)
             const uint64_t mb = a.mz_base[r];
+            if (tid == 0 && a.abort) {             // status words 7 / 14: anchors and minimizers seeded here (bench pricing)
+                atomicAdd((unsigned long long*)a.abort + 7, (unsigned long long)A0);
+                atomicAdd((unsigned long long*)a.abort + 14, (unsigned long long)fm);
+            }
             uint32_t carry = 0;
             constexpr int FS = 2;   // minimizers per thread per step (a 10 kb read's ~1.8 k in one step)
             for (uint32_t i0 = 0; i0 < fm; i0 += NT * FS) {

@@ -223,3 +223,39 @@ def test_shared_genome_one_generator(tmp_path):
     assert got[0][1:4] == got[1][1:4] and sum(got[0][2]) > 0
     assert got[1][4] == "memmap"
     assert not os.path.exists(f"/dev/shm/mm2g_bench_t{port}.genome")
+
+
+def _records_fastq(path, names, seqs):
+    with open(path, "wb") as fh:
+        for nm, s in zip(names, seqs):
+            q = bytes(64 if i % 7 == 0 else 73 for i in range(len(s)))   # quality lines that start with '@'
+            fh.write(b"@" + nm.encode() + b" extra\n" + s + b"\n+\n" + q + b"\n")
+
+
+@pytest.mark.parametrize("fmt", ["fasta", "fastq"])
+def test_read_range_partitions_records(tmp_path, fmt):
+    """shard.read_range: the byte ranges of every world size hand each record
+    to exactly one rank, in input order, parsed as SeqStream parses them
+    (names to the first space, multi-line FASTA, FASTQ quality skipped)."""
+    import random
+    from minimap2_rs_amd.shard import read_range
+    rng = random.Random(5)
+    names = [f"q{i}" for i in range(37)]
+    seqs = [bytes(rng.choice(b"ACGTN") for _ in range(rng.choice([0, 1, 50, 81, 160, 333]))) for _ in names]
+    path = str(tmp_path / f"r.{fmt}")
+    if fmt == "fasta":
+        from tools import simdata
+        simdata.write_fasta(path, names, seqs)
+    else:
+        _records_fastq(path, names, seqs)
+    for world in (1, 2, 3, 5, 8, 40):
+        got_n, got_s = [], []
+        for r in range(world):
+            nm, buf, offs = read_range(path, r, world)
+            got_n += nm
+            got_s += [bytes(buf[int(offs[i]):int(offs[i + 1])]) for i in range(len(nm))]
+        assert got_n == names and got_s == seqs, world
+    empty = str(tmp_path / "empty.fa")
+    open(empty, "wb").close()
+    nm, buf, offs = read_range(empty, 0, 2)
+    assert nm == [] and len(offs) == 1
