@@ -536,7 +536,7 @@ def main():
             sub = np.ascontiguousarray(offs[lo:hi + 1], dtype=np.uint64)     # absolute offsets into rb
             units.append({
                 "b": b, "k": k, "lo": lo, "n": nr, "offs": sub,
-                "names": (C.c_char_p * max(nr, 1))(*[f"r{b}_{i}".encode() for i in range(lo, hi)]),
+                "names": (C.c_char_p * max(nr, 1))(*[read_name(rank, b, i).encode() for i in range(lo, hi)]),
                 "res": (L.ReadResult * max(nr, 1))(),
                 "cap": (1024 if multi else 256) * nr + (1 << 20), "len": 0, "cnt": None,
             })
@@ -680,7 +680,7 @@ def main():
     # ---- oracle parity on a sample of every rank's timed batches; CPU baseline
     # N=1: ~3,000 reads (the CPU baseline's ~8 s runs come out of it); N>1: 500 per rank
     n_sample = 0 if args.no_parity else min(args.reads * args.steps, 3000 if world == 1 else 500)
-    samp = sample_reads(args, batches, timed, n_sample, S)
+    samp = sample_reads(args, batches, timed, n_sample, S, rank)
     gathered = [samp] if world == 1 else [None] * world
     if world > 1:
         dist.all_gather_object(gathered, samp)
@@ -871,7 +871,13 @@ def quiet_gpu_profile(lib, L, d0, units, batches, P, opts, n_batches, args):
     return pi, cnt_i, np.concatenate(res_i), nb
 
 
-def sample_reads(args, batches, timed, n_sample: int, S: int):
+def read_name(rank: int, b: int, i: int) -> str:
+    """Read i of batch b on this rank: names are unique over the ranks, since the
+    parity check gathers every rank's sample into one PAF keyed by name."""
+    return f"r{b}_{i}" if rank == 0 else f"r{b}_{i}_rank{rank}"
+
+
+def sample_reads(args, batches, timed, n_sample: int, S: int, rank: int = 0):
     """The first reads of every timed batch (spread over all of them), with the
     GPU's per-read results and PAF lines: what the oracle re-checks."""
     if n_sample <= 0:
@@ -890,7 +896,7 @@ def sample_reads(args, batches, timed, n_sample: int, S: int):
             lines.update(paf_lines_by_read(bytes(u["buf"].raw[:u["len"]])))
         res = np.concatenate([np.frombuffer(u["res"], dtype=RES_DTYPE, count=u["n"]) for u in us if u["n"]])
         for i in range(min(per, len(offs) - 1)):
-            nm = f"r{b}_{i}"
+            nm = read_name(rank, b, i)
             out["reads"].append((nm, bytes(rb[int(offs[i]):int(offs[i + 1])])))
             out["res"].append(res[i].tobytes())
             if nm in lines:

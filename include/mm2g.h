@@ -51,8 +51,9 @@ int mm2g_index_build_fasta(const char* path, int w, int k, int b, int flag, int 
 /* Same from in-memory sequences (names may be NULL -> no name). */
 int mm2g_index_build_seqs(uint32_t n_seq, const char* const* names, const uint8_t* const* seqs, const uint64_t* lens,
                           int w, int k, int b, int flag, int n_threads, mm2g_index** out);
-/* The same builds on a GPU (reference sketching, bucket
- * sort by hash and p/h construction on `device`, S packed there too); the
+/* The same builds on a GPU (reference sketching, a
+ * hand-written radix sort by (bucket, hash, position) and the p/h construction
+ * on `device`; S packed by host threads meanwhile); the
  * result is identical to the host build (same .mmi bytes).  Odd and even k
  * (per-view warm-ups sized on the host) and HPC (flag & 1: TinyQueue spans,
  * src/sketch.rs:51-64, computed per base on the device) are built on the
@@ -362,7 +363,8 @@ enum {
     MM2G_IKNOB_GPU_STRICT = 4,   /* tests: a GPU index build the device cannot do fails instead of falling
                                     back to the host build [0]                                               */
     MM2G_IKNOB_FORCE_FALLBACK = 5, /* tests: GPU index builds take the host fallback (MM2G_IX_GPU_FALLBACK) [0] */
-    MM2G_IKNOB_COUNT = 6
+    MM2G_IKNOB_IXSORTV = 6,      /* tests: the GPU index build sorts by value even when the pairs arrive sorted [0] */
+    MM2G_IKNOB_COUNT = 7
 };
 int mm2g_set_index_knob(int knob, int64_t value);
 

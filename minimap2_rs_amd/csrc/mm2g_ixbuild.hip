@@ -9,14 +9,17 @@
 //      the warm-up, and only steps >= the view's own first base emit, so the
 //      views' emissions partition the contig's.
 //   2. k_ix_compact: (hash, rid<<32 | pos<<1 | strand) pairs, contig order.
-//   3. two stable LSD radix sorts (rocPRIM): by value, then by hash -> sorted by
-//      (hash, value), which is post_process's order: per hash a run; runs of
-//      one are singletons, longer runs sorted position slices.
-//   4. the host distributes runs to buckets (hash & (2^b-1)) in hash order:
-//      exactly finish_bucket's h / p, so .mmi, stats, mid_occ and the device
-//      table are byte-identical with the host build (tests/test_gpu_parity.py).
-//   5. S, the 4-bit packed reference (src/index.rs:14-19), is packed on the
-//      device (k_pack4).
+//   3. a hand-written stable LSD radix sort (8-bit digits, ballot-ranked tiles)
+//      by the bucket-major key (hash & (2^b-1), hash >> b) -- after a stable sort
+//      by value when the values arrive out of order (even k only) -> sorted by
+//      (bucket, hash, value): per hash a run (post_process's order); runs of one
+//      are singletons, longer runs sorted position slices.
+//   4. runs -> finish_bucket's h / p on the device (scans of run starts and of
+//      multi-run members), bucket by bucket; host threads copy each bucket's
+//      slices through pinned buffers.  .mmi, stats, mid_occ and the device table
+//      are byte-identical with the host build (tests/test_gpu_parity.py).
+//   5. S, the 4-bit packed reference (src/index.rs:14-19), is packed by host
+//      threads while the device sketches and sorts.
 //   HPC (flag & 1, src/sketch.rs:51-64): the reference never advances i past a
 //      homopolymer run, so k-mers are the plain ones and only the
 //      spans change: span(i) = sum of skip_len over the last k ACGT bases since
@@ -27,7 +30,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -109,17 +111,205 @@ __global__ __launch_bounds__(256) void k_hpc_span(const uint8_t* seq, uint64_t t
     }
 }
 
-// S (src/index.rs:14-19): 8 bases per u32 word, base j of the concatenation in
-// bits 4(j%8)..; words past the sequence stay 0 (kroundup64 padding)
-__global__ void k_pack4(const uint8_t* seq, uint64_t total, uint64_t n_words, uint32_t* S) {
-    const uint64_t wd = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (wd >= n_words) return;
-    uint32_t v = 0;
-    for (int j = 0; j < 8; ++j) {
-        const uint64_t p = wd * 8 + j;
-        if (p < total) v |= (nt4_dev(seq[p]) & 0xFu) << (4 * j);
+// The contigs in the device nt4 format of the query reads (include/mm2g.h "nt4
+// read batch"), so the build's sketch runs the query kernel's tuned SeqNt4 path
+// with views: contig r's 2-bit codes at u64 word pk_off[r] (base i at bits
+// 2(i%8) of u16 word i/8), its ambiguity bitmap at amb_off[r] (bit i%8 of byte
+// i/8).  One thread per 8 bases; gs[r] = the first 8-base group of contig r.
+__global__ __launch_bounds__(256) void k_pack_nt4(const uint8_t* seq, const uint64_t* coff, const uint64_t* gs, uint32_t n,
+                                                  uint64_t n_groups, const uint64_t* pk_off, const uint64_t* amb_off,
+                                                  uint64_t* words) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups; g += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = n;          // gs[lo] <= g < gs[hi]
+        while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (gs[mid] <= g) lo = mid; else hi = mid; }
+        const uint64_t j = g - gs[lo], p0 = coff[lo] + 8 * j, e = coff[lo + 1];
+        uint32_t code = 0, amb = 0;
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t p = p0 + (uint64_t)u;
+            const uint32_t c = p < e ? nt4_dev(seq[p]) : 4u;
+            if (c < 4) code |= c << (2 * u); else if (p < e) amb |= 1u << u;
+        }
+        ((uint16_t*)(words + pk_off[lo]))[j] = (uint16_t)code;
+        ((uint8_t*)(words + amb_off[lo]))[j] = (uint8_t)amb;
     }
-    S[wd] = v;
+}
+
+// ---- device-wide scans and the LSD radix sort of the build's (hash, position) pairs
+// (post_process's sort, src/index.rs:74-109), hand-written for gfx950: 8-bit digits,
+// tiles of RS_TILE pairs per 256-thread block, stable ranks from wave ballots.
+constexpr int SC_T = 1024, SC_PER = 16;            // scan: 16,384 elements per block
+constexpr uint64_t SC_CHUNK = (uint64_t)SC_T * SC_PER;
+constexpr int RS_ROWS = 16;                        // radix: rows of 256 pairs per tile
+constexpr uint64_t RS_TILE = 256ull * RS_ROWS;
+
+template <typename T>
+__device__ __forceinline__ T block_excl_scan1024(T v, T& total, T* sh) {   // 1024 threads, sh: 16 T
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    T x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { const T o = __shfl_up(x, d, 64); if (lane >= d) x += o; }
+    if (lane == 63) sh[wv] = x;
+    __syncthreads();
+    T wbase = 0, tot = 0;
+    for (int t = 0; t < 16; ++t) { const T c = sh[t]; if (t < wv) wbase += c; tot += c; }
+    __syncthreads();
+    total = tot;
+    return wbase + x - v;
+}
+
+// per-chunk sums
+template <typename T>
+__global__ __launch_bounds__(SC_T) void k_scan_reduce(const T* in, uint64_t n, T* part) {
+    __shared__ T sh[16];
+    const uint64_t c0 = (uint64_t)blockIdx.x * SC_CHUNK;
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_PER; ++j) { const uint64_t i = c0 + (uint64_t)j * SC_T + threadIdx.x; if (i < n) s += in[i]; }
+    T tot;
+    (void)block_excl_scan1024<T>(s, tot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+// exclusive scan of the chunk sums in place (one block)
+template <typename T>
+__global__ __launch_bounds__(SC_T) void k_scan_parts(T* part, uint32_t np) {
+    __shared__ T sh[16];
+    T carry = 0;
+    for (uint32_t b0 = 0; b0 < np; b0 += SC_T) {
+        const uint32_t i = b0 + threadIdx.x;
+        const T v = i < np ? part[i] : 0;
+        T tot;
+        const T ex = block_excl_scan1024<T>(v, tot, sh);
+        if (i < np) part[i] = carry + ex;
+        carry += tot;
+    }
+}
+// exclusive scan of each chunk from its base; out may alias in
+template <typename T>
+__global__ __launch_bounds__(SC_T) void k_scan_down(const T* in, T* out, uint64_t n, const T* part) {
+    __shared__ T sh[16];
+    const uint64_t c0 = (uint64_t)blockIdx.x * SC_CHUNK;
+    T carry = part[blockIdx.x];
+    for (int j = 0; j < SC_PER; ++j) {
+        const uint64_t i = c0 + (uint64_t)j * SC_T + threadIdx.x;
+        const T v = i < n ? in[i] : 0;
+        T tot;
+        const T ex = block_excl_scan1024<T>(v, tot, sh);
+        if (i < n) out[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+// digit counts of one tile: cnt[d * nb + tile]
+__global__ __launch_bounds__(256) void k_rs_count(const uint64_t* key, uint64_t n, int shift, uint32_t* cnt, uint32_t nb) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll
+    for (int j = 0; j < RS_ROWS; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * 256 + threadIdx.x;
+        if (i < n) atomicAdd(&h[(uint32_t)(key[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    cnt[(uint64_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+
+// stable scatter of one tile: rows of 256 pairs in index order; inside a row a
+// pair's rank among the equal digits of lower lanes comes from digit ballots,
+// across the row's four waves from their per-digit counts
+__global__ __launch_bounds__(256) void k_rs_scatter(const uint64_t* kin, const uint64_t* vin, uint64_t* kout, uint64_t* vout,
+                                                    uint64_t n, int shift, const uint32_t* off, uint32_t nb) {
+    __shared__ uint32_t base[256];
+    __shared__ uint32_t wc[4][256];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    base[tid] = off[(uint64_t)tid * nb + blockIdx.x];
+    for (int w = 0; w < 4; ++w) wc[w][tid] = 0;
+    const uint64_t t0 = (uint64_t)blockIdx.x * RS_TILE;
+    const uint64_t lt = (1ULL << lane) - 1ULL;
+    __syncthreads();
+    for (int j = 0; j < RS_ROWS; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * 256 + tid;
+        const bool valid = i < n;
+        const uint64_t k = valid ? kin[i] : 0ULL, v = valid ? vin[i] : 0ULL;
+        const uint32_t d = (uint32_t)(k >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const bool on = (d >> bit) & 1u;
+            const uint64_t bb = __ballot(on);
+            peers &= on ? bb : ~bb;
+        }
+        const uint32_t r = (uint32_t)__popcll(peers & lt);
+        if (valid && r == 0) wc[wv][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        uint32_t pos = 0;
+        if (valid) {
+            pos = base[d] + r;
+            for (int w = 0; w < wv; ++w) pos += wc[w][d];
+        }
+        __syncthreads();
+        base[tid] += wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
+        wc[0][tid] = 0; wc[1][tid] = 0; wc[2][tid] = 0; wc[3][tid] = 0;
+        __syncthreads();
+        if (valid) { kout[pos] = k; vout[pos] = v; }
+    }
+}
+
+// 1 iff the values are not in ascending order (the pairs come in contig order, so odd k
+// never needs the value sort: its minimizer positions strictly increase)
+__global__ __launch_bounds__(256) void k_unsorted(const uint64_t* v, uint64_t n, int32_t* flag) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (v[i - 1] > v[i]) { *flag = 1; return; }
+}
+// bucket-major sort key: (hash & (2^b-1)) << sh | hash >> b, sh = max(2k - b, 0)
+__global__ __launch_bounds__(256) void k_rot_keys(uint64_t* h, uint64_t n, int b, int sh) {
+    const uint64_t bm = (1ULL << b) - 1;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        h[i] = ((h[i] & bm) << sh) | (h[i] >> b);
+}
+// per pair: run start (1) in the low word, member of a run of >= 2 (1) in the high word
+__global__ __launch_bounds__(256) void k_run_flags(const uint64_t* rk, uint64_t n, uint64_t* fl) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t x = rk[i];
+        const bool st = i == 0 || rk[i - 1] != x, en = i + 1 == n || rk[i + 1] != x;
+        fl[i] = (st ? 1ULL : 0ULL) | ((st && en) ? 0ULL : (1ULL << 32));
+    }
+}
+// scanned flags -> positions of multi runs (P, bucket order) and run starts / their P index
+__global__ __launch_bounds__(256) void k_run_emit(const uint64_t* rk, const uint64_t* val, const uint64_t* sc, uint64_t n,
+                                                  uint64_t* P, uint64_t* rs, uint64_t* rq) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t x = rk[i], e = sc[i];
+        const uint64_t r = e & 0xffffffffULL, q = e >> 32;
+        const bool st = i == 0 || rk[i - 1] != x, en = i + 1 == n || rk[i + 1] != x;
+        if (!(st && en)) P[q] = val[i];
+        if (st) { rs[r] = i; rq[r] = q; }
+    }
+}
+// first run of every bucket (rf[nbk] = R); buckets are the rotated key's top bits
+__global__ __launch_bounds__(256) void k_bucket_first(const uint64_t* rk, const uint64_t* rs, uint64_t R, int sh, uint64_t nbk, uint64_t* rf) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= R; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t bk = r < R ? rk[rs[r]] >> sh : nbk;
+        const uint64_t pb = r ? rk[rs[r - 1]] >> sh : 0;
+        for (uint64_t t = r ? pb + 1 : 0; t <= bk; ++t) rf[t] = r;
+    }
+}
+__global__ __launch_bounds__(256) void k_gather_u64(const uint64_t* src, const uint64_t* ix, uint64_t n, uint64_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = src[ix[i]];
+}
+// finish_bucket's h entries (src/index.rs:77-108), bucket by bucket: (key>>b)<<1 | 1 -> position
+// for a run of one, (key>>b)<<1 -> (offset in the bucket's p) << 32 | n otherwise
+__global__ __launch_bounds__(256) void k_run_entries(const uint64_t* rk, const uint64_t* val, const uint64_t* rs, const uint64_t* rq,
+                                                     uint64_t R, uint64_t n, int sh, const uint64_t* rf, uint64_t* H) {
+    const uint64_t tm = (1ULL << sh) - 1;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = rs[r], len = (r + 1 < R ? rs[r + 1] : n) - i;
+        const uint64_t x = rk[i], bk = x >> sh, top = x & tm;
+        const uint64_t pbase = rq[rf[bk]];
+        H[2 * r] = (top << 1) | (len == 1 ? 1ULL : 0ULL);
+        H[2 * r + 1] = len == 1 ? val[i] : ((rq[r] - pbase) << 32) | len;
+    }
 }
 
 struct Dev {
@@ -178,6 +368,36 @@ int64_t view_warmup(const uint8_t* seq, int64_t c0, int w, int k) {
     }
 }
 
+
+// exclusive scan of n values (in place allowed); part: scratch of ceil(n / SC_CHUNK) T
+template <typename T>
+hipError_t dev_excl_scan(const T* in, T* out, uint64_t n, T* part, hipStream_t st) {
+    const uint32_t np = (uint32_t)((n + SC_CHUNK - 1) / SC_CHUNK);
+    if (np == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scan_reduce<T>, dim3(np), dim3(SC_T), 0, st, in, n, part);
+    hipLaunchKernelGGL(k_scan_parts<T>, dim3(1), dim3(SC_T), 0, st, part, np);
+    hipLaunchKernelGGL(k_scan_down<T>, dim3(np), dim3(SC_T), 0, st, in, out, n, (const T*)part);
+    return hipGetLastError();
+}
+
+// stable LSD radix sort of (k, v) pairs by the low `bits` bits of k, ping-ponging between
+// (k0, v0) and (k1, v1); returns in `flip` whether the result is in (k1, v1)
+hipError_t dev_radix_sort(uint64_t* k0, uint64_t* v0, uint64_t* k1, uint64_t* v1, uint64_t n, int bits, uint32_t* cnt,
+                          uint32_t* part, hipStream_t st, bool& flip) {
+    flip = false;
+    const uint32_t nb = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    for (int sh = 0; sh < bits; sh += 8) {
+        hipLaunchKernelGGL(k_rs_count, dim3(nb), dim3(256), 0, st, (const uint64_t*)k0, n, sh, cnt, nb);
+        if (hipError_t e = dev_excl_scan<uint32_t>(cnt, cnt, 256ull * nb, part, st)) return e;
+        hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(256), 0, st, (const uint64_t*)k0, (const uint64_t*)v0, k1, v1, n, sh,
+                           (const uint32_t*)cnt, nb);
+        if (hipError_t e = hipGetLastError()) return e;
+        std::swap(k0, k1); std::swap(v0, v1);
+        flip = !flip;
+    }
+    return hipSuccess;
+}
+
 inline int bit_width64(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
 inline size_t kroundup64(size_t x) { --x; x |= x >> 1; x |= x >> 2; x |= x >> 4; x |= x >> 8; x |= x >> 16; x |= x >> 32; return x + 1; }
 
@@ -226,8 +446,12 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     if (!d_seq) { err = "hipMalloc(reference) failed"; return false; }
     for (size_t i = 0; i < n; ++i)
         if (lens[i]) IXCHK(hipMemcpyAsync(d_seq + idx.seq[i].offset, seqs[i], lens[i], hipMemcpyHostToDevice, st));
+    if (prof) { IXCHK(hipStreamSynchronize(st)); lap("H2D reference"); }
     int64_t chunk = IX_CHUNK;
     if (const int64_t v = g_index_knob[1].load()) chunk = std::max<int64_t>(256, v);   // MM2G_IKNOB_IXCHUNK (tests)
+    // non-HPC builds sketch the contigs in the query reads' nt4 format (k_pack_nt4): views then
+    // start at a multiple of 8 bases (the warm-up only grows) and view_off is contig-relative
+    const bool nt4 = !(flag & 1);
     std::vector<uint64_t> v_off, v_base, v_end;
     std::vector<uint32_t> v_len, v_pre, v_from, v_rid;
     std::vector<uint8_t> v_last;
@@ -235,23 +459,26 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     for (size_t r = 0; r < n; ++r) {
         const int64_t L = (int64_t)lens[r];
         for (int64_t c0 = 0; c0 < L; c0 += chunk) {
-            const int64_t vs = c0 ? view_warmup(seqs[r], c0, w, k) : 0, ve = std::min<int64_t>(L, c0 + chunk);
-            v_off.push_back(idx.seq[r].offset + (uint64_t)vs);
+            int64_t vs = c0 ? view_warmup(seqs[r], c0, w, k) : 0;
+            const int64_t ve = std::min<int64_t>(L, c0 + chunk);
+            if (nt4) vs &= ~(int64_t)7;
+            v_off.push_back(nt4 ? (uint64_t)vs : idx.seq[r].offset + (uint64_t)vs);
             v_len.push_back((uint32_t)(ve - vs)); v_pre.push_back((uint32_t)vs); v_from.push_back((uint32_t)(c0 - vs));
             v_last.push_back(ve == L ? 1 : 0); v_rid.push_back((uint32_t)r);
-            v_base.push_back(cap); cap += (uint64_t)(ve - vs) + 16; v_end.push_back(cap);
+            // minimizer slots: ~2/(w+1) per base is the usual density; a quarter per base (+256) holds
+            // it, and a view that needs more (homopolymer runs emit at every base) is re-run exactly
+            v_base.push_back(cap); cap += (uint64_t)((ve - vs) >> 2) + 256; v_end.push_back(cap);
         }
     }
     const uint32_t nv = (uint32_t)v_off.size();
-    std::vector<uint32_t> S_host;
-    idx.S.assign(kroundup64((size_t)((total + 7) / 8)), 0u);
-    if (nv == 0) { idx.B.assign((size_t)1 << b, HostBucket()); return true; }
+    if (nv == 0) { idx.S.assign(kroundup64((size_t)((total + 7) / 8)), 0u); idx.B.assign((size_t)1 << b, HostBucket()); return true; }
     uint64_t* d_voff = D.alloc<uint64_t>(nv); uint32_t* d_vlen = D.alloc<uint32_t>(nv); uint32_t* d_vpre = D.alloc<uint32_t>(nv);
     uint32_t* d_vfrom = D.alloc<uint32_t>(nv); uint8_t* d_vlast = D.alloc<uint8_t>(nv); uint32_t* d_vrid = D.alloc<uint32_t>(nv);
     uint64_t* d_vbase = D.alloc<uint64_t>(nv); uint64_t* d_vend = D.alloc<uint64_t>(nv);
     uint64_t* d_mx = D.alloc<uint64_t>(cap); uint32_t* d_my = D.alloc<uint32_t>(cap); uint32_t* d_cnt = D.alloc<uint32_t>(nv);
+    uint32_t* d_need = D.alloc<uint32_t>(nv);
     int32_t* d_ovf = D.alloc<int32_t>(4);
-    if (!d_voff || !d_vlen || !d_vpre || !d_vfrom || !d_vlast || !d_vrid || !d_vbase || !d_vend || !d_mx || !d_my || !d_cnt || !d_ovf) {
+    if (!d_voff || !d_vlen || !d_vpre || !d_vfrom || !d_vlast || !d_vrid || !d_vbase || !d_vend || !d_mx || !d_my || !d_cnt || !d_need || !d_ovf) {
         err = "hipMalloc(index views) failed"; return false;
     }
     IXCHK(hipMemcpyAsync(d_voff, v_off.data(), nv * 8, hipMemcpyHostToDevice, st));
@@ -263,15 +490,42 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     IXCHK(hipMemcpyAsync(d_vbase, v_base.data(), nv * 8, hipMemcpyHostToDevice, st));
     IXCHK(hipMemcpyAsync(d_vend, v_end.data(), nv * 8, hipMemcpyHostToDevice, st));
     IXCHK(hipMemsetAsync(d_ovf, 0, 16, st));
-    // ---- 2. S on the device (overlaps nothing on the host; small)
+    // ---- 2. S (src/index.rs:14-19) on host threads, overlapping the device work below: 8 bases
+    // per u32 word, base j of the concatenation in bits 4(j%8); words past the sequence stay 0
+    struct Joiner { std::thread t; ~Joiner() { if (t.joinable()) t.join(); } } s_pack;
     {
-        uint32_t* d_S = D.alloc<uint32_t>(idx.S.size());
-        if (!d_S) { err = "hipMalloc(S) failed"; return false; }
-        const uint64_t nw = idx.S.size();
-        hipLaunchKernelGGL(k_pack4, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, d_seq, total, nw, d_S);
-        IXCHK(hipGetLastError());
-        IXCHK(hipMemcpyAsync(idx.S.data(), d_S, nw * 4, hipMemcpyDeviceToHost, st));
+        const uint64_t nw = (total + 7) / 8;
+        std::vector<uint32_t>* Sv = &idx.S;
+        s_pack.t = std::thread([&seqs, &lens, Sv, nw, n]() {
+            Sv->assign(kroundup64((size_t)nw), 0u);     // (the zero fill of ~2 GB too, off the main thread)
+            uint32_t* S = Sv->data();
+            static const uint8_t T4[256] = {
+                4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,
+                4,0,4,1,4,4,4,2,4,4,4,4,4,4,4,4, 4,4,4,4,3,4,4,4,4,4,4,4,4,4,4,4, 4,0,4,1,4,4,4,2,4,4,4,4,4,4,4,4, 4,4,4,4,3,4,4,4,4,4,4,4,4,4,4,4,
+                4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,
+                4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4};
+            std::vector<uint64_t> coff(n + 1, 0);
+            for (size_t i = 0; i < n; ++i) coff[i + 1] = coff[i] + lens[i];
+            const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, nw / (1u << 20)));
+            std::vector<std::thread> th;
+            for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() {
+                const uint64_t w0 = nw * t / nt, w1 = nw * (t + 1) / nt;
+                size_t r = (size_t)(std::upper_bound(coff.begin(), coff.end(), w0 * 8) - coff.begin()) - 1;
+                for (uint64_t wd = w0; wd < w1; ++wd) {
+                    uint32_t v = 0;
+                    for (int j = 0; j < 8; ++j) {
+                        const uint64_t p = wd * 8 + (uint64_t)j;
+                        while (r < n && p >= coff[r + 1]) ++r;
+                        if (r >= n) break;
+                        v |= (uint32_t)(T4[seqs[r][p - coff[r]]] & 0xFu) << (4 * j);
+                    }
+                    S[wd] = v;
+                }
+            });
+            for (auto& x : th) x.join();
+        });
     }
+    if (prof) { IXCHK(hipStreamSynchronize(st)); lap("views (S packs on the host)"); }
     // ---- 3. HPC spans (flag & 1), then sketch every view (one wave each)
     uint16_t* d_span = nullptr;
     if (flag & 1) {
@@ -291,106 +545,192 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     SketchArgs sa{d_seq, nullptr, nv, w, k, d_vbase, d_vend, d_mx, d_my, d_cnt, d_ovf};
     sa.view_off = d_voff; sa.view_len = d_vlen; sa.view_pre = d_vpre; sa.emit_from = d_vfrom; sa.view_last = d_vlast;
     sa.hpc_span = d_span;
-    if (launch_sketch(sa, (int)std::min<uint32_t>((nv + 3) / 4, 4096u), st) != 0) { err = "k_sketch launch failed"; return false; }
+    if (nt4) {   // contig r = "read" r of an nt4 batch; view r reads contig v_rid[r]
+        std::vector<uint64_t> coff(n + 1, 0), gs(n + 1, 0), pko(n), ambo(n);
+        uint64_t nwords = 0;
+        for (size_t i = 0; i < n; ++i) {
+            coff[i + 1] = coff[i] + lens[i];
+            const uint64_t ng = (lens[i] + 7) / 8;
+            gs[i + 1] = gs[i] + ng;
+            pko[i] = nwords; nwords += (ng + 3) / 4;       // 4 u16 code words per u64
+            ambo[i] = nwords; nwords += (ng + 7) / 8;      // 8 bitmap bytes per u64
+        }
+        uint64_t* d_coff = D.alloc<uint64_t>(n + 1); uint64_t* d_gs = D.alloc<uint64_t>(n + 1);
+        uint64_t* d_pko = D.alloc<uint64_t>(n); uint64_t* d_ambo = D.alloc<uint64_t>(n);
+        uint64_t* d_words = D.alloc<uint64_t>(nwords + 1);
+        if (!d_coff || !d_gs || !d_pko || !d_ambo || !d_words) { err = "hipMalloc(nt4 reference) failed"; return false; }
+        IXCHK(hipMemcpyAsync(d_coff, coff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        IXCHK(hipMemcpyAsync(d_gs, gs.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        IXCHK(hipMemcpyAsync(d_pko, pko.data(), n * 8, hipMemcpyHostToDevice, st));
+        IXCHK(hipMemcpyAsync(d_ambo, ambo.data(), n * 8, hipMemcpyHostToDevice, st));
+        const unsigned nb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((gs[n] + 255) / 256, 65536));
+        hipLaunchKernelGGL(k_pack_nt4, dim3(nb), dim3(256), 0, st, d_seq, d_coff, d_gs, (uint32_t)n, gs[n], d_pko, d_ambo, d_words);
+        IXCHK(hipGetLastError());
+        sa.pk_words = d_words; sa.pk_off = d_pko; sa.amb_off = d_ambo; sa.view_read = d_vrid;
+    }
+    sa.mz_need = d_need;
     std::vector<uint32_t> cnt(nv);
-    int32_t ovf = 0;
-    IXCHK(hipMemcpyAsync(cnt.data(), d_cnt, nv * 4, hipMemcpyDeviceToHost, st));
-    IXCHK(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
-    IXCHK(hipStreamSynchronize(st));
-    if (ovf) { unsupported = true; err = "GPU index build: minimizer slot overflow (host build)"; return false; }
-    lap("H2D + S + sketch");
+    for (int pass = 0;; ++pass) {
+        if (launch_sketch(sa, (int)std::min<uint32_t>((nv + 3) / 4, 4096u), st) != 0) { err = "k_sketch launch failed"; return false; }
+        int32_t ovf = 0;
+        IXCHK(hipMemcpyAsync(cnt.data(), d_cnt, nv * 4, hipMemcpyDeviceToHost, st));
+        IXCHK(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
+        IXCHK(hipStreamSynchronize(st));
+        if (!ovf) break;
+        if (pass) { unsupported = true; err = "GPU index build: minimizer slot overflow (host build)"; return false; }
+        // a view outgrew its slot: every view again with exactly its own count (mz_need)
+        IXCHK(hipMemcpy(cnt.data(), d_need, nv * 4, hipMemcpyDeviceToHost));
+        cap = 0;
+        for (uint32_t v = 0; v < nv; ++v) { v_base[v] = cap; cap += (uint64_t)cnt[v] + 16; v_end[v] = cap; }
+        d_mx = D.alloc<uint64_t>(cap); d_my = D.alloc<uint32_t>(cap);
+        if (!d_mx || !d_my) { err = "hipMalloc(index minimizers) failed"; return false; }
+        IXCHK(hipMemcpyAsync(d_vbase, v_base.data(), nv * 8, hipMemcpyHostToDevice, st));
+        IXCHK(hipMemcpyAsync(d_vend, v_end.data(), nv * 8, hipMemcpyHostToDevice, st));
+        IXCHK(hipMemsetAsync(d_ovf, 0, 16, st));
+        sa.mz_x = d_mx; sa.mz_y = d_my;
+    }
+    lap("sketch");
     std::vector<uint64_t> ooff(nv);
     uint64_t M = 0;
     for (uint32_t v = 0; v < nv; ++v) { ooff[v] = M; M += cnt[v]; }
-    // ---- 4. pairs, then sort by (hash, value)
+    if (M >= (1ULL << 32)) { unsupported = true; err = "GPU index build: 2^32 or more minimizers (host build)"; return false; }
+    if (M == 0) { idx.B.assign((size_t)1 << b, HostBucket()); return true; }
+    // ---- 4. pairs (contig order), then sorted by (bucket, hash, value) on the device
     uint64_t* d_ooff = D.alloc<uint64_t>(nv);
     uint64_t* h0 = D.alloc<uint64_t>(M); uint64_t* v0 = D.alloc<uint64_t>(M);
     uint64_t* h1 = D.alloc<uint64_t>(M); uint64_t* v1 = D.alloc<uint64_t>(M);
-    if (!d_ooff || !h0 || !v0 || !h1 || !v1) { err = "hipMalloc(index pairs) failed"; return false; }
+    const uint32_t rnb = (uint32_t)((M + RS_TILE - 1) / RS_TILE);
+    uint32_t* d_cnt8 = D.alloc<uint32_t>(256ull * rnb);
+    uint32_t* d_part32 = D.alloc<uint32_t>(256ull * rnb / SC_CHUNK + 2);
+    uint64_t* d_part64 = D.alloc<uint64_t>(M / SC_CHUNK + 2);
+    int32_t* d_flag = D.alloc<int32_t>(1);
+    if (!d_ooff || !h0 || !v0 || !h1 || !v1 || !d_cnt8 || !d_part32 || !d_part64 || !d_flag) { err = "hipMalloc(index pairs) failed"; return false; }
     IXCHK(hipMemcpyAsync(d_ooff, ooff.data(), nv * 8, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_ix_compact, dim3((nv + 3) / 4), dim3(256), 0, st, nv, d_vbase, d_cnt, d_mx, d_my, d_vrid, d_vpre, d_ooff, h0, v0);
     IXCHK(hipGetLastError());
+    if (prof) { IXCHK(hipStreamSynchronize(st)); lap("pairs"); }
     const int vbits = 32 + std::max(1, bit_width64(n ? n - 1 : 0)), hbits = 2 * k;
-    size_t tb1 = 0, tb2 = 0;
-    IXCHK(rocprim::radix_sort_pairs(nullptr, tb1, v0, v1, h0, h1, (size_t)M, 0, vbits, st));
-    IXCHK(rocprim::radix_sort_pairs(nullptr, tb2, h1, h0, v1, v0, (size_t)M, 0, hbits, st));
-    void* tmp = D.alloc<uint8_t>(std::max(tb1, tb2));
-    if (!tmp) { err = "hipMalloc(sort scratch) failed"; return false; }
-    size_t tb = std::max(tb1, tb2);
-    IXCHK(rocprim::radix_sort_pairs(tmp, tb, v0, v1, h0, h1, (size_t)M, 0, vbits, st));   // by value (stable)
-    tb = std::max(tb1, tb2);
-    IXCHK(rocprim::radix_sort_pairs(tmp, tb, h1, h0, v1, v0, (size_t)M, 0, hbits, st));   // then by hash
-    // pinned staging: the two sorted arrays come back at PCIe rate
-    uint64_t *hh = nullptr, *vv = nullptr;
-    IXCHK(hipHostMalloc((void**)&hh, std::max<uint64_t>(M, 1) * 8, hipHostMallocDefault));
-    struct PinGuard { uint64_t* p; ~PinGuard() { if (p) (void)hipHostFree(p); } } g1{hh};
-    IXCHK(hipHostMalloc((void**)&vv, std::max<uint64_t>(M, 1) * 8, hipHostMallocDefault));
-    PinGuard g2{vv};
+    const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((M + 255) / 256, 65536));
+    // post_process orders each hash's positions; the pairs arrive in contig order, so only a
+    // value out of order (possible for even k) needs the stable sort by value first
+    int32_t unsorted = 0;
+    IXCHK(hipMemsetAsync(d_flag, 0, 4, st));
+    hipLaunchKernelGGL(k_unsorted, dim3(gs), dim3(256), 0, st, (const uint64_t*)v0, M, d_flag);
+    IXCHK(hipMemcpyAsync(&unsorted, d_flag, 4, hipMemcpyDeviceToHost, st));
     IXCHK(hipStreamSynchronize(st));
-    lap("pairs + 2 radix sorts");
-    IXCHK(hipMemcpyAsync(hh, h0, M * 8, hipMemcpyDeviceToHost, st));
-    IXCHK(hipMemcpyAsync(vv, v0, M * 8, hipMemcpyDeviceToHost, st));
+    if (g_index_knob[6].load()) unsorted = 1;   // MM2G_IKNOB_IXSORTV (tests)
+    bool flip = false;
+    if (unsorted) {
+        IXCHK(dev_radix_sort(v0, h0, v1, h1, M, vbits, d_cnt8, d_part32, st, flip));
+        if (flip) { std::swap(h0, h1); std::swap(v0, v1); }
+    }
+    // bucket-major key: the .mmi and the host index keep every bucket's keys in hash order
+    const int rsh = hbits > b ? hbits - b : 0;
+    const uint64_t nbk = (uint64_t)1 << b;
+    hipLaunchKernelGGL(k_rot_keys, dim3(gs), dim3(256), 0, st, h0, M, b, rsh);
+    IXCHK(dev_radix_sort(h0, v0, h1, v1, M, hbits, d_cnt8, d_part32, st, flip));
+    if (flip) { std::swap(h0, h1); std::swap(v0, v1); }
+    if (prof) { IXCHK(hipStreamSynchronize(st)); lap(unsorted ? "radix sorts (value, hash)" : "radix sort (hash)"); }
+    // ---- 5. runs -> finish_bucket's h and p (src/index.rs:77-108), bucket by bucket, on the device
+    uint64_t* fl = h1;                // free after the sort
+    uint64_t* sc = v1;
+    hipLaunchKernelGGL(k_run_flags, dim3(gs), dim3(256), 0, st, (const uint64_t*)h0, M, fl);
+    IXCHK(hipGetLastError());
+    IXCHK(dev_excl_scan<uint64_t>(fl, sc, M, d_part64, st));
+    uint64_t lastf = 0, lasts = 0;
+    IXCHK(hipMemcpyAsync(&lastf, fl + (M - 1), 8, hipMemcpyDeviceToHost, st));
+    IXCHK(hipMemcpyAsync(&lasts, sc + (M - 1), 8, hipMemcpyDeviceToHost, st));
     IXCHK(hipStreamSynchronize(st));
-    lap("D2H pairs (pinned)");
-    // ---- 5. runs -> buckets (finish_bucket's h and p, src/index.rs:77-108).
-    // Threads take contiguous hash ranges cut at run starts; per (thread, bucket)
-    // counts give every thread its slice of each bucket's h and p, so runs land
-    // in hash order exactly as the serial distribution would place them.
-    const size_t nb = (size_t)1 << b;
-    const uint64_t bmask = nb - 1;
-    int nt = (int)std::min<uint64_t>(std::max(1u, std::thread::hardware_concurrency()), 32);
+    const uint64_t R = (lasts & 0xffffffffULL) + (lastf & 0xffffffffULL), PT = (lasts >> 32) + (lastf >> 32);
+    uint64_t* dP = D.alloc<uint64_t>(PT); uint64_t* rs = D.alloc<uint64_t>(R); uint64_t* rq = D.alloc<uint64_t>(R + 1);
+    uint64_t* rf = D.alloc<uint64_t>(nbk + 1); uint64_t* pb = D.alloc<uint64_t>(nbk + 1); uint64_t* dH = D.alloc<uint64_t>(2 * R);
+    if (!dP || !rs || !rq || !rf || !pb || !dH) { err = "hipMalloc(index buckets) failed"; return false; }
+    IXCHK(hipMemcpyAsync(rq + R, &PT, 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_run_emit, dim3(gs), dim3(256), 0, st, (const uint64_t*)h0, (const uint64_t*)v0, (const uint64_t*)sc, M, dP, rs, rq);
+    const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((R + 256) / 256, 65536));
+    hipLaunchKernelGGL(k_bucket_first, dim3(gr), dim3(256), 0, st, (const uint64_t*)h0, (const uint64_t*)rs, R, rsh, nbk, rf);
+    hipLaunchKernelGGL(k_gather_u64, dim3((unsigned)((nbk + 256) / 256)), dim3(256), 0, st, (const uint64_t*)rq, (const uint64_t*)rf, nbk + 1, pb);
+    hipLaunchKernelGGL(k_run_entries, dim3(gr), dim3(256), 0, st, (const uint64_t*)h0, (const uint64_t*)v0, (const uint64_t*)rs,
+                       (const uint64_t*)rq, R, M, rsh, (const uint64_t*)rf, dH);
+    IXCHK(hipGetLastError());
+    std::vector<uint64_t> hrf(nbk + 1), hpb(nbk + 1);
+    IXCHK(hipMemcpyAsync(hrf.data(), rf, (nbk + 1) * 8, hipMemcpyDeviceToHost, st));
+    IXCHK(hipMemcpyAsync(hpb.data(), pb, (nbk + 1) * 8, hipMemcpyDeviceToHost, st));
+    IXCHK(hipStreamSynchronize(st));
+    lap("runs -> buckets (device)");
+    // ---- 6. the buckets' h and p to the host: every thread sizes its share of the buckets,
+    // then copies its slice of H and of P through its own pinned buffer and stream
+    int nt = (int)std::min<uint64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
     if (M < (1u << 16)) nt = 1;
-    std::vector<uint64_t> cut(nt + 1, M);
-    cut[0] = 0;
-    for (int t = 1; t < nt; ++t) {
-        uint64_t c = M * (uint64_t)t / (uint64_t)nt;
-        while (c > 0 && c < M && hh[c] == hh[c - 1]) ++c;
-        cut[t] = std::max(c, cut[t - 1]);
-    }
-    std::vector<std::vector<uint64_t>> cnt_h(nt, std::vector<uint64_t>(nb, 0)), cnt_p(nt, std::vector<uint64_t>(nb, 0));
-    auto run_threads = [&](auto fn) {
+    idx.B.assign(nbk, HostBucket());
+    {
         std::vector<std::thread> th;
-        for (int t = 0; t < nt; ++t) th.emplace_back(fn, t);
-        for (auto& x : th) x.join();
-    };
-    run_threads([&](int t) {
-        for (uint64_t s = cut[t]; s < cut[t + 1];) {
-            uint64_t e = s + 1;
-            while (e < cut[t + 1] && hh[e] == hh[s]) ++e;
-            const size_t bk = (size_t)(hh[s] & bmask);
-            cnt_h[t][bk] += 1; if (e - s > 1) cnt_p[t][bk] += e - s;
-            s = e;
-        }
-    });
-    idx.B.assign(nb, HostBucket());
-    for (size_t bk = 0; bk < nb; ++bk) {   // exclusive offsets per (thread, bucket)
-        uint64_t oh = 0, op = 0;
-        for (int t = 0; t < nt; ++t) {
-            const uint64_t ch = cnt_h[t][bk], cp = cnt_p[t][bk];
-            cnt_h[t][bk] = oh; cnt_p[t][bk] = op; oh += ch; op += cp;
-        }
-        idx.B[bk].h.resize(oh); idx.B[bk].p.resize(op);
-        idx.B[bk].has_h = oh > 0;
-    }
-    run_threads([&](int t) {
-        std::vector<uint64_t>& oh = cnt_h[t];
-        std::vector<uint64_t>& op = cnt_p[t];
-        for (uint64_t s = cut[t]; s < cut[t + 1];) {
-            uint64_t e = s + 1;
-            while (e < cut[t + 1] && hh[e] == hh[s]) ++e;
-            const size_t bk = (size_t)(hh[s] & bmask);
-            HostBucket& B = idx.B[bk];
-            const uint64_t key_top = (hh[s] >> b) << 1;
-            if (e - s == 1) B.h[oh[bk]++] = {key_top | 1, vv[s]};
-            else {
-                B.h[oh[bk]++] = {key_top, (op[bk] << 32) | (uint64_t)(e - s)};
-                std::copy(vv + s, vv + e, B.p.begin() + (ptrdiff_t)op[bk]);
-                op[bk] += e - s;
+        for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() {
+            for (uint64_t bk = nbk * t / nt; bk < nbk * (t + 1) / nt; ++bk) {
+                HostBucket& B = idx.B[bk];
+                B.h.resize(hrf[bk + 1] - hrf[bk]);
+                B.p.resize(hpb[bk + 1] - hpb[bk]);
+                B.has_h = !B.h.empty();
             }
-            s = e;
-        }
-    });
-    lap("host bucket distribution");
+        });
+        for (auto& x : th) x.join();
+    }
+    lap("host buckets sized");
+    constexpr uint64_t PIN_WORDS = 1u << 22;            // 32 MB per thread
+    std::vector<std::string> errs(nt);
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() {
+            auto fail = [&](const char* what, hipError_t e) { errs[t] = std::string(what) + ": " + hipGetErrorString(e); };
+            if (hipError_t e = hipSetDevice(device)) { fail("hipSetDevice", e); return; }
+            hipStream_t ts;
+            if (hipError_t e = hipStreamCreateWithFlags(&ts, hipStreamNonBlocking)) { fail("hipStreamCreate", e); return; }
+            uint64_t* pin = nullptr;
+            if (hipError_t e = hipHostMalloc((void**)&pin, PIN_WORDS * 8, hipHostMallocDefault)) { fail("hipHostMalloc", e); (void)hipStreamDestroy(ts); return; }
+            // words [a, z) of a device array through the pinned buffer; place(first word, host words, count)
+            auto pull = [&](const uint64_t* src, uint64_t a, uint64_t z, auto place) -> bool {
+                for (uint64_t c = a; c < z; c += PIN_WORDS) {
+                    const uint64_t m = std::min<uint64_t>(PIN_WORDS, z - c);
+                    hipError_t e = hipMemcpyAsync(pin, src + c, m * 8, hipMemcpyDeviceToHost, ts);
+                    if (!e) e = hipStreamSynchronize(ts);
+                    if (e) { fail("D2H buckets", e); return false; }
+                    place(c, pin, m);
+                }
+                return true;
+            };
+            // H: entries (2 words) [e0, e1) of this thread, into the buckets they belong to
+            const uint64_t e0 = R * t / nt, e1 = R * (t + 1) / nt;
+            bool ok = pull(dH, 2 * e0, 2 * e1, [&](uint64_t c, const uint64_t* hw, uint64_t m) {
+                uint64_t e = c / 2;
+                const uint64_t ee = (c + m) / 2;
+                size_t bk = (size_t)(std::upper_bound(hrf.begin(), hrf.end(), e) - hrf.begin()) - 1;
+                while (e < ee) {
+                    while (hrf[bk + 1] <= e) ++bk;
+                    const uint64_t q = std::min(ee, hrf[bk + 1]) - e;
+                    memcpy((void*)(idx.B[bk].h.data() + (e - hrf[bk])), hw + 2 * (e - c / 2), q * 16);
+                    e += q;
+                }
+            });
+            const uint64_t p0 = PT * t / nt, p1 = PT * (t + 1) / nt;
+            if (ok) ok = pull(dP, p0, p1, [&](uint64_t c, const uint64_t* pw, uint64_t m) {
+                uint64_t e = c;
+                size_t bk = (size_t)(std::upper_bound(hpb.begin(), hpb.end(), e) - hpb.begin()) - 1;
+                while (e < c + m) {
+                    while (hpb[bk + 1] <= e) ++bk;
+                    const uint64_t q = std::min(c + m, hpb[bk + 1]) - e;
+                    memcpy(idx.B[bk].p.data() + (e - hpb[bk]), pw + (e - c), q * 8);
+                    e += q;
+                }
+            });
+            (void)hipHostFree(pin);
+            (void)hipStreamDestroy(ts);
+        });
+        for (auto& x : th) x.join();
+    }
+    for (const std::string& e : errs) if (!e.empty()) { err = e; return false; }
+    lap("D2H buckets (pinned, threads)");
+    if (s_pack.t.joinable()) s_pack.t.join();
+    lap("S (host threads) joined");
     return true;
 }
 

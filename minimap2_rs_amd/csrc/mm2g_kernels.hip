@@ -207,6 +207,7 @@ struct SeqAscii {
     DEVI uint64_t raw(int64_t p0) const { return load_bases8(s, p0, L); }
     DEVI void decode(uint64_t v, uint32_t& code16, uint32_t& valid8) const { codes8(v, code16, valid8); }
     DEVI uint32_t code(int64_t p) const { return nt4d(s[p]); }
+    DEVI bool amb8(int64_t) const { return false; }
 };
 DEVI uint32_t rev2_16(uint32_t x) {
     x = ((x >> 2) & 0x3333u) | ((x & 0x3333u) << 2);
@@ -230,6 +231,8 @@ struct SeqNt4 {
         if (am && ((am[p >> 3] >> (p & 7)) & 1u)) return 4u;
         return ((uint32_t)s2[p >> 3] >> (2 * (p & 7))) & 3u;
     }
+    // the 8 bases at p8 (a multiple of 8) are all ambiguous (a walk-back steps over N runs 8 at a time)
+    DEVI bool amb8(int64_t p8) const { return am && am[p8 >> 3] == 0xffu; }
     // 8 bases at p0 < 0 (a multiple of 8) of a query view: the read's bases before the view
     DEVI uint64_t raw_back(int64_t p0) const {
         const uint64_t v = s2[p0 >> 3], m = am ? am[p0 >> 3] : 0u;
@@ -241,7 +244,8 @@ struct SeqNt4 {
 // ~0u stays free for "no info"); every x = hash << 8 | k then, so x and hash order alike
 template <bool K32, typename Src, bool HPC = false, bool X32 = false>
 // waves per SIMD (override with -D): the query sketch (nt4) at 96 VGPRs 5; the index build
-// (ASCII) at 128 4; the 32-bit window (X32) at 80 VGPRs 6 (no spills)
+// (ASCII) at 128 4 (also with the 32-bit window: at 80 VGPRs its byte loads and decode spilled
+// 57 VGPRs, the build's sketch wrote ~23 GB of scratch); the query's 32-bit window (X32) at 80 VGPRs 6
 #ifndef SK_WPE_NT4
 #define SK_WPE_NT4 5
 #endif
@@ -251,7 +255,7 @@ template <bool K32, typename Src, bool HPC = false, bool X32 = false>
 #ifndef SK_WPE_X32
 #define SK_WPE_X32 6
 #endif
-__global__ __launch_bounds__(256, X32 ? SK_WPE_X32 : (std::is_same<Src, SeqNt4>::value ? SK_WPE_NT4 : SK_WPE_ASCII)) void k_sketch(SketchArgs a) {
+__global__ __launch_bounds__(256, (!std::is_same<Src, SeqNt4>::value ? SK_WPE_ASCII : (X32 ? SK_WPE_X32 : SK_WPE_NT4))) void k_sketch(SketchArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     static_assert(!X32 || (K32 && !HPC), "X32: k <= 15 query/index sketch without HPC spans");
     using XT = typename std::conditional<X32, uint32_t, uint64_t>::type;
@@ -302,6 +306,7 @@ __global__ __launch_bounds__(256, X32 ? SK_WPE_X32 : (std::is_same<Src, SeqNt4>:
         uint64_t count = 0;
         uint32_t n_tiles = 0, n_slow = 0;      // MM2G_SKETCH_PROF: tiles, tiles on the exact (2-pass) step path
         int32_t l_carry = 0;
+        uint64_t ckf = 0, ckr = 0;             // k-mer registers at the end of the previous tile
         // bases of this lane's chunk, prefetched one tile ahead; lanes 0-3 also
         // keep the previous tile's last 32 bases (codes | reversed validity << 16)
         uint32_t code16, valid8;
@@ -352,12 +357,46 @@ __global__ __launch_bounds__(256, X32 ? SK_WPE_X32 : (std::is_same<Src, SeqNt4>:
                 const bool slow = ps < pe && (ps + pre < k - 1 || (V & need_bits) != need_bits);
                 kf = W & ((k - 1 >= 32) ? U64MAX : ((1ULL << (2 * (k - 1))) - 1));
                 kr = (rev2_64(~W) >> (64 - 2 * k)) & ~3ULL;
-                if (any(slow)) {
+                if (any(slow) && t0 > 0) {
+                    // after the first tile: the registers at the previous tile's end (ckf, ckr, exact)
+                    // with the valid bases of the chunks before this lane's shifted in -- an exclusive
+                    // wave scan of (last 32 valid codes, count), so no lane walks back over HBM
+                    // (an N gap of the index build's contigs had every lane of every tile in it
+                    // walk back to its start, base by base)
+                    uint64_t pc = 0; uint32_t pn = 0;
+#pragma unroll
+                    for (int u = 0; u < SK_CH; ++u) {
+                        const bool vu = (valid8 >> u) & 1u;
+                        pc = vu ? (pc << 2) | ((code16 >> (2 * (7 - u))) & 3u) : pc;
+                        pn += vu ? 1u : 0u;
+                    }
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t olo = (uint32_t)__shfl_up((int)(uint32_t)pc, d, 64), ohi = (uint32_t)__shfl_up((int)(uint32_t)(pc >> 32), d, 64);
+                        const uint32_t on = (uint32_t)__shfl_up((int)pn, d, 64);
+                        if (ln >= d && pn < 32) { pc = ((((uint64_t)ohi << 32) | olo) << (2 * pn)) | pc; pn = min(32u, pn + on); }
+                    }
+                    {   // exclusive
+                        const uint32_t olo = (uint32_t)__shfl_up((int)(uint32_t)pc, 1, 64), ohi = (uint32_t)__shfl_up((int)(uint32_t)(pc >> 32), 1, 64);
+                        const uint32_t on = (uint32_t)__shfl_up((int)pn, 1, 64);
+                        pc = ln ? ((uint64_t)ohi << 32) | olo : 0; pn = ln ? on : 0u;
+                    }
+                    const uint64_t rc = rev2_64(~pc) >> (64 - 2 * k);   // complements, the newest at the top slot
+                    if (pn >= (uint32_t)k) { kf = pc & mask; kr = rc; }
+                    else {
+                        const uint64_t low = (1ULL << (2 * (k - pn))) - 1;
+                        kf = ((ckf << (2 * pn)) | pc) & mask;
+                        kr = (ckr >> (2 * pn)) | (rc & ~low);
+                    }
+                } else if (any(slow)) {
                     if (slow) { kf = 0; kr = 0; }
                     int64_t wsp = ps;
                     int need = slow ? k - 1 : 0;
                     while (any(need > 0 && wsp > -pre)) {   // back to the contig start (views: before the view)
-                        if (need > 0 && wsp > -pre) { --wsp; if (src.code(wsp) < 4) --need; }
+                        if (need > 0 && wsp > -pre) {
+                            if ((wsp & 7) == 0 && wsp - 8 >= -pre && src.amb8(wsp - 8)) wsp -= 8;   // an N run, 8 at a time
+                            else { --wsp; if (src.code(wsp) < 4) --need; }
+                        }
                     }
                     int64_t pw = slow ? wsp : ps;
                     while (any(pw < ps)) {
@@ -410,6 +449,7 @@ __global__ __launch_bounds__(256, X32 ? SK_WPE_X32 : (std::is_same<Src, SeqNt4>:
                 rs |= r0;
                 lc = r0 ? 0 : ((in && fl == 2u) ? (lc + 1 < CAP ? lc + 1 : CAP) : lc);
             }
+            ckf = uni64(__shfl((uint64_t)kf2, 63, 64)); ckr = uni64(__shfl((uint64_t)kr2, 63, 64));
             // ---- segmented scan of l over lanes: (reset, count)
             int32_t er, ec;
             {

@@ -47,11 +47,11 @@ def test_shard_map_vs_oracle_cli(tmp_path, world, fmt):
     reads = str(tmp_path / "reads.fa")
     simdata.write_genome("hg38", 0.002, 41, ref)           # 24 contigs, ~6 Mb, hg38-shaped repeats
     simdata.write_reads(ref, 600, 5000, 42, reads)
-    if fmt == "fq":
+    want = subprocess.run([MM2RS_CPU, "align", ref, reads], check=True, capture_output=True, timeout=300).stdout
+    if fmt == "fq":        # the same records as FASTQ (the oracle CLI reads FASTA only)
         fq = str(tmp_path / "reads.fq")
         _fastq(fq, reads)
         reads = fq
-    want = subprocess.run([MM2RS_CPU, "align", ref, reads], check=True, capture_output=True, timeout=300).stdout
     out, rep = str(tmp_path / "out.paf"), str(tmp_path / "rep.json")
     p = subprocess.run([sys.executable, "-m", "minimap2_rs_amd.shard", ref, reads, "-o", out, "--gpus", str(world),
                         "--batch-reads", "128", "--report", rep], cwd=ROOT, env=_env(), capture_output=True, text=True,

@@ -434,8 +434,8 @@ def _mmi_bytes(idx, path):
     return open(path, "rb").read()
 
 
-@pytest.mark.parametrize("chunk", [None, 4096, 300])
-def test_gpu_index_build(tmp_path, chunk):
+@pytest.mark.parametrize("chunk,sortv", [(None, 0), (4096, 1), (300, 0)])
+def test_gpu_index_build(tmp_path, chunk, sortv):
     """GPU index build (sketch views, pair sort, bucket distribution, packed S)
     equals the oracle's build_index_from_fasta + save_to_mmi (index.rs:74-109,
     233-307) byte for byte (.mmi), with stats and calc_mid_occ (index.rs:
@@ -446,7 +446,10 @@ def test_gpu_index_build(tmp_path, chunk):
     to grow past its default; HPC (flag 1: TinyQueue spans, sketch.rs:51-64)
     with homopolymer runs up to 400 bases (spans >= 256 give no info).  The build must run on the device
     (MM2G_IKNOB_GPU_STRICT: no host fallback).  The product's host build must
-    agree as well."""
+    agree as well.  The device pair sort is the hand-written radix; sortv=1 forces its
+    stable value pass too (otherwise only taken when the pairs arrive out of value
+    order), and w/k with over a quarter minimizer per base ((3, 2), (2, 3)) outgrow
+    the first per-view slots, so the sketch re-runs with exact slots."""
     rng = random.Random(11)
     names, lens, gbuf = simdata.genome("hg38", 0.0006, 5)
     seqs = [gbuf[int(o):int(o + l)].tobytes() for o, l in zip(np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)]
@@ -475,6 +478,7 @@ def test_gpu_index_build(tmp_path, chunk):
     seqs.append(bytes(hp)); names.append("homopolymers")
     M.set_index_knob("ixchunk", chunk or 0)
     M.set_index_knob("gpu_strict", 1)
+    M.set_index_knob("ixsortv", sortv)
     try:
         buf = np.frombuffer(b"".join(seqs), dtype=np.uint8)
         lv = np.array([len(x) for x in seqs], dtype=np.uint64)
@@ -494,6 +498,7 @@ def test_gpu_index_build(tmp_path, chunk):
     finally:
         M.set_index_knob("ixchunk", 0)
         M.set_index_knob("gpu_strict", 0)
+        M.set_index_knob("ixsortv", 0)
 
 
 def test_cli_align_devices(small_world, tmp_path):

@@ -259,3 +259,9 @@ def test_read_range_partitions_records(tmp_path, fmt):
     open(empty, "wb").close()
     nm, buf, offs = read_range(empty, 0, 2)
     assert nm == [] and len(offs) == 1
+
+
+def test_read_names_unique_over_ranks():
+    """bench.py's parity check gathers every rank's sampled PAF into one dict keyed by read name."""
+    names = {bench.read_name(r, b, i) for r in range(8) for b in range(3) for i in range(50)}
+    assert len(names) == 8 * 3 * 50 and bench.read_name(0, 2, 7) == "r2_7"

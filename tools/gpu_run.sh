@@ -19,6 +19,7 @@
 #   sq      one SQ counter pass (stall shares, LDS bank conflicts), 1 stream
 #   ab      alternate bench runs of knob sets: AB="sort_lds_kb=157|sort_lds_kb=128" N=3
 #   abdir   alternate quick bench runs of whole trees (same box): DIRS=". .ab/r02" N=2
+#   ixb     GPU index build of the hg38-shaped reference, phase times (IXFLAGS="0 0 1")
 # Outputs: gpurun_out/<TAG>/ (TAG defaults to "run").
 set -euo pipefail
 STEPS_ARG=${1:?steps}
@@ -107,6 +108,8 @@ for S in "${STEPS[@]}"; do
           echo "[$D] $(line "$OUT/abd_${nm}_$i.json")" | tee -a "$OUT/abdir.txt"
         done
       done ;;
+    ixb)
+      timeout -k 10 300 python -u tools/ixbuild_hpc_time.py ${IXFLAGS:-0 0 1} > "$OUT/ixb.json" 2> "$OUT/ixb.err"; cat "$OUT/ixb.json"; grep ixbuild "$OUT/ixb.err" || true ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
   echo "step $S done" >> "$OUT/progress.txt"
