@@ -433,7 +433,7 @@ int mm2g_index_release_tables(mm2g_index* idx) {
     if (idx->released) return 0;
     idx->h.stats(idx->st_keys, idx->st_occ, idx->st_spacing, idx->st_total);
     std::vector<HostBucket>().swap(idx->h.B);
-    std::vector<uint32_t>().swap(idx->h.S);
+    SVec().swap(idx->h.S);
     idx->released = true;
     return 0;
 }

@@ -2,7 +2,9 @@
 #pragma once
 #include <atomic>
 #include <stdint.h>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace mm2g {
@@ -36,6 +38,18 @@ bool host_sketch(const uint8_t* seq, size_t len, int w, int k, uint32_t rid, boo
 
 struct HostSeq { bool has_name; std::string name; uint64_t offset; uint32_t len; };
 
+// An allocator whose resize leaves new elements uninitialised (no zero fill of the
+// ~2 GB S of hg38 on one thread); every writer of S fills all of it.
+template <typename T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <typename U> struct rebind { using other = DefaultInitAlloc<U>; };
+    DefaultInitAlloc() = default;
+    template <typename U> DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <typename U> void construct(U* p) noexcept { ::new ((void*)p) U; }
+    template <typename U, typename... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+using SVec = std::vector<uint32_t, DefaultInitAlloc<uint32_t>>;
+
 // Bucket b of the reference Index (src/index.rs:31): `p` plus the hash table
 // `h`, kept here as (key, value) pairs sorted by key.
 struct HostBucket {
@@ -48,7 +62,7 @@ struct HostIndex {
     int32_t w = 0, k = 0, b = 0, flag = 0;
     uint32_t n_seq = 0;
     std::vector<HostSeq> seq;
-    std::vector<uint32_t> S;               // 4-bit packed reference (index.rs:14-19)
+    SVec S;                                // 4-bit packed reference (index.rs:14-19)
     std::vector<HostBucket> B;
     uint32_t max_len = 0;
 

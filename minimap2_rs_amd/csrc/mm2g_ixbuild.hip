@@ -495,10 +495,12 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
     struct Joiner { std::thread t; ~Joiner() { if (t.joinable()) t.join(); } } s_pack;
     {
         const uint64_t nw = (total + 7) / 8;
-        std::vector<uint32_t>* Sv = &idx.S;
+        SVec* Sv = &idx.S;
         s_pack.t = std::thread([&seqs, &lens, Sv, nw, n]() {
-            Sv->assign(kroundup64((size_t)nw), 0u);     // (the zero fill of ~2 GB too, off the main thread)
+            const size_t nall = kroundup64((size_t)nw);
+            Sv->resize(nall);                           // uninitialised (SVec): the threads write every word
             uint32_t* S = Sv->data();
+            std::fill(S + nw, S + nall, 0u);            // kroundup64 padding
             static const uint8_t T4[256] = {
                 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,
                 4,0,4,1,4,4,4,2,4,4,4,4,4,4,4,4, 4,4,4,4,3,4,4,4,4,4,4,4,4,4,4,4, 4,0,4,1,4,4,4,2,4,4,4,4,4,4,4,4, 4,4,4,4,3,4,4,4,4,4,4,4,4,4,4,4,
@@ -506,7 +508,7 @@ bool build_index_gpu(int device, const std::vector<const uint8_t*>& seqs, const 
                 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4, 4,4,4,4,4,4,4,4,4,4,4,4,4,4,4,4};
             std::vector<uint64_t> coff(n + 1, 0);
             for (size_t i = 0; i < n; ++i) coff[i + 1] = coff[i] + lens[i];
-            const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>(8, nw / (1u << 20)));
+            const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>(16, nw / (1u << 20)));
             std::vector<std::thread> th;
             for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() {
                 const uint64_t w0 = nw * t / nt, w1 = nw * (t + 1) / nt;

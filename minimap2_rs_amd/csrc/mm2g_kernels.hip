@@ -159,9 +159,9 @@ __host__ __device__ inline size_t sketch_wave_slots(int w) {
     const size_t nb = (size_t)SK_TS + (size_t)w;
     return nb + (nb >> 3) + 1;
 }
-__host__ __device__ inline size_t sketch_wave_lds(int w) {
+__host__ __device__ inline size_t sketch_wave_lds(int w) {   // + 16 B: the k-mer registers carried from the previous tile
     const size_t pnb = sketch_wave_slots(w);
-    return ((pnb * 8 + pnb * 2) + 15) & ~(size_t)15;
+    return (((pnb * 8 + pnb * 2) + 15) & ~(size_t)15) + 16;
 }
 
 // reverse the order of the 32 2-bit groups of x
@@ -306,7 +306,8 @@ __global__ __launch_bounds__(256, (!std::is_same<Src, SeqNt4>::value ? SK_WPE_AS
         uint64_t count = 0;
         uint32_t n_tiles = 0, n_slow = 0;      // MM2G_SKETCH_PROF: tiles, tiles on the exact (2-pass) step path
         int32_t l_carry = 0;
-        uint64_t ckf = 0, ckr = 0;             // k-mer registers at the end of the previous tile
+        // k-mer registers at the end of the previous tile, in LDS (held in registers they cost spills)
+        uint64_t* CK = (uint64_t*)(smem + sketch_wave_lds(w) * (wv + 1) - 16);
         // bases of this lane's chunk, prefetched one tile ahead; lanes 0-3 also
         // keep the previous tile's last 32 bases (codes | reversed validity << 16)
         uint32_t code16, valid8;
@@ -385,8 +386,8 @@ __global__ __launch_bounds__(256, (!std::is_same<Src, SeqNt4>::value ? SK_WPE_AS
                     if (pn >= (uint32_t)k) { kf = pc & mask; kr = rc; }
                     else {
                         const uint64_t low = (1ULL << (2 * (k - pn))) - 1;
-                        kf = ((ckf << (2 * pn)) | pc) & mask;
-                        kr = (ckr >> (2 * pn)) | (rc & ~low);
+                        kf = ((CK[0] << (2 * pn)) | pc) & mask;
+                        kr = (CK[1] >> (2 * pn)) | (rc & ~low);
                     }
                 } else if (any(slow)) {
                     if (slow) { kf = 0; kr = 0; }
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(256, (!std::is_same<Src, SeqNt4>::value ? SK_WPE_AS
                 rs |= r0;
                 lc = r0 ? 0 : ((in && fl == 2u) ? (lc + 1 < CAP ? lc + 1 : CAP) : lc);
             }
-            ckf = uni64(__shfl((uint64_t)kf2, 63, 64)); ckr = uni64(__shfl((uint64_t)kr2, 63, 64));
+            if (ln == 63) { CK[0] = (uint64_t)kf2; CK[1] = (uint64_t)kr2; }   // read by the next tile (after its wave_lds_sync)
             // ---- segmented scan of l over lanes: (reset, count)
             int32_t er, ec;
             {
