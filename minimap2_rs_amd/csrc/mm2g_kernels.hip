@@ -4186,10 +4186,26 @@ __global__ __launch_bounds__(256) void k_chain_fin(ChainArgs a) {
             const int32_t lo_c = idx - FIN_CH + 1 > 0 ? idx - FIN_CH + 1 : 0;
             for (int32_t t = lo_c + lane; t <= idx; t += 64) spp[t - lo_c] = PP[CK(t, A)];
             wave_lds_sync();
+            // up to 64 links per step: lane l looks at anchor idx - l; while the links are
+            // consecutive (pprev[t] == t - 1, the usual case along a chain) the walk passes
+            // them all at once, and the first other link continues it
             while (idx >= lo_c && cm < A2) {
-                if (lane == 0) CB[cm] = (uint32_t)idx;
-                ++cm; root = idx;
-                idx = uni(spp[idx - lo_c]);
+                const int32_t t = idx - lane;
+                const bool in = t >= lo_c;
+                const int32_t pt = in ? spp[t - lo_c] : -1;
+                const uint64_t nl = ballot(!(in && pt == t - 1));
+                int32_t cnt, nxt;
+                if (nl == 0ULL) { cnt = 64; nxt = idx - 64; }
+                else {
+                    const int32_t m = (int32_t)ctz64(nl);
+                    const bool min_ = idx - m >= lo_c;             // lane m's anchor is staged: it is on the chain
+                    cnt = min_ ? m + 1 : m;
+                    nxt = min_ ? __shfl(pt, m, 64) : idx - m;       // (idx - m = lo_c - 1: restaged below)
+                }
+                cnt = min(cnt, A2 - cm);
+                if (lane < cnt) CB[cm + lane] = (uint32_t)(idx - lane);
+                cm += cnt; root = idx - (cnt - 1);
+                idx = uni(nxt);
             }
             wave_lds_sync();
         }
