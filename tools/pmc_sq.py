@@ -14,7 +14,7 @@ def main():
     n = defaultdict(set)
     with open(sys.argv[1]) as fh:
         for row in csv.DictReader(fh):
-            k = row["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+            k = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
             acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
             n[k].add(row.get("Dispatch_Id", ""))
     out = {"source": "rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS "

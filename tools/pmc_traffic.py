@@ -40,7 +40,7 @@ def per_kernel(path: str, counter: str):
                 continue
             # template instantiations stay apart (k_sketch<true, SeqNt4, false> of the
             # query path vs k_sketch<..., SeqAscii, ...> of the index build)
-            name = row["Kernel_Name"].replace("void ", "", 1).split("(")[0].strip()
+            name = row["Kernel_Name"].replace("void ", "", 1).replace("(anonymous namespace)::", "").split("(")[0].strip()
             acc[name].append(float(row["Counter_Value"]) * 1024.0)
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
