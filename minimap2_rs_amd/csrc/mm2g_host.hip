@@ -1396,14 +1396,15 @@ static int multi_epilogue(mm2g_ctx* c) {
     std::vector<uint64_t> aoff((size_t)n + 1);
     HIPCHK(hipMemcpy(aoff.data(), c->a_off.p, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost));
     const uint64_t A = aoff[n];
-    std::vector<uint64_t> keys(A), xy(2 * A);
-    std::vector<int32_t> f(A), pp(A);
+    // uninitialised host buffers (no zero fill of ~24 B per anchor); the keys are unpacked per read
+    // by the workers below
+    std::vector<uint64_t, DefaultInitAlloc<uint64_t>> keys(A);
+    std::vector<int32_t, DefaultInitAlloc<int32_t>> f(A), pp(A);
     if (A) {
         HIPCHK(hipMemcpy(keys.data(), c->keys.p, A * 8, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(f.data(), c->fbuf.p, A * 4, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(pp.data(), c->ppbuf.p, A * 4, hipMemcpyDeviceToHost));
     }
-    unpack_keys(c->kl, (uint64_t)o.k, keys.data(), (int64_t)A, xy.data());
     // query minimizer positions of the dv sketch (idx.w, idx.k; paf.rs:155-160)
     const SketchBufs& D = c->dv_separate ? c->sk2 : c->sk1;
     std::vector<uint64_t> mb(n);
@@ -1431,6 +1432,7 @@ static int multi_epilogue(mm2g_ctx* c) {
     auto work = [&]() {
     try {
     std::vector<int32_t> mp;
+    std::vector<uint64_t> xy;
     for (;;) {
     const uint32_t b0 = next.fetch_add(64);
     if (b0 >= n) break;
@@ -1440,10 +1442,12 @@ static int multi_epilogue(mm2g_ctx* c) {
         const uint64_t a0 = aoff[i], na = aoff[i + 1] - aoff[i];
         mp.resize(mc[i]);
         for (uint32_t t = 0; t < mc[i]; ++t) mp[t] = (int32_t)(my[mb[i] + t] >> 1);
+        xy.resize(2 * na);
+        unpack_keys(c->kl, (uint64_t)o.k, keys.data() + a0, (int64_t)na, xy.data());
         // avg_k = sum of spans / count in f32 (query spans are all k, non-HPC)
         const float avg_k = mc[i] ? (float)((uint64_t)mc[i] * (uint64_t)kdv) / (float)mc[i] : (float)H.k;
         mm2g::MultiRead& M = c->multi[i];
-        mm2g::multi_chain_read(xy.data() + 2 * a0, f.data() + a0, pp.data() + a0, (int64_t)na, r.qlen, mp.data(), (int64_t)mc[i],
+        mm2g::multi_chain_read(xy.data(), f.data() + a0, pp.data() + a0, (int64_t)na, r.qlen, mp.data(), (int64_t)mc[i],
                                avg_k, kdv, tlen.data(), H.n_seq, P, M);
         const int32_t keep = r.flags & MM2G_R_RESCUED;
         const int32_t qlen = r.qlen, nanc = r.n_anchors;
