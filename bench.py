@@ -365,6 +365,15 @@ def alg_bytes(cnt: dict, res) -> dict:
     na = res["n_anchors"].astype(np.int64)
     mapped = (res["flags"] & 1) != 0
     cm = int(res["cm"][mapped].astype(np.int64).sum())
+    # anchors per sort class as the library dispatched them (counters 18-20): without the
+    # singleton filter (multi-chain output, debug) every read above the small class goes whole
+    # to k_sort_radix and k_sort_read only lists it
+    if "sort_whole_anchors" in cnt:
+        s_small, s_cell, s_whole = cnt["sort_small_anchors"], cnt["sort_cell_anchors"], cnt["sort_whole_anchors"]
+    else:
+        s_small = int(na[(na > 1) & (na <= SORT_SMALL)].sum())
+        s_cell = int(na[(na > SORT_SMALL) & (na <= SORT_CELL_MAX)].sum())
+        s_whole = int(na[na > SORT_CELL_MAX].sum())
     mdv = int(res["m_dv"][mapped].astype(np.int64).sum())
     return {
         "mz_base": 24 * n,
@@ -373,10 +382,10 @@ def alg_bytes(cnt: dict, res) -> dict:
         "filter": 9 * m,                                  # x in, keep flag out
         "seed_count": 9 * m + 16 * mk + 8 * m,            # keep+x in, 16 B table entry per kept, (n, poff) out
         "seed_write": 12 * (m - mf) + 16 * (A - Af),      # (n, poff, y) in; 8 B position in + 8 B key out per anchor
-        "sort_small": 16 * int(na[(na > 1) & (na <= SORT_SMALL)].sum()),
-        "sort_large": 16 * int(na[(na > SORT_SMALL) & (na <= SORT_CELL_MAX)].sum()) + 12 * mf + 8 * Af,
-        "sort_radix": 16 * int(na[na > SORT_CELL_MAX].sum()),
-        "sort_big": 16 * int(na[na > SORT_CELL_MAX].sum()),
+        "sort_small": 16 * s_small,
+        "sort_large": 16 * s_cell + 12 * mf + 8 * Af,
+        "sort_radix": 16 * s_whole,
+        "sort_big": 16 * s_whole,
         "chain_items": 8 * n,
         "chain_lb": 8 * cnt.get("lb_stream_anchors", Adp) + Adp // 8,   # keys in, segment-start bits out
         "chain_cands": Adp // 8 + 12 * n,                        # segment-start bits in (per read: a_off, cnt2, fmin)

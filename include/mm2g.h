@@ -383,9 +383,11 @@ int mm2g_prof_reset(mm2g_ctx* ctx);
  * streams [14] (0 when it did not run: debug, multi-chain or pruning off), and
  * rescued anchors k_chain_seg streams in the rescue pass [15]; the anchors [16]
  * and minimizers [17] of the reads whose keys k_sort_read makes itself (fused
- * seeding: k_seed_write skips them).
+ * seeding: k_seed_write skips them); the anchors of the reads the sort hands
+ * to k_sort_small [18], to k_sort_read's cell path [19] and to the whole-read
+ * kernel (k_sort_big with the singleton filter on, k_sort_radix without) [20].
  * Copies min(n, MM2G_N_COUNTERS) values; returns how many. */
-#define MM2G_N_COUNTERS 18
+#define MM2G_N_COUNTERS 21
 int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus

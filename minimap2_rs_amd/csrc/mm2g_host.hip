@@ -161,6 +161,8 @@ struct mm2g_ctx {
     std::vector<int16_t> h_lut; float lut_gap = -1; int lut_n = 0; bool lut_dirty = true; void* lut_dev = nullptr;
     bool debug = false;
     bool full_last = false;                // the last map kept every anchor (debug mode or multi-chain output)
+    bool filt_last = false;                // the last map's sort ran the singleton-filter cell path
+    uint32_t small_last = 0;               // ... and handed reads of 2..small_last anchors to k_sort_small
     bool multi_last = false;               // ... and its results come from the multi-chain epilogue (-n <= 1, -m <= k)
     std::vector<mm2g::MultiRead> multi;    // per read of the last collected multi-chain batch
     std::vector<mm2g_read_result> h_res;   // per-read results of the last collected batch (mm2g_batch_paf)
@@ -1269,6 +1271,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         if (LW > 2 * nw + 64 + 2048) fuse_mmax = std::min<uint32_t>((LW - 2 * nw - 64 - 2048) / 4, 0xffffu);   // 4 words per minimizer + 4096 u16 owner starts
     }
     sa.fuse_mmax = fuse_mmax; sa.small_max = sort_small_max;
+    c->filt_last = filt; c->small_last = sort_small_max;
     {
         ProfScope ps(c, "seed_write");
         LCHK(launch_seed_write(sa, grid_for(n), c->stream));
@@ -1489,6 +1492,7 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     const HostIndex& H = *c->hidx;
     const int kdv = c->dv_separate ? H.k : c->last_opts.k;
     uint64_t cnt[6] = {c->total_bases, c->h_stat[3], 0, c->n_anchors, 0, 0};
+    uint64_t scls[3] = {0, 0, 0};   // anchors per sort class (counters 18-20, launch_sort_read)
     c->h_res.resize(c->n_reads);
     for (uint32_t i = 0; i < c->n_reads; ++i) {
         const ReadOut& o = c->h_out[i];
@@ -1501,6 +1505,10 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
         r.qlen = (int32_t)L;
         if (L == 0) { r.flags = MM2G_R_EMPTY; continue; }
         r.n_anchors = o.n_anchors;
+        {
+            const uint32_t na = (uint32_t)o.n_anchors;
+            if (na > 1) scls[na <= c->small_last ? 0 : (c->filt_last && na <= 65535u) ? 1 : 2] += na;
+        }
         if (!(o.flags & RF_MAPPED)) continue;
         r.flags = MM2G_R_MAPPED | ((o.flags & RF_RESCUED) ? MM2G_R_RESCUED : 0) | ((o.flags & RF_DV_FOUND) ? MM2G_R_DV_FOUND : 0) |
                   ((o.flags & RF_PANIC) ? MM2G_R_PANIC : 0);
@@ -1537,6 +1545,7 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     c->counters[15] = c->h_stat[6];   // rescued anchors whose keys k_chain_seg streams (pass 1)
     c->counters[16] = c->h_stat[7];   // anchors of the reads k_sort_read seeds itself (fused seeding)
     c->counters[17] = c->h_stat[14];  // ... and their minimizers
+    for (int t = 0; t < 3; ++t) c->counters[18 + t] = scls[t];
     return 0;
 }
 

@@ -110,6 +110,8 @@ def test_sparse_items_taken(dev, small_world, dense_world):
     assert c["dp_anchors"] > 0 and c["seg_stream_anchors"] < c["dp_anchors"], c
     # the batch sums (written by the last chain pass's k_seg_items since round 5)
     assert c["minimizers"] >= c["kept_minimizers"] > 0 and c["anchors"] >= c["dp_anchors"], c
+    # sort classes (counters 18-20): the filter is on, so the cell path takes the reads above the small class
+    assert c["sort_cell_anchors"] > 0 and c["sort_small_anchors"] + c["sort_cell_anchors"] + c["sort_whole_anchors"] <= c["anchors"], c
     with knobs(dev, seg_sparse=0):
         _production_vs_oracle(dev, small_world, dense_world, tag="streamed")
         c = dev.counters()
@@ -125,6 +127,9 @@ def test_wide_gaps_vs_oracle(dev, small_world, dense_world, max_gap, bw_long):
     with knobs(dev, sort_small=1):
         _production_vs_oracle(dev, small_world, dense_world, opts=M.map_opts(max_gap=max_gap, bw_long=bw_long),
                               tag=f"-g {max_gap} -r 500,{bw_long}")
+        c = dev.counters()
+        # no singleton filter: k_sort_read lists every read above the small class for k_sort_radix
+        assert c["sort_cell_anchors"] == 0 and c["sort_whole_anchors"] > 0, c
 
 
 @pytest.mark.parametrize("max_gap,bw,bw_long", [(5000, 500, 200), (300, 500, 400), (300, 2000, 20000)])
