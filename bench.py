@@ -357,10 +357,12 @@ def alg_bytes(cnt: dict, res) -> dict:
     sorts, so k_seed_write is charged only for the other reads, and the sort
     for those reads' minimizer records (12 B) and position fetches (8 B per
     anchor) on top of its 16 B: SURVEY.md §8d's per-anchor position fetch +
-    anchor write + anchor read at 8-B keys."""
+    anchor write + anchor read at 8-B keys.  The same for
+    the reads over 65535 anchors that k_sort_big seeds (counters 21/22)."""
     n = len(res)
     A, m, mk, L = cnt["anchors"], cnt["minimizers"], cnt["kept_minimizers"], cnt["bases"]
     Af, mf = cnt.get("fused_anchors", 0), cnt.get("fused_minimizers", 0)
+    Ab, mb = cnt.get("fused_big_anchors", 0), cnt.get("fused_big_minimizers", 0)   # ... made by k_sort_big
     Adp = cnt.get("dp_anchors", A)
     na = res["n_anchors"].astype(np.int64)
     mapped = (res["flags"] & 1) != 0
@@ -381,11 +383,11 @@ def alg_bytes(cnt: dict, res) -> dict:
         "scan": 24 * n,                                   # two scans: u32 in, u64 out per read
         "filter": 9 * m,                                  # x in, keep flag out
         "seed_count": 9 * m + 16 * mk + 8 * m,            # keep+x in, 16 B table entry per kept, (n, poff) out
-        "seed_write": 12 * (m - mf) + 16 * (A - Af),      # (n, poff, y) in; 8 B position in + 8 B key out per anchor
+        "seed_write": 12 * (m - mf - mb) + 16 * (A - Af - Ab),   # (n, poff, y) in; 8 B position in + 8 B key out per anchor
         "sort_small": 16 * s_small,
         "sort_large": 16 * s_cell + 12 * mf + 8 * Af,
         "sort_radix": 16 * s_whole,
-        "sort_big": 16 * s_whole,
+        "sort_big": 16 * s_whole + 12 * mb + 8 * Ab,
         "chain_items": 8 * n,
         "chain_lb": 8 * cnt.get("lb_stream_anchors", Adp) + Adp // 8,   # keys in, segment-start bits out
         "chain_cands": Adp // 8 + 12 * n,                        # segment-start bits in (per read: a_off, cnt2, fmin)

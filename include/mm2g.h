@@ -351,7 +351,9 @@ enum {
                                     the kept keys to, <= 126; 0 = the per-key scatter to bucket slots [126]   */
     MM2G_KNOB_CANDS_LONGW = 39,  /* k_seg_cands: reads over this many 64-anchor segment-start words are walked
                                     by a whole workgroup instead of one wave; 0 = never [1024]               */
-    MM2G_KNOB_COUNT = 40
+    MM2G_KNOB_SEED_FUSE_BIG = 40, /* reads over 65535 anchors (k_sort_big) get their anchor keys from its first
+                                    pass instead of k_seed_write [1]                                          */
+    MM2G_KNOB_COUNT = 41
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);
@@ -385,9 +387,11 @@ int mm2g_prof_reset(mm2g_ctx* ctx);
  * and minimizers [17] of the reads whose keys k_sort_read makes itself (fused
  * seeding: k_seed_write skips them); the anchors of the reads the sort hands
  * to k_sort_small [18], to k_sort_read's cell path [19] and to the whole-read
- * kernel (k_sort_big with the singleton filter on, k_sort_radix without) [20].
+ * kernel (k_sort_big with the singleton filter on, k_sort_radix without) [20];
+ * the anchors [21] and minimizers [22] of the reads whose keys k_sort_big makes
+ * itself (MM2G_KNOB_SEED_FUSE_BIG).
  * Copies min(n, MM2G_N_COUNTERS) values; returns how many. */
-#define MM2G_N_COUNTERS 21
+#define MM2G_N_COUNTERS 23
 int mm2g_batch_counters(mm2g_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus

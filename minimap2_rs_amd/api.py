@@ -417,7 +417,8 @@ class Device:
         keys = ["bases", "minimizers", "kept_minimizers", "anchors", "rescued_anchors", "dp_pairs", "dp_anchors",
                 "long_anchors", "giant_anchors", "med_anchors", "long_anchors_rescue", "giant_anchors_rescue", "med_anchors_rescue",
                 "seg_stream_anchors", "lb_stream_anchors", "seg_stream_rescue", "fused_anchors", "fused_minimizers",
-                "sort_small_anchors", "sort_cell_anchors", "sort_whole_anchors"]
+                "sort_small_anchors", "sort_cell_anchors", "sort_whole_anchors",
+                "fused_big_anchors", "fused_big_minimizers"]
         buf = (C.c_uint64 * len(keys))()
         check(load().mm2g_batch_counters(self._h, buf, len(keys)), "counters")
         return dict(zip(keys, list(buf)))

@@ -77,7 +77,7 @@ struct ProfSlot { std::string name; double ms = 0; int64_t calls = 0; };
 // in the DP, [5] / [6] of them in reads k_chain_seg streams / k_chain_lb runs
 // on, [8 + 3 pass ..] anchors in long (< / >= giant_min) and medium
 // segments of each DP pass (k_lseg_order)
-constexpr int STAT_WORDS = 16;
+constexpr int STAT_WORDS = 18;
 
 // pinned host staging of one read batch (header + nt4 words), double-buffered
 struct Stage { uint64_t* p = nullptr; uint64_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; };
@@ -110,6 +110,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_SPEC_BATCH: return 4;
     case MM2G_KNOB_DV_PAR: return 1;
     case MM2G_KNOB_SEED_FUSE: return 1;
+    case MM2G_KNOB_SEED_FUSE_BIG: return 1;
     case MM2G_KNOB_SKETCH_X32: return 1;
     case MM2G_KNOB_BIG_WND: return 126;
     case MM2G_KNOB_CANDS_LONGW: return 1024;
@@ -1270,7 +1271,8 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
         const uint32_t LW = sort_read_lds_words(t), nw = (t.cells + 31) / 32;
         if (LW > 2 * nw + 64 + 2048) fuse_mmax = std::min<uint32_t>((LW - 2 * nw - 64 - 2048) / 4, 0xffffu);   // 4 words per minimizer + 4096 u16 owner starts
     }
-    sa.fuse_mmax = fuse_mmax; sa.small_max = sort_small_max;
+    const uint32_t fuse_big = (filt && K[MM2G_KNOB_SEED_FUSE_BIG]) ? 1u : 0u;   // k_sort_big seeds the reads over 65535 anchors
+    sa.fuse_mmax = fuse_mmax; sa.small_max = sort_small_max; sa.fuse_big = fuse_big;
     c->filt_last = filt; c->small_last = sort_small_max;
     {
         ProfScope ps(c, "seed_write");
@@ -1298,6 +1300,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.order = rorder;
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     so.fuse_mmax = fuse_mmax;
+    so.fuse_big = fuse_big; so.a_part = a_part;
     so.big_wnd = (uint32_t)std::max<int64_t>(0, K[MM2G_KNOB_BIG_WND]);
     so.rd_off = c->d_rd_off; so.mz_base = mz_base; so.mz_cnt = mz_cnt; so.mz_y = (const uint32_t*)c->sk1.y.p;
     so.mz_n = mz_n; so.mz_poff = mz_poff; so.ix_pos = (const uint64_t*)c->dix->ix_pos.p; so.kl = kl; so.span = o->k;
@@ -1546,6 +1549,8 @@ int mm2g_batch_results(mm2g_ctx* c, mm2g_read_result* res, uint32_t n) {
     c->counters[16] = c->h_stat[7];   // anchors of the reads k_sort_read seeds itself (fused seeding)
     c->counters[17] = c->h_stat[14];  // ... and their minimizers
     for (int t = 0; t < 3; ++t) c->counters[18 + t] = scls[t];
+    c->counters[21] = c->h_stat[15];  // anchors of the reads k_sort_big seeds itself
+    c->counters[22] = c->h_stat[16];  // ... and their minimizers
     return 0;
 }
 

@@ -148,6 +148,9 @@ struct SeedArgs {
     // fused seeding: reads with small_max < A <= 65535 anchors and at most fuse_mmax minimizers
     // get their keys from k_sort_read's first pass instead (0 = off; SortArgs::fuse_mmax)
     uint32_t fuse_mmax = 0, small_max = 0;
+    // fused seeding of the whole-read sort: reads over 65535 anchors get their keys from k_sort_big's
+    // first pass (SortArgs::fuse_big; 0 = off)
+    uint32_t fuse_big = 0;
 };
 // seed_write splits each read's minimizers into this many contiguous parts
 // (whole 64-minimizer chunks), one wave each; seed_count records where they start
@@ -183,6 +186,10 @@ struct SortArgs {
     const uint64_t* rd_off = nullptr; const uint64_t* mz_base = nullptr; const uint32_t* mz_cnt = nullptr;
     const uint32_t* mz_y = nullptr; const uint32_t* mz_n = nullptr; const uint32_t* mz_poff = nullptr;
     const uint64_t* ix_pos = nullptr; KeyLayout kl{}; int span = 0; uint64_t cap_pos = 0;
+    // fused seeding in k_sort_big (reads over 65535 anchors, k_seed_write skipped them): its first
+    // pass runs k_seed_write's parts, one wave each, from k_seed_count's part starts
+    uint32_t fuse_big = 0;
+    const uint32_t* a_part = nullptr;
 };
 struct ChainArgs {
     uint32_t n;

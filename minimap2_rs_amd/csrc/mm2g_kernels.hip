@@ -986,6 +986,7 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
             const uint64_t A0 = uni64(a.a_off[r + 1]) - obase;
             if (A0 > a.small_max && A0 <= 65535u) continue;
         }
+        if (a.fuse_big && uni64(a.a_off[r + 1]) - obase > 65535u) continue;   // ... k_sort_big's first pass
         const int32_t qlen = (int32_t)(uni64(a.rd_off[r + 1]) - uni64(a.rd_off[r]));
         uint64_t* out = a.keys;
         uint64_t run = part ? (uint64_t)(uint32_t)uni((int32_t)a.a_part[(uint64_t)r * (SEED_PARTS - 1) + part - 1]) : 0;
@@ -2054,6 +2055,78 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
         // ---- P1: seen / seen-twice bitmaps (staged: all cells, then all atomics)
         for (uint32_t i = tid; i < 2 * nw; i += 1024) dyn[i] = 0;
         __syncthreads();
+        if (a.fuse_big && A0 > 65535u) {
+            // fused seeding: k_seed_write skipped this read, so P1 makes its keys (push_anchor,
+            // seeds.rs:62-79) as k_seed_write would: wave w takes part w of the read's 64-minimizer
+            // chunks (k_seed_count's part starts), stages each chunk's offsets above the bitmaps,
+            // gathers the positions, writes the keys to K for P2 / P3 and sets the bitmaps
+            static_assert(SEED_PARTS == 16, "a wave per part, 16 per 1024-thread workgroup");
+            const int wv = wave_id();
+            uint32_t* Wi = dyn + 2 * nw + (uint32_t)wv * 256;   // inclusive offsets, then poff, y, raw n
+            uint32_t* Wp = Wi + 64;
+            uint32_t* Wy = Wp + 64;
+            uint32_t* Wh = Wy + 64;
+            const uint64_t mb = a.mz_base[r];
+            const uint32_t m = a.mz_cnt[r];
+            const uint32_t nch = (m + 63) >> 6;
+            const uint32_t cb = (nch * (uint32_t)wv) / SEED_PARTS, ce = (nch * (uint32_t)(wv + 1)) / SEED_PARTS;
+            const uint32_t cend = ce * 64 < m ? ce * 64 : m;
+            const int32_t qlen = (int32_t)(a.rd_off[r + 1] - a.rd_off[r]);
+            uint32_t run = wv ? a.a_part[(uint64_t)r * (SEED_PARTS - 1) + (uint32_t)wv - 1] : 0u;
+            if (tid == 0 && a.abort) {             // status words 15 / 16: anchors and minimizers seeded here (bench pricing)
+                atomicAdd((unsigned long long*)a.abort + 15, (unsigned long long)A0);
+                atomicAdd((unsigned long long*)a.abort + 16, (unsigned long long)m);
+            }
+            constexpr int U = 8;
+            for (uint32_t c0 = cb * 64; c0 < cend; c0 += 64) {
+                const uint32_t i = c0 + (uint32_t)lane;
+                const bool vi = i < m;
+                const uint32_t nraw = vi ? a.mz_n[mb + i] : 0u;
+                const uint32_t n = ix_count(nraw);
+                uint32_t tot;
+                const uint32_t ex = wave_excl_sum(n, tot);
+                Wi[lane] = ex + n; Wp[lane] = vi ? a.mz_poff[mb + i] : 0u; Wy[lane] = vi ? a.mz_y[mb + i] : 0u; Wh[lane] = nraw;
+                wave_lds_sync();
+                for (uint32_t tb = 0; tb < tot; tb += 64 * U) {
+                    uint64_t x[U];
+                    uint32_t own[U], c[U], old[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t t = tb + (uint32_t)u * 64 + (uint32_t)lane;
+                        x[u] = 0; own[u] = 0;
+                        if (t < tot) {
+                            uint32_t lo = 0;   // owner: the number of inclusive offsets <= t
+#pragma unroll
+                            for (uint32_t step = 32; step >= 1; step >>= 1)
+                                if (Wi[lo + step - 1] <= t) lo += step;
+                            const uint32_t exo = lo ? Wi[lo - 1] : 0u, h = Wh[lo];
+                            own[u] = lo;
+                            x[u] = (h & IX_INLINE) ? ((uint64_t)(h & ~IX_INLINE) << 32) | Wp[lo]   // Single: no gather
+                                                   : a.ix_pos[CK((uint64_t)Wp[lo] + (t - exo), a.cap_pos)];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t t = tb + (uint32_t)u * 64 + (uint32_t)lane;
+                        x[u] = pack_anchor(x[u], Wy[own[u]], qlen, a.span, a.kl);
+                        if (t < tot) K[CK(run + t, A0)] = x[u];
+                        c[u] = cell_of(x[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t t = tb + (uint32_t)u * 64 + (uint32_t)lane;
+                        old[u] = t < tot ? atomicOr(&B1[c[u] >> 5], 1u << (c[u] & 31)) : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t t = tb + (uint32_t)u * 64 + (uint32_t)lane, bit = 1u << (c[u] & 31);
+                        if (t < tot && (old[u] & bit)) atomicOr(&B2[c[u] >> 5], bit);
+                    }
+                }
+                run += tot;
+                wave_lds_sync();
+            }
+        } else
         for (uint32_t i0 = 0; i0 < A0; i0 += 1024 * SORT_U1) {
             uint64_t x[SORT_U1];
             uint32_t c[SORT_U1], old[SORT_U1];

@@ -166,6 +166,13 @@ def test_c5_hg38_100kb(hg38, tmp_path):
                 assert np.array_equal(gf[:n], f) and np.array_equal(gpp[:n].astype(np.int64), pp), r
     # production defaults (the rescue pass pruned by pass 0's bound): PAF and per-read outcome
     _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5prune")
+    # the reads over 65535 anchors were seeded by k_sort_big's first pass (counters 21-22) ...
+    c = dev.counters()
+    assert 0 < c["fused_big_anchors"] <= c["sort_whole_anchors"], c
+    # ... and the same with k_seed_write writing their keys
+    with knobs(dev, seed_fuse_big=0):
+        _map_vs_oracle(dev, idx, oi, mid, rn, seqs, tmp_path, "c5nofuse")
+        assert dev.counters()["fused_big_anchors"] == 0
     # pass 0's 100 kb chains with more speculative rounds per block, 8 predecessors per step,
     # and the long reads' candidate segments found by one wave each (cands_longw=0)
     with knobs(dev, spec_rounds=8, spec_batch=8, cands_longw=0):
