@@ -353,7 +353,12 @@ enum {
                                     by a whole workgroup instead of one wave; 0 = never [1024]               */
     MM2G_KNOB_SEED_FUSE_BIG = 40, /* reads over 65535 anchors (k_sort_big) get their anchor keys from its first
                                     pass instead of k_seed_write [1]                                          */
-    MM2G_KNOB_COUNT = 41
+    MM2G_KNOB_READ_TINY = 41,    /* k_sort_read: cell segments up to this many keys are ranked by a linear scan
+                                    (longer: 64-key chunk sort first), 1..1024 [16]                          */
+    MM2G_KNOB_BIG_TINY = 42,     /* the same for k_sort_big's buckets, 1..2048 [16]                              */
+    MM2G_KNOB_SPEC_EVAL = 43,    /* k_chain_long: a block's next-round guesses are evaluated along the predecessors
+                                    the round chose (pointer doubling) instead of taken as computed [1]        */
+    MM2G_KNOB_COUNT = 44
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

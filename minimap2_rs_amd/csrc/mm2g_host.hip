@@ -111,6 +111,9 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_DV_PAR: return 1;
     case MM2G_KNOB_SEED_FUSE: return 1;
     case MM2G_KNOB_SEED_FUSE_BIG: return 1;
+    case MM2G_KNOB_READ_TINY: return 16;
+    case MM2G_KNOB_BIG_TINY: return 16;
+    case MM2G_KNOB_SPEC_EVAL: return 1;
     case MM2G_KNOB_SKETCH_X32: return 1;
     case MM2G_KNOB_BIG_WND: return 126;
     case MM2G_KNOB_CANDS_LONGW: return 1024;
@@ -948,6 +951,7 @@ static int run_chain(mm2g_ctx* c, uint32_t n, const uint64_t* rd_off, const Chai
     }
     ca.seg_chunk = std::max<uint32_t>(64u, (uint32_t)K[MM2G_KNOB_SEG_CHUNK] & ~63u);
     ca.spec_rounds = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(16, K[MM2G_KNOB_SPEC_ROUNDS]));
+    ca.spec_eval = K[MM2G_KNOB_SPEC_EVAL] ? 1u : 0u;
     ca.spec_batch = K[MM2G_KNOB_SPEC_BATCH] == 8 ? 8u : 4u;
     ca.cands_longw = K[MM2G_KNOB_CANDS_LONGW] > 0 ? (uint32_t)std::min<int64_t>(K[MM2G_KNOB_CANDS_LONGW], 0x7fffffff) : 0x7fffffffu;
     // Giant segments (k_chain_giant): the rescue pass's pseudo-group clusters
@@ -1301,6 +1305,8 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.lds_words = (uint32_t)(std::max<int64_t>(0, K[MM2G_KNOB_SORT_LDS_KB]) * 256);
     so.fuse_mmax = fuse_mmax;
     so.fuse_big = fuse_big; so.a_part = a_part;
+    so.read_tiny = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_READ_TINY], 1024));
+    so.big_tiny = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_BIG_TINY], 2048));
     so.big_wnd = (uint32_t)std::max<int64_t>(0, K[MM2G_KNOB_BIG_WND]);
     so.rd_off = c->d_rd_off; so.mz_base = mz_base; so.mz_cnt = mz_cnt; so.mz_y = (const uint32_t*)c->sk1.y.p;
     so.mz_n = mz_n; so.mz_poff = mz_poff; so.ix_pos = (const uint64_t*)c->dix->ix_pos.p; so.kl = kl; so.span = o->k;

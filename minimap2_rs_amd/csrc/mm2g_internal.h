@@ -190,6 +190,9 @@ struct SortArgs {
     // pass runs k_seed_write's parts, one wave each, from k_seed_count's part starts
     uint32_t fuse_big = 0;
     const uint32_t* a_part = nullptr;
+    // segments up to this many keys are ranked by a linear scan, longer ones chunk-sorted first
+    // (k_sort_read / k_sort_big; MM2G_KNOB_READ_TINY / MM2G_KNOB_BIG_TINY)
+    uint32_t read_tiny = 16, big_tiny = 16;
 };
 struct ChainArgs {
     uint32_t n;
@@ -230,6 +233,7 @@ struct ChainArgs {
     uint32_t giant_gmax;     // global variant: anchors per workgroup scratch slice (0 = off)
     void* giant_scr;         // global variant scratch: grid x giant_gmax x 42 B
     uint32_t spec_rounds = 3; // k_chain_long: speculative rounds per 64-anchor block (MM2G_KNOB_SPEC_ROUNDS)
+    uint32_t spec_eval = 1;   // k_chain_long: next-round guesses evaluated along the round's predecessors (MM2G_KNOB_SPEC_EVAL)
     uint32_t spec_batch = 4;  // k_chain_long: predecessors per step of a speculative round, 4 or 8 (MM2G_KNOB_SPEC_BATCH)
     uint32_t cands_longw = 1024;         // k_seg_cands: reads over this many segment-start words take a whole workgroup
     const uint32_t* mz_cnt = nullptr;    // with bsum: k_seg_items writes bsum[3] = sum mz_cnt, bsum[4] = sum cnt2

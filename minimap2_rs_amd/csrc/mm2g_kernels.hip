@@ -1786,8 +1786,8 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                     seg_of(xa, sa, ea);
                     seg_of(xb, sb, eb);
                     xa = va ? xa : U64MAX; xb = vb ? xb : U64MAX;
-                    const bool na = any(va && ea - sa > SEG_TINY && ea - sa <= a.seg_small);
-                    const bool nb = any(vb && eb - sb > SEG_TINY && eb - sb <= a.seg_small);
+                    const bool na = any(va && ea - sa > a.read_tiny && ea - sa <= a.seg_small);
+                    const bool nb = any(vb && eb - sb > a.read_tiny && eb - sb <= a.seg_small);
                     if (na) { wave_bitonic64_np(xa); if (va) S[ia] = xa; }
                     if (nb) { wave_bitonic64_np(xb); if (vb) S[ib] = xb; }
                 }
@@ -1816,10 +1816,10 @@ __global__ __launch_bounds__(NT) void k_sort_read(SortArgs a) {
                     const uint32_t xl = (uint32_t)x;
                     uint32_t rank = 0;
                     if (pq) {
-                        if (L <= SEG_TINY) ++pc_tiny;
+                        if (L <= a.read_tiny) ++pc_tiny;
                         else if (L > 64) { ++pc_long; pc_srch += ((e - 1) >> 6) - (s >> 6); }
                     }
-                    if (L <= SEG_TINY) {
+                    if (L <= a.read_tiny) {
                         for (uint32_t j = s; j < e; ++j) { const uint32_t y = S32[2 * j]; rank += (y < xl || (y == xl && j < i)) ? 1u : 0u; }
                     } else {
                         const uint32_t co = i >> 6;
@@ -2389,7 +2389,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                 const bool v = i < nwin;
                 uint32_t s0 = 0, e0 = 0;
                 if (v) seg_of(i, s0, e0);
-                if (any(v && e0 - s0 > SEG_TINY && e0 - s0 <= SEG_RANK)) {
+                if (any(v && e0 - s0 > a.big_tiny && e0 - s0 <= SEG_RANK)) {
                     uint64_t x = v ? S[i] : U64MAX;
                     wave_bitonic64_np(x);
                     if (v) S[i] = x;
@@ -2410,7 +2410,7 @@ __global__ __launch_bounds__(1024) void k_sort_big(SortArgs a) {
                     continue;
                 }
                 uint32_t rank = 0;
-                if (L <= SEG_TINY) {
+                if (L <= a.big_tiny) {
                     for (uint32_t j = s0; j < e0; ++j) { const uint64_t y = S[j]; rank += (y < x || (y == x && j < i)) ? 1u : 0u; }
                 } else {
                     const uint32_t co = i >> 6;
@@ -3448,7 +3448,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                 int32_t committed = ib;
                 for (int rnd = 0; rnd < (int)a.spec_rounds && committed < ie; ++rnd) {
                     const bool act0 = kv && k >= committed;
-                    int32_t mf = span, mj = -1, ns = 0, vis = 0;
+                    int32_t mf = span, mj = -1, ns = 0, vis = 0, mfin = 0;   // mfin: the f of mj this round read
                     uint64_t mkm = 0;       // marks t[j] = k by offset d = k - j (bit d-1)
                     bool brk = false;
                     // four predecessors per step: their loads and comput_sc are
@@ -3456,7 +3456,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     // n_skip / marks update is sequential
                     for (int d0 = 1; d0 <= 64; d0 += SB) {
                         if (!any(act0 && !brk && d0 <= dlim)) break;
-                        int32_t sv4[SB], pp4[SB];
+                        int32_t sv4[SB], pp4[SB], fx4[SB];
                         bool ok4[SB];
 #pragma unroll
                         for (int u = 0; u < SB; ++u) {
@@ -3471,7 +3471,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                             ok4[u] = inr && dq > 0 && dq <= maxdx && dr != 0 && dq <= maxdy && dd <= bw;
                             const int32_t dg = dr < dq ? dr : dq;
                             sv4[u] = (span < dg ? span : dg) - (int32_t)lut[ok4[u] ? dd : 0] + fpj.x;
-                            pp4[u] = fpj.y;
+                            pp4[u] = fpj.y; fx4[u] = fpj.x;
                         }
 #pragma unroll
                         for (int u = 0; u < SB; ++u) {
@@ -3479,7 +3479,7 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                             const bool act = act0 && !brk && d <= dlim;
                             vis += act ? 1 : 0;
                             if (act && ok4[u]) {
-                                if (sv4[u] > mf) { mf = sv4[u]; mj = k - d; if (ns > 0) --ns; }
+                                if (sv4[u] > mf) { mf = sv4[u]; mj = k - d; mfin = fx4[u]; if (ns > 0) --ns; }
                                 else if ((mkm >> (d - 1)) & 1ULL) { ++ns; if (ns > P.max_skip) brk = true; }
                                 if (!brk && pp4[u] >= 0) { const int32_t t = k - pp4[u]; if (t <= 64) mkm |= 1ULL << ((t - 1) & 63); }
                             }
@@ -3493,8 +3493,29 @@ __global__ __launch_bounds__(DP_NW * 64) void k_chain_long(ChainArgs a) {
                     const int32_t cend = fb_deep ? fb : (fb < ie ? fb + 1 : ie);     // committed after this round
                     cpairs += (uint64_t)wave_sum((act0 && k < cend) ? (uint32_t)vis : 0u);
                     ++n_steps;
+                    // next guesses of the lanes after fb: by default what they computed (on inputs
+                    // that were guesses).  spec_eval: the f those lanes' chosen predecessors give
+                    // once evaluated along the choices (policy evaluation, pointer doubling over
+                    // the block: f[k] = f[mj] + (mf - the f[mj] this round read), rooted at lane fb,
+                    // at committed anchors and at predecessors before fb).  Any guess keeps the
+                    // commit rule exact; better ones commit more per round.
+                    int32_t gf = mf;
+                    if (a.spec_eval && !fb_deep && fb + 1 < ie) {
+                        const int l = lane;
+                        const bool upd = act0 && k > fb && !deep;
+                        bool done = !(upd && mj >= fb);           // roots: lane fb, chains leaving the unsettled part
+                        int32_t acc = done ? (upd || k == fb ? mf : gv.x) : mf - mfin;
+                        int32_t ptr = done ? l : mj - i0;
+#pragma unroll
+                        for (int it = 0; it < 6; ++it) {
+                            const int32_t pa = __shfl(acc, ptr, 64), pn = __shfl(ptr, ptr, 64);
+                            const bool pd = __shfl((int)done, ptr, 64) != 0;
+                            if (!done) { acc += pa; ptr = pn; done = pd; }
+                        }
+                        gf = acc;
+                    }
                     wave_lds_sync();
-                    if (act0 && k >= fb && !deep) rfp[k & (RK - 1)] = make_int2(mf, mj);   // lane fb exact, later lanes the next guess
+                    if (act0 && k >= fb && !deep) rfp[k & (RK - 1)] = make_int2(k == fb ? mf : gf, mj);   // lane fb exact, later lanes the next guess
                     wave_lds_sync();
                     if (PROF) { pn_spec += (uint64_t)(cend - committed); pn_rounds += 1; }
                     committed = cend;

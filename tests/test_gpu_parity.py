@@ -157,8 +157,9 @@ def test_pipeline_parity(dev, small_world, tmp_path):
     assert _map_nodebug(dev, rnames, rseqs)[0] == got          # production path (singleton filter on)
 
 
-@pytest.mark.parametrize("mid_occ,sr,sb", [(None, 3, 4), (20, 3, 4), (5000, 3, 4), (None, 1, 8), (20, 8, 8), (5000, 16, 8)])
-def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ, sr, sb):
+@pytest.mark.parametrize("mid_occ,sr,sb,se", [(None, 3, 4, 1), (20, 3, 4, 1), (5000, 3, 4, 1), (None, 1, 8, 1), (20, 8, 8, 1),
+                                            (5000, 16, 8, 1), (None, 3, 4, 0), (5000, 3, 4, 0)])
+def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ, sr, sb, se):
     """The production DP shortcuts keep every f/pprev exact: k_chain_long's
     simple paths (no mark source can break the loop; a chain's maximum visited
     early with a break proven inside the first window) and lazy windows, and
@@ -170,8 +171,9 @@ def test_lazy_dp_exact(dev, small_world, dense_world, mid_occ, sr, sb):
     idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
     mid = max(idx.calc_mid_occ(2e-4), 10) if mid_occ is None else mid_occ
     dev.upload_index(idx, mid)
-    # sr / sb: speculative rounds of k_chain_long per 64-anchor block and predecessors per step
-    with knobs(dev, lazy=2, giant_min=64, spec_rounds=sr, spec_batch=sb):
+    # sr / sb: speculative rounds of k_chain_long per 64-anchor block and predecessors per step;
+    # se: next-round guesses evaluated along the round's predecessor choices (1) or taken as computed
+    with knobs(dev, lazy=2, giant_min=64, spec_rounds=sr, spec_batch=sb, spec_eval=se):
         dev.set_debug(True)
         dev.set_reads(rseqs)
         res = dev.map(M.map_opts())
