@@ -1113,7 +1113,7 @@ constexpr int RS_CH = 1024 * RS_ITEMS;
 constexpr int RS_DB = 9;                 // digit bits
 constexpr int RS_ND = 1 << RS_DB;
 constexpr int RS_MAXP = 5;               // digit passes: (group, rpos) has at most 7 + 31 bits
-constexpr uint32_t SEG_TINY = 16;        // segments up to this length: ranked by a scan
+// (segments up to SortArgs::read_tiny / big_tiny keys, 16 by default, are ranked by a linear scan)
 constexpr uint32_t SEG_RANK = 2048;      // up to this: block-wide rank count; beyond: radix
 constexpr int BIG_MAX = 128;             // larger segments listed per read (more: radix over the read)
 constexpr int GOFF_LDS = 256;            // group offsets staged in LDS when 2 * n_seq + 2 fits
