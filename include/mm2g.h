@@ -358,7 +358,9 @@ enum {
     MM2G_KNOB_BIG_TINY = 42,     /* the same for k_sort_big's buckets, 1..2048 [16]                              */
     MM2G_KNOB_SPEC_EVAL = 43,    /* k_chain_long: a block's next-round guesses are evaluated along the predecessors
                                     the round chose (pointer doubling) instead of taken as computed [1]        */
-    MM2G_KNOB_COUNT = 44
+    MM2G_KNOB_SMALL_REG = 44,    /* k_sort_small: reads of 257..4096 anchors are sorted with the keys in registers
+                                    (lane and wave exchanges; LDS only across waves) [1]                     */
+    MM2G_KNOB_COUNT = 45
 };
 int mm2g_ctx_set_knob(mm2g_ctx* ctx, int knob, int64_t value);
 int64_t mm2g_ctx_get_knob(const mm2g_ctx* ctx, int knob);

@@ -65,7 +65,7 @@ class ChainLine(C.Structure):
 KNOBS = {"sort_small": 1, "seg_small": 2, "seg_chunk": 3, "giant_min": 4, "giant_min0": 5, "giant_lcap": 6, "giant_gmax": 7,
          "giant_gblocks": 8, "filter": 9, "lazy": 10, "prune": 11, "giant": 12, "sketch_prof": 13, "sort_prof": 14,
          "lseg_prof": 15, "midhist_bins": 16, "sync_each": 17, "host_threads": 18, "ws_min": 19,
-         "sort_lds_kb": 20, "stop_at": 21, "spec_rounds": 22, "med_pairs": 23, "med_pairs_rescue": 24, "ws_fail": 25, "sketch_view": 27, "prune_rescue": 29, "view_reads": 30, "seg_sparse": 31, "spec_batch": 32, "dv_par": 33, "seed_fuse": 36, "sketch_x32": 37, "big_wnd": 38, "cands_longw": 39, "seed_fuse_big": 40, "read_tiny": 41, "big_tiny": 42, "spec_eval": 43}
+         "sort_lds_kb": 20, "stop_at": 21, "spec_rounds": 22, "med_pairs": 23, "med_pairs_rescue": 24, "ws_fail": 25, "sketch_view": 27, "prune_rescue": 29, "view_reads": 30, "seg_sparse": 31, "spec_batch": 32, "dv_par": 33, "seed_fuse": 36, "sketch_x32": 37, "big_wnd": 38, "cands_longw": 39, "seed_fuse_big": 40, "read_tiny": 41, "big_tiny": 42, "spec_eval": 43, "small_reg": 44}
 INDEX_KNOBS = {"ixchunk": 1, "ixprof": 2, "load_threads": 3, "gpu_strict": 4, "force_fallback": 5, "ixsortv": 6}
 # mm2g_index_origin values
 INDEX_ORIGINS = {1: "host build", 2: "gpu build", 3: "gpu build fell back to the host build", 4: ".mmi load"}

@@ -114,6 +114,7 @@ static int64_t knob_default(int k) {
     case MM2G_KNOB_READ_TINY: return 16;
     case MM2G_KNOB_BIG_TINY: return 16;
     case MM2G_KNOB_SPEC_EVAL: return 1;
+    case MM2G_KNOB_SMALL_REG: return 1;
     case MM2G_KNOB_SKETCH_X32: return 1;
     case MM2G_KNOB_BIG_WND: return 126;
     case MM2G_KNOB_CANDS_LONGW: return 1024;
@@ -1307,6 +1308,7 @@ static int map_enqueue(mm2g_ctx* c, const mm2g_map_opts* o, bool stop_after_sort
     so.fuse_big = fuse_big; so.a_part = a_part;
     so.read_tiny = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_READ_TINY], 1024));
     so.big_tiny = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(K[MM2G_KNOB_BIG_TINY], 2048));
+    so.small_reg = K[MM2G_KNOB_SMALL_REG] ? 1u : 0u;
     so.big_wnd = (uint32_t)std::max<int64_t>(0, K[MM2G_KNOB_BIG_WND]);
     so.rd_off = c->d_rd_off; so.mz_base = mz_base; so.mz_cnt = mz_cnt; so.mz_y = (const uint32_t*)c->sk1.y.p;
     so.mz_n = mz_n; so.mz_poff = mz_poff; so.ix_pos = (const uint64_t*)c->dix->ix_pos.p; so.kl = kl; so.span = o->k;

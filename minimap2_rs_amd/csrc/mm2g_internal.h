@@ -193,6 +193,7 @@ struct SortArgs {
     // segments up to this many keys are ranked by a linear scan, longer ones chunk-sorted first
     // (k_sort_read / k_sort_big; MM2G_KNOB_READ_TINY / MM2G_KNOB_BIG_TINY)
     uint32_t read_tiny = 16, big_tiny = 16;
+    uint32_t small_reg = 1;   // k_sort_small: reads of 257..4096 anchors sorted with the keys in registers (MM2G_KNOB_SMALL_REG)
 };
 struct ChainArgs {
     uint32_t n;

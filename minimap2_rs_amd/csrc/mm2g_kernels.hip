@@ -1042,6 +1042,62 @@ __global__ __launch_bounds__(256) void k_seed_write(SeedArgs a) {
 //   one 1024-thread workgroup per read, stable ranking by wave match.
 // ============================================================================
 constexpr int SORT_SMALL = 4096;
+// Bitonic sort of the 2^LOG keys in s (2^LOG >= 512) by 256 threads with the keys in registers:
+// thread t holds keys t*KPT .. t*KPT+KPT-1.  Stages with j < KPT compare inside a thread, stages
+// with j < 64 KPT exchange with lane t ^ (j / KPT) of the same wave, and only the stages with
+// j >= 64 KPT (three of them) go through LDS with workgroup barriers.  The sorted keys are left in s.
+template <int LOG>
+DEVI void small_sort_reg(uint64_t* s) {
+    constexpr int NP = 1 << LOG, KPT = NP / 256;
+    const int t = threadIdx.x;
+    uint64_t x[KPT];
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) x[r] = s[t * KPT + r];
+#pragma unroll
+    for (int kk = 2; kk <= NP; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j < KPT) {
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) {
+                    if ((r ^ j) > r) {
+                        const bool up = ((t * KPT + r) & kk) == 0;
+                        const uint64_t p = x[r], q = x[r ^ j];
+                        const bool sw = (p > q) == up;
+                        x[r] = sw ? q : p; x[r ^ j] = sw ? p : q;
+                    }
+                }
+            } else if (j < 64 * KPT) {
+                const int m = j / KPT;
+                const bool lowt = (t & m) == 0, up = ((t * KPT) & kk) == 0;
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) {
+                    const uint32_t yl = (uint32_t)__shfl_xor((int)(uint32_t)x[r], m, 64);
+                    const uint32_t yh = (uint32_t)__shfl_xor((int)(uint32_t)(x[r] >> 32), m, 64);
+                    const uint64_t y = ((uint64_t)yh << 32) | yl;
+                    x[r] = (lowt == up) ? (x[r] < y ? x[r] : y) : (x[r] > y ? x[r] : y);
+                }
+            } else {
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) s[t * KPT + r] = x[r];
+                __syncthreads();
+                const int m = j / KPT;
+                const bool lowt = (t & m) == 0, up = ((t * KPT) & kk) == 0;
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) {
+                    const uint64_t y = s[(t ^ m) * KPT + r];
+                    x[r] = (lowt == up) ? (x[r] < y ? x[r] : y) : (x[r] > y ? x[r] : y);
+                }
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) s[t * KPT + r] = x[r];
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) { *a.rcount = 0; if (a.rwork) *a.rwork = 0; }   // k_sort_read's list for k_sort_radix / k_sort_big
     if (a.abort && (*a.abort & BS_ANCHORS)) return;   // anchor workspace too small: the host re-runs the batch
@@ -1058,6 +1114,14 @@ __global__ __launch_bounds__(256) void k_sort_small(SortArgs a) {
     uint64_t* K = a.keys;
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) s[i] = i < A ? K[CK(base + i, a.cap_keys)] : U64MAX;
     __syncthreads();
+    if (np >= 512 && a.small_reg) {   // uniform
+        if (np == 512) small_sort_reg<9>(s);
+        else if (np == 1024) small_sort_reg<10>(s);
+        else if (np == 2048) small_sort_reg<11>(s);
+        else small_sort_reg<12>(s);
+        for (uint32_t i = threadIdx.x; i < A; i += blockDim.x) a.tmp[CK(base + i, a.cap_keys)] = s[i];
+        return;
+    }
     // Thread t (256 threads) exchanges pairs (i, i ^ j) with i = t + 256 u, i < i ^ j.  For
     // j < 64 both elements stay with the same wave from stage to stage, for j >= 256 with the
     // same thread: only the stages j = 64 and 128 move elements between waves and need the

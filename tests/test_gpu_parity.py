@@ -234,22 +234,30 @@ def test_pipeline_parity_dense(dev, dense_world, tmp_path, mid_occ):
     assert dbg_pairs == counts["inner_iters"]
 
 
-def test_anchor_sort_many_shapes(dev, dense_world):
+@pytest.mark.parametrize("small_reg", [1, 0])
+def test_anchor_sort_many_shapes(dev, dense_world, small_reg):
     """Sorted anchors equal the oracle's for reads whose buckets take every
-    path of the per-read sort (single keys, <= 8, <= 64, <= 512, block radix)."""
+    path of the per-read sort (single keys, <= 8, <= 64, <= 512, block radix),
+    with k_sort_small's register bitonic (reads of 257..4096 anchors, 512..4096
+    padded) or its LDS-only network."""
     ref, reads, rnames, rseqs = dense_world
     oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
     idx = M.Index.build_index_from_fasta(ref, 10, 15, 14, 0, 4)
     rng = random.Random(9)
     qs = list(rseqs) + [rseqs[0] * 3, rseqs[8] + rseqs[16], _rand_seq(rng, 20000)]
-    for mid_occ in (10, 100000):
-        dev.upload_index(idx, mid_occ)
-        dev.set_debug(True)
-        dev.set_reads(qs)
-        dev.map(M.map_opts())
-        for r, q in enumerate(qs):
-            want_a, _ = oi.anchors(q, 10, 15, mid_occ)
-            assert np.array_equal(dev.debug_anchors(r), want_a), (mid_occ, r, len(want_a))
+    qs += [rseqs[i][: 300 * (i + 1)] for i in range(12)]          # prefixes: anchor counts across the padded sizes
+    with knobs(dev, small_reg=small_reg):
+        for mid_occ in (10, 100000):
+            dev.upload_index(idx, mid_occ)
+            dev.set_debug(True)
+            dev.set_reads(qs)
+            dev.map(M.map_opts())
+            sizes = set()
+            for r, q in enumerate(qs):
+                want_a, _ = oi.anchors(q, 10, 15, mid_occ)
+                sizes.add(len(want_a))
+                assert np.array_equal(dev.debug_anchors(r), want_a), (mid_occ, r, len(want_a))
+            assert any(256 < n <= 4096 for n in sizes), sorted(sizes)
 
 
 def test_golden_world_gpu(dev, tmp_path):
