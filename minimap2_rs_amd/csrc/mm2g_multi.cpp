@@ -172,6 +172,7 @@ struct Scratch {
     std::vector<int32_t> keys, tpqe, tlen;
     std::vector<uint8_t> is_pri;
     std::vector<uint64_t> seen;
+    std::vector<int32_t> first_qe;
     std::vector<uint32_t> ch;
     std::vector<int32_t> cq;
 };
@@ -376,11 +377,24 @@ void multi_chain_read(const uint64_t* xy, const int32_t* f, const int32_t* pprev
     // test: either that chain became a primary (overlap qe - qs with it) or a primary overlapped it
     // by o >= o*, and the primaries only grow.  Most chains repeat one (one query minimizer hitting
     // many loci), so a hash of the ranges seen settles them before the trees.
+    // Direct coordinates: the qe of the first chain at each qs (a chain's qe is set by its qs
+    // when it is one anchor, the usual repeat); a miss only means the trees decide.
     std::vector<uint64_t>& seen = S.seen;
+    std::vector<int32_t>& first_qe = S.first_qe;
     size_t hcap = 16;
-    while (hcap < 2 * mm) hcap <<= 1;
-    seen.assign(hcap, ~0ULL);
-    auto seen_insert = [&](uint64_t key) -> bool {   // true if already present
+    if (direct) first_qe.assign(K, -1);
+    else {
+        while (hcap < 2 * mm) hcap <<= 1;
+        seen.assign(hcap, ~0ULL);
+    }
+    auto seen_insert = [&](int32_t qs, int32_t qe) -> bool {   // true if (qs, qe) was seen before
+        if (direct) {
+            int32_t& f = first_qe[(size_t)qs];
+            if (f == qe) return true;
+            if (f < 0) f = qe;
+            return false;
+        }
+        const uint64_t key = ((uint64_t)(uint32_t)qs << 32) | (uint32_t)qe;   // never ~0: qs >= 0 fits 31 bits
         size_t h = (size_t)((key * 0x9E3779B97F4A7C15ULL) >> 32) & (hcap - 1);
         for (;; h = (h + 1) & (hcap - 1)) {
             if (seen[h] == key) return true;
@@ -391,8 +405,7 @@ void multi_chain_read(const uint64_t* xy, const int32_t* f, const int32_t* pprev
         const int32_t qs = ord[ci].r.q0(), qe = ord[ci].r.qe;
         const int32_t len = std::max(wsub(qe, qs), 1);
         bool ov = false;
-        const uint64_t rkey = ((uint64_t)(uint32_t)qs << 32) | (uint32_t)qe;   // never ~0: qs >= 0 fits 31 bits
-        if (seen_insert(rkey) && (float)std::max(wsub(qe, qs), 0) / (float)len >= P.mask_level) { is_pri[ci] = 0; continue; }
+        if (seen_insert(qs, qe) && (float)std::max(wsub(qe, qs), 0) / (float)len >= P.mask_level) { is_pri[ci] = 0; continue; }
         const size_t kq = rank(qs);                   // keys <= qs: [0, kq)
         if (n_prim) {
             // the first primary (the best chain) covers most chains: its test alone settles them
