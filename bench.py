@@ -371,7 +371,7 @@ def alg_bytes(cnt: dict, res) -> dict:
     # singleton filter (multi-chain output, debug) every read above the small class goes whole
     # to k_sort_radix and k_sort_read only lists it
     if "sort_whole_anchors" in cnt:
-        s_small, s_cell, s_whole = cnt["sort_small_anchors"], cnt["sort_cell_anchors"], cnt["sort_whole_anchors"]
+        s_small, s_cell, s_whole = (cnt.get(k, 0) for k in ("sort_small_anchors", "sort_cell_anchors", "sort_whole_anchors"))
     else:
         s_small = int(na[(na > 1) & (na <= SORT_SMALL)].sum())
         s_cell = int(na[(na > SORT_SMALL) & (na <= SORT_CELL_MAX)].sum())
