@@ -156,6 +156,7 @@ struct mm2g_ctx {
     uint64_t* h_stat = nullptr;            // pinned copy of dstat (STAT_WORDS u64)
     hipEvent_t ev_done = nullptr;          // end of the queued batch
     ReadOut* h_out = nullptr; size_t h_out_cap = 0;   // pinned
+    unsigned char* h_multi = nullptr; size_t h_multi_cap = 0;   // pinned: the multi-chain epilogue's keys, f, pprev (16 B per anchor)
     bool mapped = false, collected = false, stop_after_sort = false, dv_separate = false;
     bool redo = false;                     // inside wait_batch's re-map (MM2G_KNOB_WS_MIN applies to first maps only)
     bool ws_exact = false;                 // anchor workspace sized to the batches' exact counts (HBM was short)
@@ -471,6 +472,7 @@ void mm2g_ctx_destroy(mm2g_ctx* c) {
     for (auto& S : c->stage) { if (S.p) (void)hipHostFree(S.p); if (S.ev) (void)hipEventDestroy(S.ev); }
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->h_out) (void)hipHostFree(c->h_out);
+    if (c->h_multi) (void)hipHostFree(c->h_multi);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1410,14 +1412,26 @@ static int multi_epilogue(mm2g_ctx* c) {
     std::vector<uint64_t> aoff((size_t)n + 1);
     HIPCHK(hipMemcpy(aoff.data(), c->a_off.p, ((size_t)n + 1) * 8, hipMemcpyDeviceToHost));
     const uint64_t A = aoff[n];
-    // uninitialised host buffers (no zero fill of ~24 B per anchor); the keys are unpacked per read
-    // by the workers below
-    std::vector<uint64_t, DefaultInitAlloc<uint64_t>> keys(A);
-    std::vector<int32_t, DefaultInitAlloc<int32_t>> f(A), pp(A);
+    // keys, f and pprev into the context's pinned buffer (DMA at full PCIe rate, kept across
+    // batches); the keys are unpacked per read by the workers below
+    if (c->h_multi_cap < A * 16) {
+        if (c->h_multi) (void)hipHostFree(c->h_multi);
+        c->h_multi = nullptr; c->h_multi_cap = 0;
+        const size_t want = std::max<size_t>(A * 16 + A * 4, 1 << 20);   // 25 % slack for the next batches
+        if (hipHostMalloc((void**)&c->h_multi, want, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            c->h_multi = nullptr;
+            return set_err(MM2G_E_NOMEM, "multi-chain epilogue: %zu B of pinned host memory", want);
+        }
+        c->h_multi_cap = want;
+    }
+    const uint64_t* keys = (const uint64_t*)c->h_multi;
+    const int32_t* f = (const int32_t*)(c->h_multi + A * 8);
+    const int32_t* pp = (const int32_t*)(c->h_multi + A * 12);
     if (A) {
-        HIPCHK(hipMemcpy(keys.data(), c->keys.p, A * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(f.data(), c->fbuf.p, A * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(pp.data(), c->ppbuf.p, A * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(c->h_multi, c->keys.p, A * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(c->h_multi + A * 8, c->fbuf.p, A * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(c->h_multi + A * 12, c->ppbuf.p, A * 4, hipMemcpyDeviceToHost));
     }
     // query minimizer positions of the dv sketch (idx.w, idx.k; paf.rs:155-160)
     const SketchBufs& D = c->dv_separate ? c->sk2 : c->sk1;
@@ -1457,11 +1471,11 @@ static int multi_epilogue(mm2g_ctx* c) {
         mp.resize(mc[i]);
         for (uint32_t t = 0; t < mc[i]; ++t) mp[t] = (int32_t)(my[mb[i] + t] >> 1);
         xy.resize(2 * na);
-        unpack_keys(c->kl, (uint64_t)o.k, keys.data() + a0, (int64_t)na, xy.data());
+        unpack_keys(c->kl, (uint64_t)o.k, keys + a0, (int64_t)na, xy.data());
         // avg_k = sum of spans / count in f32 (query spans are all k, non-HPC)
         const float avg_k = mc[i] ? (float)((uint64_t)mc[i] * (uint64_t)kdv) / (float)mc[i] : (float)H.k;
         mm2g::MultiRead& M = c->multi[i];
-        mm2g::multi_chain_read(xy.data(), f.data() + a0, pp.data() + a0, (int64_t)na, r.qlen, mp.data(), (int64_t)mc[i],
+        mm2g::multi_chain_read(xy.data(), f + a0, pp + a0, (int64_t)na, r.qlen, mp.data(), (int64_t)mc[i],
                                avg_k, kdv, tlen.data(), H.n_seq, P, M);
         const int32_t keep = r.flags & MM2G_R_RESCUED;
         const int32_t qlen = r.qlen, nanc = r.n_anchors;
