@@ -96,16 +96,20 @@ def parse(argv=None):
                    help="context knob for A/B runs (include/mm2g.h MM2G_KNOB_*), e.g. sort_prof=1")
     p.add_argument("--index-knob", action="append", default=[], metavar="NAME=VALUE",
                    help="process-wide index-build knob (include/mm2g.h MM2G_IKNOB_*), e.g. force_fallback=1")
-    p.add_argument("--streams", type=int, default=4,
-                   help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index "
-                        "(6 is faster over 60 steps, 4 over 10-20: profiles/r05_ab/c3_contexts_*.txt)")
+    p.add_argument("--streams", type=int, default=0,
+                   help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index; "
+                        "0 = 6 for steps of >= 50 Mb (C3: +6.5 %% at 20 and 60 steps in round 6, "
+                        "profiles/r06_ab/c3_streams_*.txt), else 4 (C2's 10 Mb steps)")
     p.add_argument("--shares", type=int, default=2,
                    help="units each batch is cut into (0 = one per stream); contexts pull units from one queue")
     p.add_argument("--min-cnt", type=int, default=3, help="-n (main.rs:45); <= 1 with --min-chain-score <= k: the multi-chain output")
     p.add_argument("--min-chain-score", type=int, default=40, help="-m (main.rs:48)")
     p.add_argument("--iso-batches", type=int, default=3,
                    help="batches mapped by one context after the timed region for the roofline's quiet-GPU launch times")
-    return p.parse_args(argv)
+    args = p.parse_args(argv)
+    if args.streams <= 0:
+        args.streams = 6 if args.reads * args.read_len >= 50_000_000 else 4
+    return args
 
 
 def share_cuts(n: int, s: int):
