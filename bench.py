@@ -96,19 +96,21 @@ def parse(argv=None):
                    help="context knob for A/B runs (include/mm2g.h MM2G_KNOB_*), e.g. sort_prof=1")
     p.add_argument("--index-knob", action="append", default=[], metavar="NAME=VALUE",
                    help="process-wide index-build knob (include/mm2g.h MM2G_IKNOB_*), e.g. force_fallback=1")
-    p.add_argument("--streams", type=int, default=0,
-                   help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index; "
-                        "0 = 6 for steps of >= 50 Mb (C3: +6.5 %% at 20 and 60 steps in round 6, "
-                        "profiles/r06_ab/c3_streams_*.txt), else 4 (C2's 10 Mb steps)")
-    p.add_argument("--shares", type=int, default=2,
-                   help="units each batch is cut into (0 = one per stream); contexts pull units from one queue")
+    p.add_argument("--streams", type=int, default=6,
+                   help="contexts (HIP streams) per GPU, each with its own host thread, sharing one device index "
+                        "(round 6: 6 over 4 by +6.5 %% on C3 at 20 and 60 steps, +4 %% on C2 with one share, "
+                        "even on C5: profiles/r06_ab/*streams*.txt)")
+    p.add_argument("--shares", type=int, default=-1,
+                   help="units each batch is cut into (0 = one per stream); contexts pull units from one queue; "
+                        "-1 = auto: 1 for steps of <= 2000 reads (C2 +50 %%, C5 +9 %% in round 6), else 2 "
+                        "(profiles/r06_ab/shares_*.txt)")
     p.add_argument("--min-cnt", type=int, default=3, help="-n (main.rs:45); <= 1 with --min-chain-score <= k: the multi-chain output")
     p.add_argument("--min-chain-score", type=int, default=40, help="-m (main.rs:48)")
     p.add_argument("--iso-batches", type=int, default=3,
                    help="batches mapped by one context after the timed region for the roofline's quiet-GPU launch times")
     args = p.parse_args(argv)
-    if args.streams <= 0:
-        args.streams = 6 if args.reads * args.read_len >= 50_000_000 else 4
+    if args.shares < 0:
+        args.shares = 1 if args.reads <= 2000 else 2
     return args
 
 
