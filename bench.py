@@ -75,8 +75,8 @@ def log(*a):
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=20)    # the driver's own setting (BENCH_r05 "cmd")
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--reads", type=int, default=10000, help="reads per GPU per step (metric: 10k x 10 kb)")
     p.add_argument("--read-len", type=int, default=10000)
     p.add_argument("--scale", type=float, default=1.0, help="reference size relative to hg38 (1.0 = 3.1 Gb)")

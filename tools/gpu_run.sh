@@ -54,7 +54,7 @@ for S in "${STEPS[@]}"; do
     quick)
       timeout -k 10 400 python -u bench.py $QUIET --steps ${N:-16} $BARGS > "$OUT/quick.json" 2> "$OUT/quick.err"; line "$OUT/quick.json" ;;
     c2)
-      timeout -k 10 400 python -u bench.py --preset ecoli --reads 1000 --steps 10 --warmup 2 --no-cpu $BARGS > "$OUT/c2.json" 2> "$OUT/c2.err"; line "$OUT/c2.json" ;;
+      timeout -k 10 400 python -u bench.py --preset ecoli --reads 1000 --steps 200 --warmup 2 --no-cpu $BARGS > "$OUT/c2.json" 2> "$OUT/c2.err"; line "$OUT/c2.json" ;;
     c5)
       timeout -k 10 600 python -u bench.py --reads 2000 --read-len 100000 --steps 12 --warmup 1 --no-cpu $BARGS > "$OUT/c5.json" 2> "$OUT/c5.err"; line "$OUT/c5.json" ;;
     multi)
