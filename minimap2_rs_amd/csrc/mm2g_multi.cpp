@@ -159,7 +159,6 @@ struct Rng {
 struct Part { uint32_t off, len, next; };
 struct Merged { uint32_t head, tail, n; Rng r; };
 
-
 // per-thread scratch: the epilogue runs once per read on the host_threads pool
 struct Scratch {
     std::vector<Pair> z, items;
@@ -169,7 +168,7 @@ struct Scratch {
     std::vector<Part> parts;
     std::vector<Rng> rng;
     std::vector<Merged> merged, msorted;
-    std::vector<int32_t> keys, tpqe, tlen;
+    std::vector<int32_t> keys, tpqe, tplen;   // select: distinct qs (past 2^20), max-pqe and max-plen trees
     std::vector<uint8_t> is_pri;
     std::vector<uint64_t> seen;
     std::vector<int32_t> first_qe;
@@ -356,7 +355,7 @@ void multi_chain_read(const uint64_t* xy, const int32_t* f, const int32_t* pprev
     size_t T = 1;
     while (T < K) T <<= 1;
     std::vector<int32_t>& tpqe = S.tpqe;
-    std::vector<int32_t>& tl = S.tlen;
+    std::vector<int32_t>& tl = S.tplen;
     tpqe.assign(2 * T, INT32_MIN); tl.assign(2 * T, INT32_MIN);
     auto upd = [&](std::vector<int32_t>& tr, size_t pos, int32_t v) {
         for (size_t x = pos + T; x >= 1; x >>= 1) { if (tr[x] >= v) break; tr[x] = v; }
