@@ -31,8 +31,11 @@ def _paf_line(name, qlen, ln, tnames, tlens):
             f"s1:i:{max(ln.s1, 0)}\ts2:i:{max(ln.s2, 0)}\tdv:f:{dv:.4f}\trl:i:0")
 
 
-@pytest.mark.parametrize("mc,m,best_n", [(1, 15, 5), (0, 0, 5), (-1, 8, 2), (1, 1, 5)])
-def test_multi_chain_host_vs_oracle(world, mc, m, best_n):
+@pytest.mark.parametrize("mc,m,best_n,mask,pri", [(1, 15, 5, 0.5, 0.8), (0, 0, 5, 0.5, 0.8), (-1, 8, 2, 0.5, 0.8), (1, 1, 5, 0.5, 0.8),
+                                                  (1, 15, 50, 0.1, 0.5), (1, 15, 50, 0.9, 0.0), (1, 15, 5, 1.0, 0.8), (1, 15, 20, 0.0, 0.3)])
+def test_multi_chain_host_vs_oracle(world, mc, m, best_n, mask, pri):
+    """-M (mask_level) and -p (pri_ratio) across their range exercise the primary test's
+    overlap threshold, its range memo and both segment trees (mm2g_multi.cpp)."""
     ref, reads, td = world
     oi = O.OIndex.build(ref, 10, 15, 14, 0, 4)
     mid = max(oi.mid_occ(2e-4), 10)
@@ -40,12 +43,12 @@ def test_multi_chain_host_vs_oracle(world, mc, m, best_n):
     targets = O.read_fasta(ref)
     tnames = [t[0] for t in targets]
     tlens = np.array([len(t[1]) for t in targets], dtype=np.uint32)
-    want_path = str(td / f"want_{mc}_{m}_{best_n}.paf")
-    oi.align_fasta(reads, want_path, min_cnt=mc, min_chain_score=m, best_n=best_n, mid_occ=mid)
+    want_path = str(td / f"want_{mc}_{m}_{best_n}_{mask}_{pri}.paf")
+    oi.align_fasta(reads, want_path, min_cnt=mc, min_chain_score=m, best_n=best_n, mid_occ=mid, mask_level=mask, pri_ratio=pri)
     want = {}
     for ln in open(want_path).read().splitlines():
         want.setdefault(ln.split("\t")[0], []).append(ln)
-    opts = M.map_opts(min_cnt=mc, min_chain_score=m, best_n=best_n)
+    opts = M.map_opts(min_cnt=mc, min_chain_score=m, best_n=best_n, mask_level=mask, pri_ratio=pri)
     n_lines = n_panic = 0
     for name, q in recs:
         xy, _ = oi.anchors(q, 10, 15, mid)
